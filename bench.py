@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""bench.py — Gray-code subset-steps/s of the exact Ryser permanent on MI355X.
+
+Workload (BASELINE.json configs[3], the metric's config): the reference corpus
+matrix double/40_0.50_0 (n = 40, d = 0.5), dense walk (-p4/-p6 path), all
+2^39 Gray steps per "step".  With N ranks (one process per GPU, launched by
+torch.distributed.run) the 2^h wave-chunks are split into N contiguous
+power-of-two-aligned shards; each rank walks its shard through the C ABI
+(sup_partial) and one RCCL all-reduce (torch.distributed, backend nccl)
+sums the fp64 partials — the only data-path collective.  Weak per-job
+scaling is NOT used: total work per step is fixed (the permanent), so
+scaling is "strong".
+
+Prints ONE JSON line on rank 0 (driver contract), including the roofline of
+the walk kernel (hipEvents on its own stream, measured inside the library)
+and a CPU baseline (oracle/ port of the reference's parallel_perman64 chunk
+loop, timed on a bounded sample of the same workload on this host's cores).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Gray-code subset-steps/sec (dense n=40, d=0.5) at 1/2/4/8 MI355X; rel-err vs CPU"
+FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 (vector = matrix), MI355X_MICROARCH.md / SURVEY §8(d)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--matrix", default=os.path.join(ROOT, "tests", "fixtures", "double__40_0.50_0"))
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
+    return ap.parse_args()
+
+
+def pmc_traffic(n: int):
+    """HBM bytes per walk launch from the committed rocprofv3 PMC summary, if any."""
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(p))
+            if d.get("n") == n and "hbm_bytes_per_launch" in d:
+                return d["hbm_bytes_per_launch"]
+        except Exception:
+            pass
+    return None
+
+
+def cpu_baseline(a, n: int, budget_s: float, gpu_sup):
+    """Reference algorithm (oracle port of cpu_perman64, gpu_exact_dense.cu:6-69)
+    on an aligned sample [2^(n-2), 2^(n-2)+S) of the same workload, all host
+    threads; also the GPU on the same sample for the relative error."""
+    import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    s0 = 1 << (n - 2)
+    probe = 1 << 24
+    t = time.perf_counter()
+    oracle.ref_dense_partial(a, s0, s0 + probe, threads)
+    dt = max(time.perf_counter() - t, 1e-3)
+    rate = probe / dt
+    k = max(20, min(n - 2, int((rate * budget_s)).bit_length() - 1))
+    size = 1 << k
+    t = time.perf_counter()
+    cpu = oracle.ref_dense_partial(a, s0, s0 + size, threads)
+    dt = time.perf_counter() - t
+    gpu = gpu_sup.partial(a, s0, s0 + size)
+    err = abs(gpu - cpu) / max(abs(cpu), 1e-300)
+    return {"value": size / dt, "unit": "gray-steps/s", "cores": threads, "kind": "port",
+            "sample": f"reference Gray indices [2^{n-2}, 2^{n-2}+2^{k}) of {os.path.basename(args.matrix)} "
+                      f"({dt:.1f} s, oracle/oracle.c orc_ref_dense_partial = cpu_perman64 restated)"}, err
+
+
+def main():
+    global args
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import superman_amd as S
+
+    a, typ, _ = S.read_matrix(args.matrix)
+    n = a.shape[0]
+    L, m, h = S.layout(n)
+    C = 1 << h
+    c0, c1 = C * rank // world, C * (rank + 1) // world
+    cb = L + m
+    start, end = c0 << cb, c1 << cb
+    my_steps = end - start
+    dev = local
+
+    def step():
+        part, st = S.partial(a, start, end, device_id=dev, return_stats=True)
+        if world > 1:
+            t = torch.tensor([part], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(t)  # RCCL over xGMI: the single data-path collective
+            part = float(t.item())
+        return (4 * (n & 1) - 2) * part, st
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    kms, perm = [], None
+    for _ in range(args.steps):
+        perm, st = step()
+        kms.append(st["kernel_ms"])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_steps = args.steps * (1 << (n - 1))
+    value = total_steps / elapsed
+    k_ms = sum(kms) / len(kms)
+    flops = 2.0 * n * my_steps  # n fp64 adds + n fp64 muls per Gray step
+    achieved = flops / (k_ms * 1e-3) / 1e12
+    traffic = pmc_traffic(n)
+    rec = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "gray-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "reference corpus matrix double/40_0.50_0 (tests/fixtures/double__40_0.50_0)",
+        "config": {"workload": "dense Ryser/Gray-code exact permanent, n=40 d=0.50 (double/40_0.50_0), "
+                               "2^39 Gray steps per step",
+                   "n": n, "density": 0.5, "gray_steps_per_step": 1 << (n - 1),
+                   "parallelism": f"dp{world}: contiguous wave-chunk shards + one RCCL all-reduce"},
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "kernel": f"sup::walk_dense<{n}>", "kernel_ms_avg": k_ms,
+                     "algorithmic_flops_per_launch": flops},
+        "permanent": perm,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cb_rec, err = cpu_baseline(a, n, args.cpu_seconds, S)
+        rec["cpu_baseline"] = cb_rec
+        rec["rel_err_vs_cpu"] = err
+    else:
+        rec["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

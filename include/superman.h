@@ -1,0 +1,206 @@
+/*
+ * superman.h — C ABI of the MI355X-native Ryser / Gray-code permanent engine.
+ *
+ * This is the drop-in boundary for the reference's GPU exact-permanent path
+ * (kamerkaya/SUPerman, v1 top level).  Every entry point below names the
+ * reference symbol it replaces (file:line in the reference tree).  The
+ * reference's wrappers are C++ templates over the storage type T in
+ * {int, float, double}; here T travels as a `sup_dtype` tag next to a
+ * `const void*`, so the ABI is plain C (pointers, sizes, an error code).
+ *
+ * Conventions (reference behaviour kept, reference defects fixed):
+ *   - Host arrays are borrowed read-only; the caller owns them
+ *     (reference: main.cu:501-528 new[]/delete[] around RunAlgo).
+ *   - Device memory is owned by the library (per-device context, created on
+ *     first use, reused across calls).
+ *   - Every function returns 0 (SUP_OK) or a negative SUP_E* code; the
+ *     message is available from sup_last_error() (thread-local).  The
+ *     reference reports nothing (no cudaGetLastError anywhere).
+ *   - The permanent is written through `out` as a double
+ *     (reference returns it by value; interface_connector.c:22 truncated it
+ *     to int — not reproduced).
+ *   - X is always fp64 (the reference v1 float-X path, algo.h:664 /
+ *     gpu_exact_dense.cu:336, is numerically wrong on real matrices and is
+ *     not reproduced).
+ *   - Device 0 is the default device (the reference hard-codes
+ *     cudaSetDevice(1), gpu_exact_dense.cu:664); `sup_opts.device_id`
+ *     selects another one (v2 flag -l, revised_perman/main.cpp:1443).
+ */
+#ifndef SUPERMAN_H
+#define SUPERMAN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SUP_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------ */
+#define SUP_OK            0
+#define SUP_EINVAL      (-1)   /* bad argument (n out of range, null pointer, bad range) */
+#define SUP_ENODEV      (-2)   /* no HIP device / device id out of range                 */
+#define SUP_EHIP        (-3)   /* a HIP runtime call failed                              */
+#define SUP_ERCCL       (-4)   /* an RCCL call failed                                    */
+#define SUP_ENOMEM      (-5)   /* host or device allocation failed                       */
+#define SUP_EIO         (-6)   /* matrix file could not be read                          */
+#define SUP_EUNSUPPORTED (-7)  /* algorithm id / option combination not provided         */
+
+#define SUP_MAX_N 64           /* 64-bit Gray index: reference limit algo.h:752,781      */
+
+/* ---- storage type of the input matrix (reference template parameter T) -- */
+typedef enum {
+  SUP_INT32 = 0,    /* file header "int"    (main.cu:494) */
+  SUP_FLOAT32 = 1,  /* file header "float"  (main.cu:530) */
+  SUP_FLOAT64 = 2   /* file header "double" (main.cu:563) */
+} sup_dtype;
+
+/* ---- kernel family ------------------------------------------------------ */
+typedef enum {
+  SUP_KERNEL_DENSE = 0,     /* kernel_xshared_coalescing_mshared          gpu_exact_dense.cu:329-399  */
+  SUP_KERNEL_SPARYSER = 1,  /* kernel_xshared_coalescing_mshared_sparse   gpu_exact_sparse.cu:455-552 */
+  SUP_KERNEL_SKIPPER = 2    /* kernel_xshared_coalescing_mshared_skipper  gpu_exact_sparse.cu:555-670 */
+} sup_kernel;
+
+/* ---- multi-device scheduling policy -------------------------------------- */
+typedef enum {
+  SUP_SCHED_SINGLE = 0,   /* one device           (-p4; gpu_exact_dense.cu:640-699)            */
+  SUP_SCHED_STATIC = 1,   /* static split         (-p5; gpu_exact_dense.cu:701-774)            */
+  SUP_SCHED_CHUNKS = 2    /* dynamic chunk queue  (-p6/-p8; gpu_exact_dense.cu:776-904,
+                                                   gpu_exact_sparse.cu:1192-1324)            */
+} sup_sched;
+
+typedef struct {
+  int gpu_num;        /* devices to use (-d); default 1                                      */
+  int device_id;      /* first device (v2 -l); default 0                                     */
+  int threads;        /* host threads for the CPU worker (-t); default 16 (main.cu:333)      */
+  int cpu_worker;     /* -c together with -g: a CPU thread also takes chunks                 */
+  int grid_dim;       /* 0 = auto (resident-wave sized); reference default 2048              */
+  int block_dim;      /* 0 = auto (256); the engine only supports 256                         */
+  int walk_log2;      /* 0 = auto; Gray steps walked per wave-chunk = 2^walk_log2            */
+  int chunk_log2;     /* 0 = auto; for SUP_SCHED_CHUNKS: wave-chunks per queue item = 2^x    */
+  int use_rccl;       /* multi-device: combine per-device partials with one RCCL all-reduce  */
+  int verbose;        /* print per-device / per-chunk timing lines like the reference        */
+} sup_opts;
+
+typedef struct {
+  double   kernel_ms;       /* device time of the walk kernels (max over devices, hipEvents)   */
+  double   wall_ms;         /* host wall time of the call (upload + launch + reduce)           */
+  uint64_t gray_steps;      /* nominal Gray steps = 2^(n-1)                                    */
+  uint64_t visited_steps;   /* steps whose product was actually evaluated (sparse/skipper)     */
+  int      devices_used;
+  int      lane_bits;       /* L: Gray bits spread over the 64 lanes of a wave                  */
+  int      walk_bits;       /* m: Gray bits walked by every wave-chunk                          */
+  int      grid;            /* blocks per launch (256 threads each) on each device             */
+  int      chunks_done_cpu; /* queue items taken by the CPU worker                              */
+  double   partials[16];    /* per-device partial sums (before the final combine)              */
+} sup_stats;
+
+/* Fill `o` with defaults. */
+void sup_opts_init(sup_opts* o);
+
+/* Library metadata. */
+int         sup_abi_version(void);
+const char* sup_last_error(void);     /* thread-local message of the last failing call */
+int         sup_device_count(int* count);
+
+/* ------------------------------------------------------------------------ *
+ * Generic entry point.  `mat` is n x n row-major of type `t` (already
+ * preprocessed by the caller when the reference would have rewritten it:
+ * SortOrder / SkipOrder, util.h:553-684).  `kernel` picks the Gray walk,
+ * `sched` the device policy.  Result: the permanent, fp64.
+ * Replaces RunAlgo<T>'s GPU exact branch (main.cu:30-143).
+ * ------------------------------------------------------------------------ */
+int sup_perman(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched sched,
+               const sup_opts* o, double* out, sup_stats* st);
+
+/* Partial Ryser sum over reference Gray indices [start, end):
+ *   sum_{i in [start,end)} (-1)^i * prod_j x_j(gray(i))
+ * with x(0) = Nijenhuis-Wilf start vector (gpu_exact_dense.cu:642-652).
+ * This is exactly what the reference chunk helpers return
+ * (cpu_perman64 gpu_exact_dense.cu:6-69; cpu_perman64_sparse
+ * gpu_exact_sparse.cu:6-87; cpu_perman64_skipper :89-191) except that index
+ * 0 (the p0 term) is included when start == 0.  start and end must be
+ * multiples of 2^(lane_bits + walk_bits) reported by the engine for this n
+ * (any power-of-two aligned chunk boundary >= 64 works), or end == 2^(n-1). */
+int sup_partial(const void* mat, sup_dtype t, int n, sup_kernel kernel,
+                uint64_t start, uint64_t end, const sup_opts* o, double* out, sup_stats* st);
+
+/* Explicit CPU algorithm for the CLI's `-c` mode (reference RunAlgo cpu
+ * branch, main.cu:186-238): the same wave-chunk walk on `threads` host
+ * threads, bit-identical to the GPU kernels.  Never used as a fallback by the
+ * GPU entry points above, which fail with SUP_ENODEV without a device. */
+int sup_perman_cpu(const void* mat, sup_dtype t, int n, sup_kernel kernel, int threads,
+                   double* out, sup_stats* st);
+
+/* Nijenhuis-Wilf prologue (gpu_exact_dense.cu:642-652): x0[j] = a[j][n-1] - rowsum_j/2,
+ * p0 = prod x0.  Host-only helper, exported for the test harness. */
+int sup_nw_start(const void* mat, sup_dtype t, int n, double* x0, double* p0);
+
+/* ------------------------------------------------------------------------ *
+ * Reference-signature wrappers: one per GPU exact wrapper of the v1 tree.
+ * Arguments keep the reference meaning; grid_dim/block_dim are accepted for
+ * signature compatibility (the engine sizes its own launch when they are <= 0
+ * or when they do not match its 256-thread wave-chunk layout).
+ * ------------------------------------------------------------------------ */
+
+/* gpu_exact_dense.cu:641 gpu_perman64_xshared_coalescing_mshared (-p4) */
+int sup_gpu_perman64_xshared_coalescing_mshared(const void* mat, sup_dtype t, int nov,
+    int grid_dim, int block_dim, double* out);
+/* gpu_exact_dense.cu:702 ..._multigpu (-p5) */
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpu(const void* mat, sup_dtype t, int nov,
+    int gpu_num, int grid_dim, int block_dim, double* out);
+/* gpu_exact_dense.cu:777 ..._multigpucpu_chunks (-p6) */
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks(const void* mat, sup_dtype t,
+    int nov, int gpu_num, int cpu, int threads, int grid_dim, int block_dim, double* out);
+/* gpu_exact_sparse.cu:854 ..._sparse (-p4 -s) */
+int sup_gpu_perman64_xshared_coalescing_mshared_sparse(const void* mat, const int* cptrs,
+    const int* rows, const void* cvals, sup_dtype t, int nov, int grid_dim, int block_dim,
+    double* out);
+/* gpu_exact_sparse.cu:917 ..._multigpu_sparse (-p5 -s) */
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpu_sparse(const void* mat, const int* cptrs,
+    const int* rows, const void* cvals, sup_dtype t, int nov, int gpu_num, int grid_dim,
+    int block_dim, double* out);
+/* gpu_exact_sparse.cu:996 ..._multigpucpu_chunks_sparse (-p6 -s) */
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_sparse(const void* mat,
+    const int* cptrs, const int* rows, const void* cvals, sup_dtype t, int nov, int gpu_num,
+    int cpu, int threads, int grid_dim, int block_dim, double* out);
+/* gpu_exact_sparse.cu:1124 ..._skipper (-p7 -s) */
+int sup_gpu_perman64_xshared_coalescing_mshared_skipper(const void* mat, const int* rptrs,
+    const int* cols, const int* cptrs, const int* rows, const void* cvals, sup_dtype t, int nov,
+    int grid_dim, int block_dim, double* out);
+/* gpu_exact_sparse.cu:1193 ..._multigpucpu_chunks_skipper (-p8 -s) */
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper(const void* mat,
+    const int* rptrs, const int* cols, const int* cptrs, const int* rows, const void* cvals,
+    sup_dtype t, int nov, int gpu_num, int cpu, int threads, int grid_dim, int block_dim,
+    double* out);
+
+/* ------------------------------------------------------------------------ *
+ * Host preprocessing (hot-path inputs).
+ * ------------------------------------------------------------------------ */
+
+/* v1 matrix file: header "n nnz type", then 0-based "i j v" lines; malformed
+ * lines skipped; binary => every listed entry is 1 (util.h:343-358,
+ * main.cu:494-498).  *mat is allocated with malloc (free with sup_free). */
+int sup_read_matrix(const char* path, int binary, void** mat, sup_dtype* t, int* n, int* nnz_header);
+void sup_free(void* p);
+
+/* CSR + CSC of a dense row-major matrix; nonzero test is != 0 (the reference
+ * uses > 0 at util.h:537,542 and silently drops negative entries).  Arrays
+ * are caller-allocated: cptrs/rptrs n+1, rows/cols/vals nnz (query nnz with
+ * sup_count_nnz).  (util.h:522-551) */
+int sup_count_nnz(const void* mat, sup_dtype t, int n, int* nnz);
+int sup_compress(const void* mat, sup_dtype t, int n, int* cptrs, int* rows, void* cvals,
+                 int* rptrs, int* cols, void* rvals);
+/* SortOrder: stable ascending column nnz; rewrites mat in place and fills
+ * colperm (new column c = old column colperm[c]).  (util.h:553-619) */
+int sup_sort_order(void* mat, sup_dtype t, int n, int* colperm);
+/* SkipOrder: greedy min-degree column order, rows in first-touch order;
+ * rewrites mat in place.  (util.h:621-684) */
+int sup_skip_order(void* mat, sup_dtype t, int n, int* rowperm, int* colperm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SUPERMAN_H */

@@ -1,0 +1,654 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE ONLY (parity checker, never shipped).
+ *
+ * CPU restatement of kamerkaya/SUPerman's Ryser / Gray-code exact permanent
+ * algorithms, written from the reference's behaviour (file:line cited per
+ * function).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the
+ * reported CPU baseline.  The product (superman_amd/) never links or calls it.
+ *
+ * Pinning: the orc_ref_* functions are checked against golden vectors produced
+ * by the reference's own CPU code compiled from /root/reference sources
+ * (oracle/Makefile target `ref`, outputs in oracle/_ref/, vectors committed in
+ * tests/golden/ by tests/golden/make_golden.py) and against exact big-integer
+ * Ryser for small n (tests/exact.py).
+ *
+ * Deviations from the reference, all deliberate:
+ *   - per-thread / per-chunk partials are combined in thread (chunk) order, not
+ *     in `omp critical` completion order, so results are deterministic;
+ *   - X is fp64 everywhere (v1's float X, algo.h:664, is wrong on reals);
+ *   - sparse structure uses `!= 0` (v1 util.h:537 keeps only `> 0`).
+ */
+#include <math.h>
+#include <omp.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_MAXN 64
+
+/* gpu_exact_dense.cu:642-652 / cpu_algos.hpp:801-808 */
+void orc_nw_start(const double* a, int n, double* x0, double* p0) {
+  double p = 1.0;
+  for (int j = 0; j < n; ++j) {
+    double rs = 0.0;
+    for (int k = 0; k < n; ++k) rs += a[j * n + k];
+    x0[j] = a[j * n + (n - 1)] - rs / 2;
+    p *= x0[j];
+  }
+  *p0 = p;
+}
+
+static void transpose(const double* a, int n, double* t) {
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) t[i * n + j] = a[j * n + i];
+}
+
+/* One thread's share of the dense Gray walk over [my_start, my_end):
+ * gpu_exact_dense.cu:26-62 (cpu_perman64 body) == cpu_algos.hpp:831-866. */
+static double dense_range(const double* mat_t, const double* x0, int n, long long my_start, long long my_end) {
+  double x[ORC_MAXN];
+  memcpy(x, x0, sizeof(double) * n);
+  long long i = my_start;
+  long long gray = (i - 1) ^ ((i - 1) >> 1);
+  for (int k = 0; k < n - 1; ++k)
+    if ((gray >> k) & 1LL)
+      for (int j = 0; j < n; ++j) x[j] += mat_t[k * n + j];
+  double my_p = 0;
+  int prodSign = (i & 1LL) ? -1 : 1;
+  while (i < my_end) {
+    int k = __builtin_ctzll(i);
+    gray ^= (1LL << k);
+    double s = ((1LL << k) & gray) ? 1.0 : -1.0;
+    double prod = 1.0;
+    for (int j = 0; j < n; ++j) {
+      x[j] += s * mat_t[k * n + j];
+      prod *= x[j];
+    }
+    my_p += prodSign * prod;
+    prodSign *= -1;
+    i++;
+  }
+  return my_p;
+}
+
+/* cpu_algos.hpp:761-873 parallel_perman64<double,double>:
+ * chunk_size = end/threads + 1, thread t walks [1 + t*cs, min(1+(t+1)*cs, end)). */
+double orc_ref_dense(const double* a, int n, int threads) {
+  double x0[ORC_MAXN], p;
+  orc_nw_start(a, n, x0, &p);
+  double* mat_t = (double*)malloc(sizeof(double) * n * n);
+  transpose(a, n, mat_t);
+  const long long start = 1, end = 1LL << (n - 1);
+  const long long cs = end / threads + 1;
+  double* part = (double*)calloc(threads, sizeof(double));
+#pragma omp parallel for num_threads(threads) schedule(static, 1)
+  for (int tid = 0; tid < threads; ++tid) {
+    long long ms = start + tid * cs;
+    long long me = start + (tid + 1) * cs;
+    if (me > end) me = end;
+    part[tid] = dense_range(mat_t, x0, n, ms, me);
+  }
+  for (int tid = 0; tid < threads; ++tid) p += part[tid];
+  free(part);
+  free(mat_t);
+  return (4 * (n & 1) - 2) * p;
+}
+
+/* gpu_exact_dense.cu:6-69 cpu_perman64: partial over [start, end) with
+ * chunk_size = (end-start)/threads + 1 (no p0, no final factor). */
+double orc_ref_dense_partial(const double* a, int n, long long start, long long end, int threads) {
+  double x0[ORC_MAXN], p0;
+  orc_nw_start(a, n, x0, &p0);
+  double* mat_t = (double*)malloc(sizeof(double) * n * n);
+  transpose(a, n, mat_t);
+  const long long cs = (end - start) / threads + 1;
+  double* part = (double*)calloc(threads, sizeof(double));
+#pragma omp parallel for num_threads(threads) schedule(static, 1)
+  for (int tid = 0; tid < threads; ++tid) {
+    long long ms = start + tid * cs;
+    long long me = start + (tid + 1) * cs;
+    if (me > end) me = end;
+    part[tid] = dense_range(mat_t, x0, n, ms, me);
+  }
+  double p = 0.0;
+  for (int tid = 0; tid < threads; ++tid) p += part[tid];
+  free(part);
+  free(mat_t);
+  return p;
+}
+
+/* ------------------------------------------------------------------ sparse */
+typedef struct {
+  int n, nnz;
+  int cptrs[ORC_MAXN + 1], rptrs[ORC_MAXN + 1];
+  int rows[ORC_MAXN * ORC_MAXN], cols[ORC_MAXN * ORC_MAXN];
+  double cvals[ORC_MAXN * ORC_MAXN], rvals[ORC_MAXN * ORC_MAXN];
+} csx;
+
+/* util.h:522-551 matrix2compressed (!= 0) */
+static void compress(const double* a, int n, csx* s) {
+  int er = 0, ec = 0;
+  s->n = n;
+  for (int i = 0; i < n; ++i) {
+    s->rptrs[i] = er;
+    s->cptrs[i] = ec;
+    for (int j = 0; j < n; ++j) {
+      if (a[i * n + j] != 0) {
+        s->cols[er] = j;
+        s->rvals[er++] = a[i * n + j];
+      }
+      if (a[j * n + i] != 0) {
+        s->rows[ec] = j;
+        s->cvals[ec++] = a[j * n + i];
+      }
+    }
+  }
+  s->rptrs[n] = er;
+  s->cptrs[n] = ec;
+  s->nnz = er;
+}
+
+/* cpu_algos.hpp:682-749 (per-thread body) == gpu_exact_sparse.cu:14-80 */
+static double sparse_range(const csx* s, const double* x0, int n, long long my_start, long long my_end) {
+  double x[ORC_MAXN];
+  memcpy(x, x0, sizeof(double) * n);
+  long long i = my_start;
+  long long gray = (i - 1) ^ ((i - 1) >> 1);
+  for (int k = 0; k < n - 1; ++k)
+    if ((gray >> k) & 1LL)
+      for (int j = s->cptrs[k]; j < s->cptrs[k + 1]; ++j) x[s->rows[j]] += s->cvals[j];
+  double prod = 1.0;
+  int zero_num = 0;
+  for (int j = 0; j < n; ++j) {
+    if (x[j] == 0) zero_num++;
+    else prod *= x[j];
+  }
+  double my_p = 0;
+  int prodSign = (i & 1LL) ? -1 : 1;
+  while (i < my_end) {
+    int k = __builtin_ctzll(i);
+    gray ^= (1LL << k);
+    double sg = ((1LL << k) & gray) ? 1.0 : -1.0;
+    for (int j = s->cptrs[k]; j < s->cptrs[k + 1]; ++j) {
+      const int r = s->rows[j];
+      if (x[r] == 0) {
+        zero_num--;
+        x[r] += sg * s->cvals[j];
+        prod *= x[r];
+      } else {
+        prod /= x[r];
+        x[r] += sg * s->cvals[j];
+        if (x[r] == 0) zero_num++;
+        else prod *= x[r];
+      }
+    }
+    if (zero_num == 0) my_p += prodSign * prod;
+    prodSign *= -1;
+    i++;
+  }
+  return my_p;
+}
+
+/* cpu_algos.hpp:635-757 parallel_perman64_sparse<double,double> */
+double orc_ref_sparse(const double* a, int n, int threads) {
+  csx* S = (csx*)malloc(sizeof(csx));
+  compress(a, n, S);
+  double x0[ORC_MAXN], p;
+  orc_nw_start(a, n, x0, &p);
+  const long long start = 1, end = 1LL << (n - 1);
+  const long long cs = end / threads + 1;
+  double* part = (double*)calloc(threads, sizeof(double));
+#pragma omp parallel for num_threads(threads) schedule(static, 1)
+  for (int tid = 0; tid < threads; ++tid) {
+    long long ms = start + tid * cs;
+    long long me = start + (tid + 1) * cs;
+    if (me > end) me = end;
+    part[tid] = sparse_range(S, x0, n, ms, me);
+  }
+  for (int tid = 0; tid < threads; ++tid) p += part[tid];
+  free(part);
+  free(S);
+  return (4 * (n & 1) - 2) * p;
+}
+
+/* gpu_exact_sparse.cu:6-87 cpu_perman64_sparse (partial, no p0) */
+double orc_ref_sparse_partial(const double* a, int n, long long start, long long end, int threads) {
+  csx* S = (csx*)malloc(sizeof(csx));
+  compress(a, n, S);
+  double x0[ORC_MAXN], p0;
+  orc_nw_start(a, n, x0, &p0);
+  const long long cs = (end - start) / threads + 1;
+  double* part = (double*)calloc(threads, sizeof(double));
+#pragma omp parallel for num_threads(threads) schedule(static, 1)
+  for (int tid = 0; tid < threads; ++tid) {
+    long long ms = start + tid * cs;
+    long long me = start + (tid + 1) * cs;
+    if (me > end) me = end;
+    part[tid] = sparse_range(S, x0, n, ms, me);
+  }
+  double p = 0.0;
+  for (int tid = 0; tid < threads; ++tid) p += part[tid];
+  free(part);
+  free(S);
+  return p;
+}
+
+/* One SkipPer chunk [my_start, my_end) starting from x (copied):
+ * cpu_algos.hpp:1122-1196 == gpu_exact_sparse.cu:110-186.  Returns the partial
+ * and adds the number of evaluated products to *visited. */
+static double skip_range(const csx* s, const double* xin, int n, unsigned long long my_start,
+                         unsigned long long my_end, unsigned long long* visited) {
+  double my_x[ORC_MAXN];
+  memcpy(my_x, xin, sizeof(double) * n);
+  double my_p = 0;
+  unsigned long long my_prev_gray = 0, i = my_start, vis = 0;
+  while (i < my_end) {
+    unsigned long long my_gray = i ^ (i >> 1);
+    unsigned long long gray_diff = my_prev_gray ^ my_gray;
+    int j = 0;
+    while (gray_diff > 0) {
+      unsigned long long onej = 1ULL << j;
+      if (gray_diff & onej) {
+        gray_diff ^= onej;
+        if (my_gray & onej) {
+          for (int ptr = s->cptrs[j]; ptr < s->cptrs[j + 1]; ptr++) my_x[s->rows[ptr]] += s->cvals[ptr];
+        } else {
+          for (int ptr = s->cptrs[j]; ptr < s->cptrs[j + 1]; ptr++) my_x[s->rows[ptr]] -= s->cvals[ptr];
+        }
+      }
+      j++;
+    }
+    my_prev_gray = my_gray;
+    int last_zero = -1;
+    double my_prod = 1;
+    for (j = n - 1; j >= 0; j--) {
+      my_prod *= my_x[j];
+      if (my_x[j] == 0) {
+        last_zero = j;
+        break;
+      }
+    }
+    vis++;
+    if (my_prod != 0 || last_zero < 0) {  /* last_zero < 0: underflow, no zero row (ref reads rptrs[-1]) */
+      my_p += ((i & 1ULL) ? -1.0 : 1.0) * my_prod;
+      i++;
+    } else {
+      unsigned long long change_j = ~0ULL;
+      for (int ptr = s->rptrs[last_zero]; ptr < s->rptrs[last_zero + 1]; ptr++) {
+        unsigned long long step_start = 1ULL << s->cols[ptr];
+        unsigned long long period = step_start << 1;
+        unsigned long long ci = step_start;
+        if (i >= step_start) {
+          unsigned long long steps = (i - step_start) / period;
+          ci = step_start + ((steps + 1) * period);
+        }
+        if (ci < change_j) change_j = ci;
+      }
+      i++;
+      if (change_j > i) i = change_j;
+    }
+  }
+  *visited += vis;
+  return my_p;
+}
+
+/* cpu_algos.hpp:1035-1213 parallel_skip_perman64_w_balanced<double,double>
+ * (512 chunks; chunk partials summed in chunk order). */
+double orc_ref_skip(const double* a, int n, int threads, unsigned long long* visited) {
+  csx* S = (csx*)malloc(sizeof(csx));
+  compress(a, n, S);
+  double x[ORC_MAXN];
+  for (int j = 0; j < n; j++) {
+    double rs = 0.0;
+    for (int ptr = S->rptrs[j]; ptr < S->rptrs[j + 1]; ptr++) rs += S->rvals[ptr];
+    x[j] = -rs / (2.0f);
+  }
+  for (int ptr = S->cptrs[n - 1]; ptr < S->cptrs[n]; ptr++) x[S->rows[ptr]] += S->cvals[ptr];
+  double prod = 1;
+  for (int j = 0; j < n; j++) prod *= x[j];
+  double p = prod;
+  unsigned long long start = 1;
+  for (int j = 0; j < n; j++) {
+    if (x[j] == 0) {
+      unsigned long long change_j = ~0ULL;
+      for (int ptr = S->rptrs[j]; ptr < S->rptrs[j + 1]; ptr++) {
+        unsigned long long ci = 1ULL << S->cols[ptr];
+        if (ci < change_j) change_j = ci;
+      }
+      if (change_j > start) start = change_j;
+    }
+  }
+  const unsigned long long end = 1ULL << (n - 1);
+  const int no_chunks = 512;
+  const unsigned long long cs = (end - start + 1) / no_chunks + 1;
+  double* part = (double*)calloc(no_chunks, sizeof(double));
+  unsigned long long* vis = (unsigned long long*)calloc(no_chunks, sizeof(unsigned long long));
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1)
+  for (int cid = 0; cid < no_chunks; cid++) {
+    unsigned long long ms = start + cid * cs;
+    unsigned long long me = start + (cid + 1) * cs;
+    if (me > end) me = end;
+    part[cid] = (ms < me) ? skip_range(S, x, n, ms, me, &vis[cid]) : 0.0;
+  }
+  unsigned long long tv = 0;
+  for (int cid = 0; cid < no_chunks; cid++) {
+    p += part[cid];
+    tv += vis[cid];
+  }
+  if (visited) *visited = tv;
+  free(part);
+  free(vis);
+  free(S);
+  return (4 * (n & 1) - 2) * p;
+}
+
+/* gpu_exact_sparse.cu:89-191 cpu_perman64_skipper (partial over [start,end), x0 from the dense
+ * prologue as in the wrapper gpu_exact_sparse.cu:1207-1218, 512 chunks). */
+double orc_ref_skip_partial(const double* a, int n, long long start, long long end, int threads) {
+  csx* S = (csx*)malloc(sizeof(csx));
+  compress(a, n, S);
+  double x0[ORC_MAXN], p0;
+  orc_nw_start(a, n, x0, &p0);
+  const int no_chunks = 512;
+  const unsigned long long cs = (unsigned long long)(end - start + 1) / no_chunks + 1;
+  double* part = (double*)calloc(no_chunks, sizeof(double));
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1)
+  for (int cid = 0; cid < no_chunks; cid++) {
+    unsigned long long ms = start + cid * cs;
+    unsigned long long me = start + (cid + 1) * cs;
+    if (me > (unsigned long long)end) me = end;
+    unsigned long long v = 0;
+    part[cid] = (ms < me) ? skip_range(S, x0, n, ms, me, &v) : 0.0;
+  }
+  double p = 0.0;
+  for (int cid = 0; cid < no_chunks; cid++) p += part[cid];
+  free(part);
+  free(S);
+  return p;
+}
+
+/* ====================================================================== *
+ * Engine-schedule mirror: the same Ryser sum, enumerated exactly as the
+ * gfx950 kernels do, so the GPU result can be checked
+ * bit-for-bit.  Independent restatement of the engine's spec:
+ *   Gray bits: [0,L) lanes, [L,L+m) walk, [L+m,n-1) wave-chunk index a;
+ *   lane state  x = x0 + sum_{b in gray(a)} A[:,L+m+b] (ascending b)
+ *                    + sum_{e<L, lane bit e} A[:,e] via fma(sel, c, x);
+ *   walk t=1..2^m-1 flips walk bit k=ctz(t), neg=(t>>(k+1))&1;
+ *   term(t) = (-1)^t * prod, lane result negated if (a ^ popcount(lane)) & 1;
+ *   wave value = pairwise tree over the 64 lanes (lanes >= 2^L give 0);
+ *   range value = pairwise tree over wave-chunks, 64-way zero padded.
+ * ====================================================================== */
+typedef struct {
+  int n, NP, kind, L, m, h;
+  int rowperm[ORC_MAXN], colmap[ORC_MAXN], nblk[ORC_MAXN];
+  unsigned long long rowmask[ORC_MAXN], umask;
+  double x0[ORC_MAXN];
+  double col[2 * ORC_MAXN][ORC_MAXN]; /* [2e+neg][j] */
+} eplan;
+
+/* Layout: L = min(6, n-1); m = max(min(rest, 10), rest - 20); h = rest - m. */
+void orc_engine_layout(int n, int* L, int* m, int* h) {
+  int nb = n - 1;
+  int l = nb < 6 ? nb : 6;
+  int rest = nb - l;
+  int mm = rest < 10 ? rest : 10;
+  if (rest - 20 > mm) mm = rest - 20;
+  *L = l;
+  *m = mm;
+  *h = rest - mm;
+}
+
+static void engine_plan(const double* a, int n, int kind, int identity, int L, int m, eplan* P) {
+  memset(P, 0, sizeof(*P));
+  P->n = n;
+  P->NP = (n + 7) & ~7;
+  P->kind = kind;
+  P->L = L;
+  P->m = m;
+  P->h = n - 1 - L - m;
+  int nb = n - 1;
+  for (int e = 0; e < nb; ++e) P->colmap[e] = e;
+  if (!identity && kind == 1 && m > 0) {
+    for (int k = 0; k < m; ++k) P->colmap[L + k] = k;
+    for (int e = 0; e < L; ++e) P->colmap[e] = m + e;
+  }
+  for (int j = 0; j < n; ++j) P->rowperm[j] = j;
+  if (kind != 0) {
+    char placed[ORC_MAXN] = {0};
+    int cnt = 0;
+    for (int k = 0; k < m; ++k) {
+      int c = P->colmap[L + k];
+      for (int i = 0; i < n; ++i)
+        if (!placed[i] && a[i * n + c] != 0.0) {
+          placed[i] = 1;
+          P->rowperm[cnt++] = i;
+        }
+      P->nblk[L + k] = (cnt + 7) / 8;
+    }
+    for (int i = 0; i < n; ++i)
+      if (!placed[i]) P->rowperm[cnt++] = i;
+  }
+  for (int e = 0; e < nb; ++e)
+    if (e < L || e >= L + m) P->nblk[e] = (n + 7) / 8;
+  for (int e = 0; e < nb; ++e)
+    for (int j = 0; j < n; ++j) {
+      double v = a[P->rowperm[j] * n + P->colmap[e]];
+      P->col[2 * e][j] = v;
+      P->col[2 * e + 1][j] = -v;
+    }
+  double x0[ORC_MAXN], p0;
+  orc_nw_start(a, n, x0, &p0);
+  for (int j = 0; j < n; ++j) P->x0[j] = x0[P->rowperm[j]];
+  P->umask = 0;
+  for (int j = 0; j < n; ++j) {
+    int i = P->rowperm[j], touched = 0;
+    for (int e = 0; e < L; ++e)
+      if (a[i * n + P->colmap[e]] != 0.0) touched = 1;
+    if (!touched) P->umask |= 1ULL << j;
+    unsigned long long rm = 0;
+    for (int k = 0; k < m; ++k)
+      if (a[i * n + P->colmap[L + k]] != 0.0) rm |= 1ULL << k;
+    P->rowmask[j] = rm;
+  }
+}
+
+static double e_prod4(const double* x, int n) {
+  double p0 = x[0], p1 = n > 1 ? x[1] : 1.0, p2 = n > 2 ? x[2] : 1.0, p3 = n > 3 ? x[3] : 1.0;
+  for (int j = 4; j < n; j += 4) {
+    p0 *= x[j];
+    if (j + 1 < n) p1 *= x[j + 1];
+    if (j + 2 < n) p2 *= x[j + 2];
+    if (j + 3 < n) p3 *= x[j + 3];
+  }
+  return (p0 * p1) * (p2 * p3);
+}
+
+static double e_bprod8(const double* x, int n, int b) {
+  double v[8];
+  for (int i = 0; i < 8; ++i) v[i] = (8 * b + i < n) ? x[8 * b + i] : 1.0;
+  return ((v[0] * v[1]) * (v[2] * v[3])) * ((v[4] * v[5]) * (v[6] * v[7]));
+}
+
+static void e_suffix(const double* x, int n, double* U) {
+  int NB = (n + 7) / 8;
+  U[NB] = 1.0;
+  for (int b = NB - 1; b >= 0; --b) U[b] = e_bprod8(x, n, b) * U[b + 1];
+}
+
+static void e_sparse_step(double* x, double* U, int n, const double* col, int nb) {
+  int NB = (n + 7) / 8;
+  for (int b = 0; b < NB && b < nb; ++b)
+    for (int j = 8 * b; j < 8 * b + 8 && j < n; ++j) x[j] += col[j];
+  for (int b = NB - 1; b >= 0; --b)
+    if (b < nb) U[b] = e_bprod8(x, n, b) * U[b + 1];
+}
+
+static void e_start(const eplan* P, unsigned long long ga, unsigned lane, double* x) {
+  int n = P->n;
+  for (int j = 0; j < n; ++j) x[j] = P->x0[j];
+  unsigned long long h = ga ^ (ga >> 1);
+  for (int b = 0; h; ++b, h >>= 1)
+    if (h & 1)
+      for (int j = 0; j < n; ++j) x[j] += P->col[2 * (P->L + P->m + b)][j];
+  for (int e = 0; e < P->L; ++e) {
+    double sel = ((lane >> e) & 1u) ? 1.0 : 0.0;
+    for (int j = 0; j < n; ++j) x[j] = fma(sel, P->col[2 * e][j], x[j]);
+  }
+}
+
+static double pair64(double* v) {
+  for (int w = 64; w > 1; w >>= 1)
+    for (int i = 0; i < w / 2; ++i) v[i] = v[2 * i] + v[2 * i + 1];
+  return v[0];
+}
+
+static unsigned next_toggle(unsigned t, unsigned k) {
+  unsigned c = ((t >> (k + 1)) << (k + 1)) + (1u << k);
+  if (c <= t) c += 2u << k;
+  return c;
+}
+
+static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long* visited) {
+  int n = P->n, L = P->L, m = P->m, NB = (n + 7) / 8;
+  unsigned T = 1u << m;
+  double lv[64];
+  if (P->kind != 2) {
+    for (unsigned l = 0; l < 64; ++l) {
+      if (l >= (1u << L)) {
+        lv[l] = 0.0;
+        continue;
+      }
+      double x[ORC_MAXN], U[ORC_MAXN / 8 + 2], acc;
+      e_start(P, ga, l, x);
+      if (P->kind == 0) {
+        acc = e_prod4(x, n);
+        for (unsigned t = 1; t < T; ++t) {
+          unsigned k = __builtin_ctz(t), neg = (t >> (k + 1)) & 1u;
+          for (int j = 0; j < n; ++j) x[j] += P->col[2 * (L + k) + neg][j];
+          double pr = e_prod4(x, n);
+          acc = (t & 1u) ? acc - pr : acc + pr;
+        }
+      } else {
+        e_suffix(x, n, U);
+        acc = U[0];
+        for (unsigned t = 1; t < T; ++t) {
+          unsigned k = __builtin_ctz(t), neg = (t >> (k + 1)) & 1u;
+          e_sparse_step(x, U, n, P->col[2 * (L + k) + neg], P->nblk[L + k]);
+          acc = (t & 1u) ? acc - U[0] : acc + U[0];
+        }
+      }
+      if ((((unsigned)ga) ^ (unsigned)__builtin_popcount(l)) & 1u) acc = -acc;
+      lv[l] = acc;
+    }
+    if (visited) *visited += (unsigned long long)T << L;
+    return pair64(lv);
+  }
+  /* skipper: 64 lanes in lock-step with wave-uniform jumps */
+  static __thread double X[64][ORC_MAXN], UU[64][ORC_MAXN / 8 + 2];
+  double acc[64];
+  (void)NB;
+  for (unsigned l = 0; l < 64; ++l) {
+    e_start(P, ga, l, X[l]);
+    e_suffix(X[l], n, UU[l]);
+    acc[l] = 0.0;
+  }
+  unsigned t = 0;
+  unsigned long long vis = 0;
+  for (;;) {
+    int all_zero = 1;
+    vis++;
+    for (unsigned l = 0; l < 64; ++l) {
+      double term = UU[l][0];
+      acc[l] = (t & 1u) ? acc[l] - term : acc[l] + term;
+      if (term != 0.0) all_zero = 0;
+    }
+    unsigned next = t + 1;
+    if (all_zero) {
+      unsigned long long zm = 0;
+      for (int r = 0; r < n; ++r)
+        if (X[0][r] == 0.0) zm |= 1ULL << r;
+      zm &= P->umask;
+      if (zm) {
+        unsigned target = t + 1;
+        while (zm) {
+          int r = __builtin_ctzll(zm);
+          zm &= zm - 1;
+          unsigned long long mm = P->rowmask[r];
+          unsigned tr = T;
+          while (mm) {
+            unsigned k = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            unsigned c = next_toggle(t, k);
+            if (c < tr) tr = c;
+          }
+          if (tr > target) target = tr;
+        }
+        next = target;
+      }
+    }
+    if (next >= T) break;
+    unsigned gn = next ^ (next >> 1), diff = (t ^ (t >> 1)) ^ gn;
+    do {
+      unsigned k = __builtin_ctz(diff);
+      diff &= diff - 1;
+      unsigned neg = ((gn >> k) & 1u) ^ 1u;
+      for (unsigned l = 0; l < 64; ++l) e_sparse_step(X[l], UU[l], n, P->col[2 * (L + k) + neg], P->nblk[L + k]);
+    } while (diff);
+    t = next;
+  }
+  if (visited) *visited += vis << L;
+  for (unsigned l = 0; l < 64; ++l) {
+    double v = acc[l];
+    if ((((unsigned)ga) ^ (unsigned)__builtin_popcount(l)) & 1u) v = -v;
+    lv[l] = (l < (1u << L)) ? v : 0.0;
+  }
+  return pair64(lv);
+}
+
+/* Engine-mirror partial over wave-chunks [c0, c1) with layout (L, m).
+ * kind: 0 dense, 1 SpaRyser, 2 SkipPer.  identity: engine bit e = column e. */
+double orc_engine_range(const double* a, int n, int kind, int identity, int L, int m, unsigned long long c0,
+                        unsigned long long c1, int threads, unsigned long long* visited) {
+  eplan* P = (eplan*)malloc(sizeof(eplan));
+  engine_plan(a, n, kind, identity, L, m, P);
+  unsigned long long count = c1 > c0 ? c1 - c0 : 0;
+  if (count == 0) {
+    free(P);
+    return 0.0;
+  }
+  double* part = (double*)malloc(sizeof(double) * count);
+  unsigned long long tv = 0;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1) reduction(+ : tv)
+  for (long long i = 0; i < (long long)count; ++i) {
+    unsigned long long v = 0;
+    part[i] = e_chunk(P, c0 + i, &v);
+    tv += v;
+  }
+  while (count > 1) {
+    unsigned long long groups = (count + 63) / 64;
+    for (unsigned long long g = 0; g < groups; ++g) {
+      double v[64];
+      for (int l = 0; l < 64; ++l) {
+        unsigned long long i = g * 64 + l;
+        v[l] = i < count ? part[i] : 0.0;
+      }
+      part[g] = pair64(v);
+    }
+    count = groups;
+  }
+  double r = part[0];
+  free(part);
+  free(P);
+  if (visited) *visited = tv;
+  return r;
+}
+
+/* Full permanent with the engine's default layout and column map. */
+double orc_engine_perman(const double* a, int n, int kind, int threads) {
+  int L, m, h;
+  orc_engine_layout(n, &L, &m, &h);
+  double s = orc_engine_range(a, n, kind, 0, L, m, 0, 1ULL << h, threads, 0);
+  return (4 * (n & 1) - 2) * s;
+}

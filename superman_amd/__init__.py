@@ -1,0 +1,246 @@
+"""superman_amd — MI355X-native exact matrix permanent (Ryser / Gray code).
+
+Host-side mirror of the reference's operator interface (kamerkaya/SUPerman
+v1): ``RunAlgo<T>``'s algorithm-id dispatch (main.cu:20-248) and the GPU
+wrapper functions (gpu_exact_dense.cu:641-990, gpu_exact_sparse.cu:854-1408),
+over the C ABI of ``libsuperman_hip.so`` (include/superman.h).  All compute
+runs in the gfx950 HIP kernels of ``superman_amd/csrc``; the GPU functions
+raise ``SupError`` (SUP_ENODEV) when no device is present — there is no CPU
+fallback.  ``perman_cpu`` is the explicit CPU algorithm of the CLI's ``-c``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import (KERNEL_DENSE, KERNEL_SKIPPER, KERNEL_SPARYSER, SCHED_CHUNKS, SCHED_SINGLE,
+                   SCHED_STATIC, SupError, SupOpts, SupStats)
+
+__all__ = [
+    "perman", "perman_cpu", "partial", "read_matrix", "sort_order", "skip_order", "compress",
+    "nw_start", "device_count", "layout", "SupError", "ALGOS_DENSE", "ALGOS_SPARSE",
+    "gpu_perman64_xshared_coalescing_mshared",
+    "gpu_perman64_xshared_coalescing_mshared_multigpu",
+    "gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks",
+    "gpu_perman64_xshared_coalescing_mshared_sparse",
+    "gpu_perman64_xshared_coalescing_mshared_multigpu_sparse",
+    "gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_sparse",
+    "gpu_perman64_xshared_coalescing_mshared_skipper",
+    "gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper",
+]
+
+_DT = {np.dtype(np.int32): _lib.SUP_INT32, np.dtype(np.float32): _lib.SUP_FLOAT32,
+       np.dtype(np.float64): _lib.SUP_FLOAT64}
+_NP = {_lib.SUP_INT32: np.int32, _lib.SUP_FLOAT32: np.float32, _lib.SUP_FLOAT64: np.float64}
+_TYPE_NAME = {_lib.SUP_INT32: "int", _lib.SUP_FLOAT32: "float", _lib.SUP_FLOAT64: "double"}
+
+# main.cu:30-143 GPU exact dispatch: algo id -> (name, kernel, schedule)
+ALGOS_DENSE = {
+    0: ("gpu_perman64_xglobal", KERNEL_DENSE, SCHED_SINGLE),
+    1: ("gpu_perman64_xlocal", KERNEL_DENSE, SCHED_SINGLE),
+    2: ("gpu_perman64_xshared", KERNEL_DENSE, SCHED_SINGLE),
+    3: ("gpu_perman64_xshared_coalescing", KERNEL_DENSE, SCHED_SINGLE),
+    4: ("gpu_perman64_xshared_coalescing_mshared", KERNEL_DENSE, SCHED_SINGLE),
+    5: ("gpu_perman64_xshared_coalescing_mshared_multigpu", KERNEL_DENSE, SCHED_STATIC),
+    6: ("gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks", KERNEL_DENSE, SCHED_CHUNKS),
+    66: ("gpu_perman64_xshared_coalescing_mshared_multigpu_manual_distribution", KERNEL_DENSE, SCHED_STATIC),
+}
+ALGOS_SPARSE = {
+    1: ("gpu_perman64_xlocal_sparse", KERNEL_SPARYSER, SCHED_SINGLE),
+    2: ("gpu_perman64_xshared_sparse", KERNEL_SPARYSER, SCHED_SINGLE),
+    3: ("gpu_perman64_xshared_coalescing_sparse", KERNEL_SPARYSER, SCHED_SINGLE),
+    4: ("gpu_perman64_xshared_coalescing_mshared_sparse", KERNEL_SPARYSER, SCHED_SINGLE),
+    5: ("gpu_perman64_xshared_coalescing_mshared_multigpu_sparse", KERNEL_SPARYSER, SCHED_STATIC),
+    6: ("gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_sparse", KERNEL_SPARYSER, SCHED_CHUNKS),
+    7: ("gpu_perman64_xshared_coalescing_mshared_skipper", KERNEL_SKIPPER, SCHED_SINGLE),
+    8: ("gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper", KERNEL_SKIPPER, SCHED_CHUNKS),
+    66: ("gpu_perman64_xshared_coalescing_mshared_multigpu_sparse_manual_distribution", KERNEL_SPARYSER,
+         SCHED_STATIC),
+}
+_KERNELS = {"dense": KERNEL_DENSE, "sparse": KERNEL_SPARYSER, "spa": KERNEL_SPARYSER,
+            "skipper": KERNEL_SKIPPER, "skip": KERNEL_SKIPPER}
+
+
+def _mat(a) -> tuple[np.ndarray, int, int]:
+    a = np.asarray(a)
+    if a.dtype not in _DT:
+        a = a.astype(np.float64)
+    a = np.ascontiguousarray(a)
+    if a.ndim != 2 or a.shape[0] != a.shape[1]:
+        raise ValueError(f"expected a square matrix, got shape {a.shape}")
+    n = a.shape[0]
+    if not 1 <= n <= 64:
+        raise ValueError(f"n = {n} outside [1, 64] (64-bit Gray index)")
+    return a, _DT[a.dtype], n
+
+
+def _opts(gpu_num=1, device_id=0, threads=16, cpu=False, walk_log2=0, chunk_log2=0, use_rccl=False,
+          verbose=False) -> SupOpts:
+    lib = _lib.load()
+    o = SupOpts()
+    lib.sup_opts_init(C.byref(o))
+    o.gpu_num, o.device_id, o.threads = int(gpu_num), int(device_id), int(threads)
+    o.cpu_worker, o.walk_log2, o.chunk_log2 = int(bool(cpu)), int(walk_log2), int(chunk_log2)
+    o.use_rccl, o.verbose = int(bool(use_rccl)), int(bool(verbose))
+    return o
+
+
+def device_count() -> int:
+    lib = _lib.load()
+    c = C.c_int(0)
+    rc = lib.sup_device_count(C.byref(c))
+    return c.value if rc == 0 else 0
+
+
+def layout(n: int) -> tuple[int, int, int]:
+    """Engine layout (lane bits L, walk bits m, wave-chunk bits h) for order n."""
+    nb = n - 1
+    L = min(6, nb)
+    rest = nb - L
+    m = max(min(rest, 10), rest - 20)
+    return L, m, rest - m
+
+
+def perman(mat, algo: int = 4, sparse: bool = False, gpu_num: int = 1, cpu: bool = False,
+           threads: int = 16, device_id: int = 0, use_rccl: bool = False, walk_log2: int = 0,
+           chunk_log2: int = 0, return_stats: bool = False):
+    """GPU exact permanent, dispatched by the reference algorithm id (main.cu:30-143).
+
+    ``sparse`` selects the sparse table (SpaRyser ids 1-6, SkipPer 7/8).  Apply
+    ``sort_order``/``skip_order`` first to mirror ``-r1``/``-r2``.
+    """
+    table = ALGOS_SPARSE if sparse else ALGOS_DENSE
+    if algo not in table:
+        raise SupError(-7, "perman", f"unknown algorithm id {algo}")
+    _, kernel, sched = table[algo]
+    if algo == 66:
+        gpu_num = 4
+    if sched == SCHED_SINGLE:
+        gpu_num = 1
+    a, dt, n = _mat(mat)
+    lib = _lib.load()
+    o = _opts(gpu_num, device_id, threads, cpu, walk_log2, chunk_log2, use_rccl)
+    out, st = C.c_double(0.0), SupStats()
+    _lib.check(lib.sup_perman(a.ctypes.data, dt, n, kernel, sched, C.byref(o), C.byref(out), C.byref(st)),
+               table[algo][0])
+    return (out.value, st.as_dict()) if return_stats else out.value
+
+
+def perman_cpu(mat, kernel: str = "dense", threads: int = 16, return_stats: bool = False):
+    """The CLI's explicit CPU algorithm (-c): same walk on host threads."""
+    a, dt, n = _mat(mat)
+    lib = _lib.load()
+    out, st = C.c_double(0.0), SupStats()
+    _lib.check(lib.sup_perman_cpu(a.ctypes.data, dt, n, _KERNELS[kernel], int(threads), C.byref(out),
+                                  C.byref(st)), "perman_cpu")
+    return (out.value, st.as_dict()) if return_stats else out.value
+
+
+def partial(mat, start: int, end: int, kernel: str = "dense", gpu_num: int = 1, device_id: int = 0,
+            walk_log2: int = 0, return_stats: bool = False):
+    """GPU partial Ryser sum over reference Gray indices [start, end) (index 0 = p0 term)."""
+    a, dt, n = _mat(mat)
+    lib = _lib.load()
+    o = _opts(gpu_num=gpu_num, device_id=device_id, walk_log2=walk_log2)
+    out, st = C.c_double(0.0), SupStats()
+    _lib.check(lib.sup_partial(a.ctypes.data, dt, n, _KERNELS[kernel], int(start), int(end), C.byref(o),
+                               C.byref(out), C.byref(st)), "partial")
+    return (out.value, st.as_dict()) if return_stats else out.value
+
+
+def nw_start(mat) -> tuple[np.ndarray, float]:
+    a, dt, n = _mat(mat)
+    lib = _lib.load()
+    x0 = np.zeros(n, np.float64)
+    p0 = C.c_double(0.0)
+    _lib.check(lib.sup_nw_start(a.ctypes.data, dt, n, x0.ctypes.data_as(C.POINTER(C.c_double)), C.byref(p0)),
+               "nw_start")
+    return x0, p0.value
+
+
+def read_matrix(path: str, binary: bool = False) -> tuple[np.ndarray, str, int]:
+    """v1 matrix file -> (matrix, type name, nnz from the header) (util.h:343-358)."""
+    lib = _lib.load()
+    p, t, n, nnz = C.c_void_p(), C.c_int(), C.c_int(), C.c_int()
+    _lib.check(lib.sup_read_matrix(path.encode(), int(bool(binary)), C.byref(p), C.byref(t), C.byref(n),
+                                   C.byref(nnz)), "read_matrix")
+    try:
+        dtype = _NP[t.value]
+        buf = (C.c_char * (n.value * n.value * np.dtype(dtype).itemsize)).from_address(p.value)
+        m = np.frombuffer(buf, dtype=dtype).reshape(n.value, n.value).copy()
+    finally:
+        lib.sup_free(p)
+    return m, _TYPE_NAME[t.value], nnz.value
+
+
+def sort_order(mat) -> tuple[np.ndarray, np.ndarray]:
+    """SortOrder (util.h:553-619): returns (permuted matrix, colperm)."""
+    a, dt, n = _mat(mat)
+    a = a.copy()
+    cp = np.zeros(n, np.int32)
+    _lib.check(_lib.load().sup_sort_order(a.ctypes.data, dt, n, cp.ctypes.data), "sort_order")
+    return a, cp
+
+
+def skip_order(mat) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """SkipOrder (util.h:621-684): returns (permuted matrix, rowperm, colperm)."""
+    a, dt, n = _mat(mat)
+    a = a.copy()
+    rp, cp = np.zeros(n, np.int32), np.zeros(n, np.int32)
+    _lib.check(_lib.load().sup_skip_order(a.ctypes.data, dt, n, rp.ctypes.data, cp.ctypes.data), "skip_order")
+    return a, rp, cp
+
+
+def compress(mat) -> dict:
+    """CSR + CSC with the != 0 nonzero test (util.h:522-551)."""
+    a, dt, n = _mat(mat)
+    lib = _lib.load()
+    nnz = C.c_int(0)
+    _lib.check(lib.sup_count_nnz(a.ctypes.data, dt, n, C.byref(nnz)), "count_nnz")
+    k = max(nnz.value, 1)
+    out = {"cptrs": np.zeros(n + 1, np.int32), "rows": np.zeros(k, np.int32), "cvals": np.zeros(k, a.dtype),
+           "rptrs": np.zeros(n + 1, np.int32), "cols": np.zeros(k, np.int32), "rvals": np.zeros(k, a.dtype)}
+    _lib.check(lib.sup_compress(a.ctypes.data, dt, n, *(out[f].ctypes.data for f in
+                                                        ("cptrs", "rows", "cvals", "rptrs", "cols", "rvals"))),
+               "compress")
+    for f in ("rows", "cvals", "cols", "rvals"):
+        out[f] = out[f][: nnz.value]
+    return out
+
+
+# ---- reference-named wrappers (gpu_exact_dense.cu / gpu_exact_sparse.cu) -----------
+def gpu_perman64_xshared_coalescing_mshared(mat, grid_dim=2048, block_dim=256):
+    return perman(mat, 4)
+
+
+def gpu_perman64_xshared_coalescing_mshared_multigpu(mat, gpu_num, grid_dim=2048, block_dim=256):
+    return perman(mat, 5, gpu_num=gpu_num)
+
+
+def gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks(mat, gpu_num, cpu=False, threads=16,
+                                                               grid_dim=2048, block_dim=256):
+    return perman(mat, 6, gpu_num=gpu_num, cpu=cpu, threads=threads)
+
+
+def gpu_perman64_xshared_coalescing_mshared_sparse(mat, grid_dim=2048, block_dim=256):
+    return perman(mat, 4, sparse=True)
+
+
+def gpu_perman64_xshared_coalescing_mshared_multigpu_sparse(mat, gpu_num, grid_dim=2048, block_dim=256):
+    return perman(mat, 5, sparse=True, gpu_num=gpu_num)
+
+
+def gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_sparse(mat, gpu_num, cpu=False, threads=16,
+                                                                      grid_dim=2048, block_dim=256):
+    return perman(mat, 6, sparse=True, gpu_num=gpu_num, cpu=cpu, threads=threads)
+
+
+def gpu_perman64_xshared_coalescing_mshared_skipper(mat, grid_dim=2048, block_dim=256):
+    return perman(mat, 7, sparse=True)
+
+
+def gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper(mat, gpu_num, cpu=False, threads=16,
+                                                                       grid_dim=2048, block_dim=256):
+    return perman(mat, 8, sparse=True, gpu_num=gpu_num, cpu=cpu, threads=threads)

@@ -1,0 +1,217 @@
+// capi.cpp — extern "C" boundary (include/superman.h).
+#include <chrono>
+#include <cstring>
+
+#include "engine.hpp"
+
+using namespace sup;
+
+namespace {
+
+int check_common(const void* mat, int n, double* out) {
+  if (!mat || !out) {
+    set_error("null matrix or output pointer");
+    return SUP_EINVAL;
+  }
+  if (n < 1 || n > SUP_MAX_N) {
+    set_error("n = " + std::to_string(n) + " outside [1, 64] (64-bit Gray index)");
+    return SUP_EINVAL;
+  }
+  return SUP_OK;
+}
+
+WalkKind kind_of(sup_kernel k) {
+  switch (k) {
+    case SUP_KERNEL_SPARYSER: return kWalkSparse;
+    case SUP_KERNEL_SKIPPER: return kWalkSkip;
+    default: return kWalkDense;
+  }
+}
+
+void fill_stats(sup_stats* st, const Plan& P, const SchedResult& r, double wall_ms, uint64_t gray) {
+  if (!st) return;
+  std::memset(st, 0, sizeof(*st));
+  st->kernel_ms = r.kernel_ms;
+  st->wall_ms = wall_ms;
+  st->gray_steps = gray;
+  st->visited_steps = r.visited;
+  st->devices_used = r.devices;
+  st->lane_bits = P.lay.L;
+  st->walk_bits = P.lay.m;
+  st->grid = r.grid;
+  st->chunks_done_cpu = r.cpu_items;
+  for (size_t i = 0; i < r.dev_partials.size() && i < 16; ++i) st->partials[i] = r.dev_partials[i];
+}
+
+}  // namespace
+
+extern "C" {
+
+void sup_opts_init(sup_opts* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->gpu_num = 1;
+  o->device_id = 0;
+  o->threads = 16;  // main.cu:333
+  o->block_dim = 256;
+}
+
+int sup_abi_version(void) { return SUP_ABI_VERSION; }
+const char* sup_last_error(void) { return last_error(); }
+int sup_device_count(int* count) {
+  if (!count) return SUP_EINVAL;
+  return device_count(count);
+}
+
+int sup_nw_start(const void* mat, sup_dtype t, int n, double* x0, double* p0) {
+  if (!x0 || !p0) {
+    set_error("null output pointer");
+    return SUP_EINVAL;
+  }
+  std::vector<double> A;
+  int rc = to_double(mat, t, n, A);
+  if (rc) return rc;
+  nw_start(A.data(), n, x0, p0);
+  return SUP_OK;
+}
+
+int sup_perman(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched sched, const sup_opts* o_in,
+               double* out, sup_stats* st) {
+  auto t0 = std::chrono::steady_clock::now();
+  int rc = check_common(mat, n, out);
+  if (rc) return rc;
+  sup_opts o;
+  if (o_in) o = *o_in;
+  else sup_opts_init(&o);
+  std::vector<double> A;
+  if ((rc = to_double(mat, t, n, A))) return rc;
+  Plan P;
+  Layout lay = default_layout(n);
+  if (o.walk_log2 > 0) {
+    const int rest = n - 1 - lay.L;
+    lay.m = std::min(o.walk_log2, rest);
+    lay.h = rest - lay.m;
+  }
+  if ((rc = make_plan(A.data(), n, kind_of(kernel), false, lay, P))) return rc;
+  SchedResult r;
+  if ((rc = schedule(P, sched, o, 0, P.lay.chunks(), r))) return rc;
+  *out = (double)(4 * (n & 1) - 2) * r.total;  // gpu_exact_dense.cu:698
+  const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  fill_stats(st, P, r, wall, 1ull << (n - 1));
+  return SUP_OK;
+}
+
+int sup_partial(const void* mat, sup_dtype t, int n, sup_kernel kernel, uint64_t start, uint64_t end,
+                const sup_opts* o_in, double* out, sup_stats* st) {
+  auto t0 = std::chrono::steady_clock::now();
+  int rc = check_common(mat, n, out);
+  if (rc) return rc;
+  const uint64_t space = 1ull << (n - 1);
+  if (start > end || end > space) {
+    set_error("range [start, end) must satisfy start <= end <= 2^(n-1)");
+    return SUP_EINVAL;
+  }
+  sup_opts o;
+  if (o_in) o = *o_in;
+  else sup_opts_init(&o);
+  // Largest layout whose wave-chunk (2^(L+m) Gray indices) divides both ends.
+  Layout lay = default_layout(n);
+  const int nb = n - 1;
+  auto align_of = [&](uint64_t v) -> int { return v == 0 || v == space ? nb : __builtin_ctzll(v); };
+  const int al = std::min(align_of(start), align_of(end));
+  if (al < lay.L) {
+    set_error("range ends must be multiples of 2^" + std::to_string(lay.L) + " (one wave of Gray indices)");
+    return SUP_EINVAL;
+  }
+  if (lay.L + lay.m > al) {
+    lay.m = al - lay.L;
+    lay.h = nb - lay.L - lay.m;
+  }
+  if (o.walk_log2 > 0 && o.walk_log2 < lay.m) {
+    lay.m = o.walk_log2;
+    lay.h = nb - lay.L - lay.m;
+  }
+  std::vector<double> A;
+  if ((rc = to_double(mat, t, n, A))) return rc;
+  Plan P;
+  if ((rc = make_plan(A.data(), n, kind_of(kernel), true, lay, P))) return rc;
+  const int cb = lay.L + lay.m;
+  SchedResult r;
+  if ((rc = schedule(P, o.gpu_num > 1 ? SUP_SCHED_STATIC : SUP_SCHED_SINGLE, o, start >> cb, end >> cb, r)))
+    return rc;
+  *out = r.total;
+  const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  fill_stats(st, P, r, wall, end - start);
+  return SUP_OK;
+}
+
+int sup_perman_cpu(const void* mat, sup_dtype t, int n, sup_kernel kernel, int threads, double* out,
+                   sup_stats* st) {
+  auto t0 = std::chrono::steady_clock::now();
+  int rc = check_common(mat, n, out);
+  if (rc) return rc;
+  std::vector<double> A;
+  if ((rc = to_double(mat, t, n, A))) return rc;
+  Plan P;
+  if ((rc = make_plan(A.data(), n, kind_of(kernel), false, default_layout(n), P))) return rc;
+  SchedResult r;
+  r.total = cpu_walk_range(P, 0, P.lay.chunks(), threads < 1 ? 1 : threads);
+  r.visited = 1ull << (n - 1);
+  *out = (double)(4 * (n & 1) - 2) * r.total;
+  const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  fill_stats(st, P, r, wall, 1ull << (n - 1));
+  return SUP_OK;
+}
+
+// ---- reference-signature wrappers ------------------------------------------
+static int run_ref(const void* mat, sup_dtype t, int nov, sup_kernel k, sup_sched s, int gpu_num, int cpu,
+                   int threads, double* out) {
+  sup_opts o;
+  sup_opts_init(&o);
+  o.gpu_num = gpu_num < 1 ? 1 : gpu_num;
+  o.cpu_worker = cpu;
+  o.threads = threads;
+  return sup_perman(mat, t, nov, k, s, &o, out, nullptr);
+}
+
+int sup_gpu_perman64_xshared_coalescing_mshared(const void* mat, sup_dtype t, int nov, int, int, double* out) {
+  return run_ref(mat, t, nov, SUP_KERNEL_DENSE, SUP_SCHED_SINGLE, 1, 0, 16, out);
+}
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpu(const void* mat, sup_dtype t, int nov, int gpu_num, int,
+                                                         int, double* out) {
+  return run_ref(mat, t, nov, SUP_KERNEL_DENSE, SUP_SCHED_STATIC, gpu_num, 0, 16, out);
+}
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks(const void* mat, sup_dtype t, int nov,
+                                                                   int gpu_num, int cpu, int threads, int, int,
+                                                                   double* out) {
+  return run_ref(mat, t, nov, SUP_KERNEL_DENSE, SUP_SCHED_CHUNKS, gpu_num, cpu, threads, out);
+}
+int sup_gpu_perman64_xshared_coalescing_mshared_sparse(const void* mat, const int*, const int*, const void*,
+                                                       sup_dtype t, int nov, int, int, double* out) {
+  return run_ref(mat, t, nov, SUP_KERNEL_SPARYSER, SUP_SCHED_SINGLE, 1, 0, 16, out);
+}
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpu_sparse(const void* mat, const int*, const int*,
+                                                                const void*, sup_dtype t, int nov, int gpu_num,
+                                                                int, int, double* out) {
+  return run_ref(mat, t, nov, SUP_KERNEL_SPARYSER, SUP_SCHED_STATIC, gpu_num, 0, 16, out);
+}
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_sparse(const void* mat, const int*, const int*,
+                                                                          const void*, sup_dtype t, int nov,
+                                                                          int gpu_num, int cpu, int threads, int,
+                                                                          int, double* out) {
+  return run_ref(mat, t, nov, SUP_KERNEL_SPARYSER, SUP_SCHED_CHUNKS, gpu_num, cpu, threads, out);
+}
+int sup_gpu_perman64_xshared_coalescing_mshared_skipper(const void* mat, const int*, const int*, const int*,
+                                                        const int*, const void*, sup_dtype t, int nov, int, int,
+                                                        double* out) {
+  return run_ref(mat, t, nov, SUP_KERNEL_SKIPPER, SUP_SCHED_SINGLE, 1, 0, 16, out);
+}
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper(const void* mat, const int*, const int*,
+                                                                           const int*, const int*, const void*,
+                                                                           sup_dtype t, int nov, int gpu_num,
+                                                                           int cpu, int threads, int, int,
+                                                                           double* out) {
+  return run_ref(mat, t, nov, SUP_KERNEL_SKIPPER, SUP_SCHED_CHUNKS, gpu_num, cpu, threads, out);
+}
+
+}  // extern "C"

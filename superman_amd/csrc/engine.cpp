@@ -1,0 +1,545 @@
+// engine.cpp — plans, per-device contexts, single/static/chunked schedulers.
+#include "engine.hpp"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+namespace sup {
+
+// ---------------------------------------------------------------- errors --
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+const char* last_error() { return g_err.c_str(); }
+
+#define SUP_HIP(call)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      set_error(std::string(#call) + ": " + hipGetErrorString(e_));                    \
+      return SUP_EHIP;                                                                 \
+    }                                                                                  \
+  } while (0)
+
+// -------------------------------------------------------------- matrices --
+int to_double(const void* mat, sup_dtype t, int n, std::vector<double>& out) {
+  if (!mat || n < 1 || n > SUP_MAX_N) {
+    set_error("matrix pointer is null or n is outside [1, 64]");
+    return SUP_EINVAL;
+  }
+  const size_t nn = (size_t)n * n;
+  out.resize(nn);
+  switch (t) {
+    case SUP_INT32: {
+      const int32_t* a = (const int32_t*)mat;
+      for (size_t i = 0; i < nn; ++i) out[i] = (double)a[i];
+      return SUP_OK;
+    }
+    case SUP_FLOAT32: {
+      const float* a = (const float*)mat;
+      for (size_t i = 0; i < nn; ++i) out[i] = (double)a[i];
+      return SUP_OK;
+    }
+    case SUP_FLOAT64:
+      std::memcpy(out.data(), mat, nn * sizeof(double));
+      return SUP_OK;
+  }
+  set_error("unknown sup_dtype");
+  return SUP_EINVAL;
+}
+
+void nw_start(const double* A, int n, double* x0, double* p0) {
+  double p = 1.0;
+  for (int j = 0; j < n; ++j) {
+    double rs = 0.0;
+    for (int k = 0; k < n; ++k) rs += A[(size_t)j * n + k];
+    x0[j] = A[(size_t)j * n + (n - 1)] - rs / 2;
+    p *= x0[j];
+  }
+  *p0 = p;
+}
+
+Layout default_layout(int n) {
+  Layout l;
+  const int nb = n - 1;
+  l.L = nb < 6 ? nb : 6;
+  const int rest = nb - l.L;
+  // >= 2^10 walk steps per wave-chunk when possible, and at most 2^20
+  // wave-chunks (8 MiB of partials) — fine-grained enough that the dynamic
+  // chunk queue balances a whole MI355X (~5k resident waves) to < 1 %.
+  int m = rest < 10 ? rest : 10;
+  if (rest - 20 > m) m = rest - 20;
+  l.m = m;
+  l.h = rest - m;
+  return l;
+}
+
+int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const Layout& lay, Plan& P) {
+  if (n < 1 || n > SUP_MAX_N) {
+    set_error("n must be in [1, 64]");
+    return SUP_EINVAL;
+  }
+  P = Plan();
+  P.n = n;
+  P.NP = pad8(n);
+  P.kind = kind;
+  P.lay = lay;
+  const int nb = n - 1;  // flippable columns (column n-1 is the Nijenhuis-Wilf column)
+  const int L = lay.L, m = lay.m;
+
+  // ---- engine bit -> matrix column
+  P.colmap.resize(nb);
+  for (int e = 0; e < nb; ++e) P.colmap[e] = e;
+  if (!identity_map && kind == kWalkSparse && m > 0) {
+    // walk bits get the first (sparsest after SortOrder/SkipOrder) columns,
+    // lane bits the next L, the high bits keep their order.
+    for (int k = 0; k < m; ++k) P.colmap[L + k] = k;
+    for (int e = 0; e < L; ++e) P.colmap[e] = m + e;
+  }
+
+  // ---- engine row order
+  P.rowperm.resize(n);
+  for (int j = 0; j < n; ++j) P.rowperm[j] = j;
+  P.nblk.assign(std::max(nb, 1), 0);
+  P.rowmask.assign(n, 0);
+  if (kind != kWalkDense) {
+    // rows in first-touch order over the walk columns (walk order), then the rest
+    std::vector<char> placed(n, 0);
+    std::vector<int> order;
+    order.reserve(n);
+    for (int k = 0; k < m; ++k) {
+      const int c = P.colmap[L + k];
+      for (int i = 0; i < n; ++i)
+        if (!placed[i] && A[(size_t)i * n + c] != 0.0) {
+          placed[i] = 1;
+          order.push_back(i);
+        }
+      P.nblk[L + k] = ((int)order.size() + 7) / 8;
+    }
+    for (int i = 0; i < n; ++i)
+      if (!placed[i]) order.push_back(i);
+    P.rowperm = order;
+    // a walk column may touch no new row: nblk must still cover its own rows,
+    // which are all inside the prefix, so the prefix count above is correct.
+  }
+  for (int e = 0; e < nb; ++e)
+    if (e < L || e >= L + m) P.nblk[e] = (n + 7) / 8;  // not used by the walk; keep sane
+
+  // ---- tables
+  P.cols.assign((size_t)2 * std::max(nb, 1) * P.NP, 0.0);
+  for (int e = 0; e < nb; ++e) {
+    const int c = P.colmap[e];
+    for (int j = 0; j < n; ++j) {
+      const double v = A[(size_t)P.rowperm[j] * n + c];
+      P.cols[(size_t)(2 * e) * P.NP + j] = v;
+      P.cols[(size_t)(2 * e + 1) * P.NP + j] = -v;
+    }
+  }
+  std::vector<double> x0(n);
+  double p0;
+  nw_start(A, n, x0.data(), &p0);
+  P.x0.assign(P.NP, 0.0);
+  for (int j = 0; j < n; ++j) P.x0[j] = x0[P.rowperm[j]];
+
+  // ---- skipper metadata
+  P.umask = 0;
+  for (int j = 0; j < n; ++j) {
+    const int i = P.rowperm[j];
+    bool lane_touched = false;
+    for (int e = 0; e < L; ++e)
+      if (A[(size_t)i * n + P.colmap[e]] != 0.0) lane_touched = true;
+    if (!lane_touched) P.umask |= 1ull << j;
+    uint64_t rm = 0;
+    for (int k = 0; k < m; ++k)
+      if (A[(size_t)i * n + P.colmap[L + k]] != 0.0) rm |= 1ull << k;
+    P.rowmask[j] = rm;
+  }
+  return SUP_OK;
+}
+
+double pairwise_host(const std::vector<double>& v) {
+  if (v.empty()) return 0.0;
+  size_t p = 1;
+  while (p < v.size()) p <<= 1;
+  std::vector<double> a(p, 0.0);
+  std::copy(v.begin(), v.end(), a.begin());
+  while (p > 1) {
+    p >>= 1;
+    for (size_t i = 0; i < p; ++i) a[i] = a[2 * i] + a[2 * i + 1];
+  }
+  return a[0];
+}
+
+// -------------------------------------------------------- device contexts --
+struct DeviceCtx {
+  int dev = 0;
+  int cus = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double* d_cols = nullptr;
+  size_t cols_cap = 0;
+  double* d_x0 = nullptr;
+  int* d_nblk = nullptr;
+  uint64_t* d_rowmask = nullptr;
+  double* d_chunk = nullptr;
+  size_t chunk_cap = 0;
+  double* d_scratch = nullptr;
+  size_t scratch_cap = 0;
+  unsigned* d_visited = nullptr;
+  size_t visited_cap = 0;
+  unsigned* d_counter = nullptr;
+  double* d_result = nullptr;
+  std::mutex mu;
+  int occ[3][SUP_MAX_N + 1] = {};
+};
+
+static std::mutex g_ctx_mu;
+static std::vector<std::unique_ptr<DeviceCtx>> g_ctx;
+
+int device_count(int* n) {
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *n = 0;
+    set_error(std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    return SUP_ENODEV;
+  }
+  *n = c;
+  return SUP_OK;
+}
+
+static int get_ctx(int dev, DeviceCtx** out) {
+  int cnt = 0;
+  if (device_count(&cnt) != SUP_OK || cnt == 0) {
+    set_error("no HIP device available (the engine has no CPU fallback for GPU algorithms)");
+    return SUP_ENODEV;
+  }
+  if (dev < 0 || dev >= cnt) {
+    set_error("device id " + std::to_string(dev) + " out of range (" + std::to_string(cnt) + " devices)");
+    return SUP_ENODEV;
+  }
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  if (g_ctx.size() < (size_t)cnt) g_ctx.resize(cnt);
+  if (!g_ctx[dev]) {
+    auto c = std::make_unique<DeviceCtx>();
+    c->dev = dev;
+    SUP_HIP(hipSetDevice(dev));
+    hipDeviceProp_t prop;
+    SUP_HIP(hipGetDeviceProperties(&prop, dev));
+    c->cus = prop.multiProcessorCount;
+    SUP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    SUP_HIP(hipEventCreate(&c->ev0));
+    SUP_HIP(hipEventCreate(&c->ev1));
+    SUP_HIP(hipMalloc(&c->d_x0, SUP_MAX_N * sizeof(double)));
+    SUP_HIP(hipMalloc(&c->d_nblk, SUP_MAX_N * sizeof(int)));
+    SUP_HIP(hipMalloc(&c->d_rowmask, SUP_MAX_N * sizeof(uint64_t)));
+    SUP_HIP(hipMalloc(&c->d_counter, 64));
+    SUP_HIP(hipMalloc(&c->d_result, 64));
+    g_ctx[dev] = std::move(c);
+  }
+  *out = g_ctx[dev].get();
+  return SUP_OK;
+}
+
+template <class T>
+static int ensure(T*& p, size_t& cap, size_t need) {
+  if (need <= cap) return SUP_OK;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  hipError_t e = hipMalloc(&p, need * sizeof(T));
+  if (e != hipSuccess) {
+    set_error(std::string("hipMalloc: ") + hipGetErrorString(e));
+    return SUP_ENOMEM;
+  }
+  cap = need;
+  return SUP_OK;
+}
+
+int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visited, RangeResult& r) {
+  r = RangeResult();
+  if (c1 <= c0) return SUP_OK;  // empty range: partial 0
+  if (c1 > P.lay.chunks()) {
+    set_error("wave-chunk range exceeds the plan");
+    return SUP_EINVAL;
+  }
+  DeviceCtx* c = nullptr;
+  int rc = get_ctx(dev, &c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(c->mu);
+  SUP_HIP(hipSetDevice(dev));
+  const uint64_t count = c1 - c0;
+  if ((rc = ensure(c->d_cols, c->cols_cap, P.cols.size()))) return rc;
+  if ((rc = ensure(c->d_chunk, c->chunk_cap, (size_t)count))) return rc;
+  if ((rc = ensure(c->d_scratch, c->scratch_cap, (size_t)pairwise_scratch_size(count)))) return rc;
+  const bool visited = want_visited && P.kind == kWalkSkip;
+  if (visited && (rc = ensure(c->d_visited, c->visited_cap, (size_t)count))) return rc;
+
+  hipStream_t s = c->stream;
+  SUP_HIP(hipMemcpyAsync(c->d_cols, P.cols.data(), P.cols.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  SUP_HIP(hipMemcpyAsync(c->d_x0, P.x0.data(), P.x0.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  SUP_HIP(hipMemcpyAsync(c->d_nblk, P.nblk.data(), P.nblk.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  SUP_HIP(hipMemcpyAsync(c->d_rowmask, P.rowmask.data(), P.rowmask.size() * sizeof(uint64_t),
+                         hipMemcpyHostToDevice, s));
+  SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
+
+  int& occ = c->occ[P.kind][P.n];
+  if (occ == 0) {
+    int b = 0;
+    SUP_HIP(walk_occupancy(P.kind, P.n, &b));
+    occ = b > 0 ? b : 1;
+  }
+  const uint64_t waves_needed = count;
+  uint64_t grid = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint64_t resident = (uint64_t)c->cus * (uint64_t)occ;
+  if (grid > resident) grid = resident;
+  if (grid < 1) grid = 1;
+
+  WalkParams p{};
+  p.cols = c->d_cols;
+  p.x0 = c->d_x0;
+  p.nblk = c->d_nblk;
+  p.rowmask = c->d_rowmask;
+  p.chunk_begin = c0;
+  p.chunk_count = count;
+  p.L = P.lay.L;
+  p.m = P.lay.m;
+  p.n = P.n;
+  p.umask = P.umask;
+  p.chunk_out = c->d_chunk;
+  p.counter = c->d_counter;
+  p.visited = visited ? c->d_visited : nullptr;
+
+  SUP_HIP(hipEventRecord(c->ev0, s));
+  SUP_HIP(launch_walk(P.kind, P.n, p, (int)grid, s));
+  SUP_HIP(hipEventRecord(c->ev1, s));
+  SUP_HIP(launch_pairwise_reduce(c->d_chunk, count, c->d_scratch, c->d_result, s));
+  double result = 0.0;
+  SUP_HIP(hipMemcpyAsync(&result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
+  std::vector<unsigned> vis;
+  if (visited) {
+    vis.resize(count);
+    SUP_HIP(hipMemcpyAsync(vis.data(), c->d_visited, count * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  }
+  SUP_HIP(hipStreamSynchronize(s));
+  float ms = 0.f;
+  SUP_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  r.partial = result;
+  r.kernel_ms = ms;
+  r.grid = (int)grid;
+  if (visited) {
+    uint64_t tot = 0;
+    for (unsigned v : vis) tot += v;
+    r.visited = tot * (uint64_t)(1ull << P.lay.L);
+  } else {
+    r.visited = count << (P.lay.L + P.lay.m);
+  }
+  return SUP_OK;
+}
+
+// ------------------------------------------------------------------ RCCL --
+int rccl_allreduce_partials(const std::vector<int>& devs, std::vector<double>& vals, double* out) {
+  const int G = (int)devs.size();
+  std::vector<ncclComm_t> comms(G);
+  ncclResult_t nr = ncclCommInitAll(comms.data(), G, devs.data());
+  if (nr != ncclSuccess) {
+    set_error(std::string("ncclCommInitAll: ") + ncclGetErrorString(nr));
+    return SUP_ERCCL;
+  }
+  std::vector<double*> buf(G, nullptr);
+  std::vector<hipStream_t> st(G, nullptr);
+  int rc = SUP_OK;
+  for (int g = 0; g < G && rc == SUP_OK; ++g) {
+    if (hipSetDevice(devs[g]) != hipSuccess || hipMalloc(&buf[g], sizeof(double)) != hipSuccess ||
+        hipStreamCreate(&st[g]) != hipSuccess ||
+        hipMemcpy(buf[g], &vals[g], sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+      set_error("RCCL staging buffer setup failed");
+      rc = SUP_EHIP;
+    }
+  }
+  if (rc == SUP_OK) {
+    ncclGroupStart();
+    for (int g = 0; g < G; ++g) {
+      nr = ncclAllReduce(buf[g], buf[g], 1, ncclFloat64, ncclSum, comms[g], st[g]);
+      if (nr != ncclSuccess) break;
+    }
+    ncclResult_t ge = ncclGroupEnd();
+    if (nr != ncclSuccess || ge != ncclSuccess) {
+      set_error(std::string("ncclAllReduce: ") + ncclGetErrorString(nr != ncclSuccess ? nr : ge));
+      rc = SUP_ERCCL;
+    }
+  }
+  if (rc == SUP_OK) {
+    for (int g = 0; g < G; ++g) {
+      if (hipSetDevice(devs[g]) != hipSuccess || hipStreamSynchronize(st[g]) != hipSuccess) rc = SUP_EHIP;
+    }
+    (void)hipSetDevice(devs[0]);
+    if (hipMemcpy(out, buf[0], sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) rc = SUP_EHIP;
+  }
+  for (int g = 0; g < G; ++g) {
+    (void)hipSetDevice(devs[g]);
+    if (buf[g]) (void)hipFree(buf[g]);
+    if (st[g]) (void)hipStreamDestroy(st[g]);
+    ncclCommDestroy(comms[g]);
+  }
+  return rc;
+}
+
+// ------------------------------------------------------------ schedulers --
+int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uint64_t c1,
+             SchedResult& out) {
+  out = SchedResult();
+  int ndev = 0;
+  int rc = device_count(&ndev);
+  if (rc) return rc;
+  if (ndev == 0) {
+    set_error("no HIP device available (the engine has no CPU fallback for GPU algorithms)");
+    return SUP_ENODEV;
+  }
+  int G = (sched == SUP_SCHED_SINGLE) ? 1 : std::max(1, o.gpu_num);
+  if (o.device_id < 0 || o.device_id + G > ndev) {
+    set_error("requested devices [" + std::to_string(o.device_id) + ", " + std::to_string(o.device_id + G) +
+              ") but only " + std::to_string(ndev) + " are visible");
+    return SUP_ENODEV;
+  }
+  std::vector<int> devs(G);
+  for (int g = 0; g < G; ++g) devs[g] = o.device_id + g;
+  const uint64_t total = c1 - c0;
+  const bool want_visited = true;
+
+  if (sched != SUP_SCHED_CHUNKS) {
+    // single device, or a static contiguous split (-p5)
+    std::vector<RangeResult> rr(G);
+    std::vector<int> rcs(G, SUP_OK);
+    auto work = [&](int g) {
+      const uint64_t a = c0 + total * (uint64_t)g / (uint64_t)G;
+      const uint64_t b = c0 + total * (uint64_t)(g + 1) / (uint64_t)G;
+      auto t0 = std::chrono::steady_clock::now();
+      rcs[g] = run_range(devs[g], P, a, b, want_visited, rr[g]);
+      if (o.verbose) {
+        double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("kernel%d in %f\n", devs[g], s);
+      }
+    };
+    if (G == 1) {
+      work(0);
+    } else {
+      std::vector<std::thread> th;
+      for (int g = 0; g < G; ++g) th.emplace_back(work, g);
+      for (auto& t : th) t.join();
+    }
+    for (int g = 0; g < G; ++g)
+      if (rcs[g]) return rcs[g];
+    out.dev_partials.resize(G);
+    for (int g = 0; g < G; ++g) {
+      out.dev_partials[g] = rr[g].partial;
+      out.kernel_ms = std::max(out.kernel_ms, rr[g].kernel_ms);
+      out.visited += rr[g].visited;
+      out.grid = std::max(out.grid, rr[g].grid);
+    }
+    out.devices = G;
+    if (G > 1 && o.use_rccl) {
+      rc = rccl_allreduce_partials(devs, out.dev_partials, &out.total);
+      if (rc) return rc;
+    } else {
+      out.total = pairwise_host(out.dev_partials);
+    }
+    return SUP_OK;
+  }
+
+  // Dynamic chunk queue (-p6 / -p8): power-of-two aligned items of wave-chunks,
+  // taken by one host thread per device (and optionally a CPU worker).  Item
+  // partials are combined in item order by the same pairwise tree, so the
+  // result does not depend on which device took which item.
+  uint64_t item = 1;
+  if (o.chunk_log2 > 0) {
+    item = 1ull << o.chunk_log2;
+  } else {
+    const uint64_t target_items = (uint64_t)G * 16;
+    while (item * 2 <= total && total / (item * 2) >= target_items) item <<= 1;
+  }
+  const uint64_t nitems = (total + item - 1) / item;
+  std::vector<double> ipart(nitems, 0.0);
+  std::vector<double> dev_ms(G + 1, 0.0);
+  std::vector<uint64_t> dev_vis(G + 1, 0);
+  std::vector<int> dev_grid(G + 1, 0);
+  std::vector<int> rcs(G + 1, SUP_OK);
+  std::vector<double> dev_sum(G, 0.0);
+  std::atomic<uint64_t> next{0};
+  std::atomic<int> cpu_items{0};
+  std::atomic<bool> failed{false};
+  auto gpu_worker = [&](int g) {
+    for (;;) {
+      if (failed.load()) return;
+      const uint64_t it = next.fetch_add(1);
+      if (it >= nitems) return;
+      const uint64_t a = c0 + it * item;
+      const uint64_t b = std::min(c1, a + item);
+      RangeResult r;
+      auto t0 = std::chrono::steady_clock::now();
+      int e = run_range(devs[g], P, a, b, want_visited, r);
+      if (e) {
+        rcs[g] = e;
+        failed.store(true);
+        return;
+      }
+      if (o.verbose) {
+        double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("ChunkID %llu is DONE by kernel%d in %f\n", (unsigned long long)it, devs[g], s);
+      }
+      ipart[it] = r.partial;
+      dev_sum[g] += r.partial;
+      dev_ms[g] += r.kernel_ms;
+      dev_vis[g] += r.visited;
+      dev_grid[g] = std::max(dev_grid[g], r.grid);
+    }
+  };
+  auto cpu_worker = [&]() {
+    for (;;) {
+      if (failed.load()) return;
+      const uint64_t it = next.fetch_add(1);
+      if (it >= nitems) return;
+      const uint64_t a = c0 + it * item;
+      const uint64_t b = std::min(c1, a + item);
+      auto t0 = std::chrono::steady_clock::now();
+      ipart[it] = cpu_walk_range(P, a, b, std::max(1, o.threads));
+      dev_vis[G] += (b - a) << (P.lay.L + P.lay.m);
+      cpu_items.fetch_add(1);
+      if (o.verbose) {
+        double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("ChunkID %llu is DONE by CPU in %f\n", (unsigned long long)it, s);
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int g = 0; g < G; ++g) th.emplace_back(gpu_worker, g);
+  if (o.cpu_worker) th.emplace_back(cpu_worker);
+  for (auto& t : th) t.join();
+  for (int g = 0; g <= G; ++g)
+    if (rcs[g]) return rcs[g];
+  out.devices = G;
+  out.cpu_items = cpu_items.load();
+  for (int g = 0; g <= G; ++g) {
+    out.kernel_ms = std::max(out.kernel_ms, dev_ms[g]);
+    out.visited += dev_vis[g];
+    out.grid = std::max(out.grid, dev_grid[g]);
+  }
+  out.dev_partials = dev_sum;
+  if (G > 1 && o.use_rccl && !o.cpu_worker) {
+    rc = rccl_allreduce_partials(devs, dev_sum, &out.total);
+    if (rc) return rc;
+  } else {
+    out.total = pairwise_host(ipart);
+  }
+  return SUP_OK;
+}
+
+}  // namespace sup

@@ -1,0 +1,223 @@
+// engine_cpu.cpp — the wave-chunk walk on host threads.
+//
+// Used for the CLI's explicit CPU algorithm (`-c`, reference RunAlgo cpu
+// branch main.cu:186-238) and as the hybrid CPU worker of the chunk queue
+// (`-c -g -p6`, reference gpu_exact_dense.cu:822-845).  It is never a
+// fallback for a GPU request: GPU entry points fail with SUP_ENODEV when no
+// device is present.  It simulates the 64 lanes of a wave and performs the
+// same fp64 operations in the same order as walk_{dense,sparse,skip}.hip, so
+// a chunk range gives bit-identical partials on CPU and GPU.
+#include <cmath>
+#include <thread>
+
+#include "engine.hpp"
+
+namespace sup {
+
+namespace {
+
+struct Lane {
+  double x[SUP_MAX_N];
+  double U[SUP_MAX_N / 8 + 2];
+};
+
+inline double prod4(const double* x, int n) {
+  double p0 = x[0];
+  double p1 = n > 1 ? x[1] : 1.0;
+  double p2 = n > 2 ? x[2] : 1.0;
+  double p3 = n > 3 ? x[3] : 1.0;
+  for (int j = 4; j < n; j += 4) {
+    p0 *= x[j];
+    if (j + 1 < n) p1 *= x[j + 1];
+    if (j + 2 < n) p2 *= x[j + 2];
+    if (j + 3 < n) p3 *= x[j + 3];
+  }
+  return (p0 * p1) * (p2 * p3);
+}
+
+inline double bprod8(const double* x, int n, int b) {
+  double v[8];
+  for (int i = 0; i < 8; ++i) v[i] = (8 * b + i < n) ? x[8 * b + i] : 1.0;
+  return ((v[0] * v[1]) * (v[2] * v[3])) * ((v[4] * v[5]) * (v[6] * v[7]));
+}
+
+inline void suffix_all(Lane& s, int n) {
+  const int NB = (n + 7) / 8;
+  s.U[NB] = 1.0;
+  for (int b = NB - 1; b >= 0; --b) s.U[b] = bprod8(s.x, n, b) * s.U[b + 1];
+}
+
+inline void sparse_step(Lane& s, int n, const double* col, int nb) {
+  const int NB = (n + 7) / 8;
+  for (int b = 0; b < NB && b < nb; ++b) {
+    const int hi = std::min(8 * b + 8, n);
+    for (int j = 8 * b; j < hi; ++j) s.x[j] += col[j];
+  }
+  for (int b = NB - 1; b >= 0; --b)
+    if (b < nb) s.U[b] = bprod8(s.x, n, b) * s.U[b + 1];
+}
+
+inline const double* col_of(const Plan& P, int e, int neg) {
+  return P.cols.data() + (size_t)(2 * e + neg) * P.NP;
+}
+
+void chunk_start(const Plan& P, uint64_t ga, unsigned lane, Lane& s) {
+  const int n = P.n, L = P.lay.L, m = P.lay.m;
+  for (int j = 0; j < n; ++j) s.x[j] = P.x0[j];
+  uint64_t h = ga ^ (ga >> 1);
+  while (h) {
+    const int b = __builtin_ctzll(h);
+    h &= h - 1;
+    const double* c = col_of(P, L + m + b, 0);
+    for (int j = 0; j < n; ++j) s.x[j] += c[j];
+  }
+  for (int e = 0; e < L; ++e) {
+    const double sel = ((lane >> e) & 1u) ? 1.0 : 0.0;
+    const double* c = col_of(P, e, 0);
+    for (int j = 0; j < n; ++j) s.x[j] = std::fma(sel, c[j], s.x[j]);
+  }
+}
+
+double pairwise64(double* v) {
+  for (int w = 64; w > 1; w >>= 1)
+    for (int i = 0; i < w / 2; ++i) v[i] = v[2 * i] + v[2 * i + 1];
+  return v[0];
+}
+
+inline uint32_t next_toggle(uint32_t t, uint32_t k) {
+  uint32_t c = ((t >> (k + 1)) << (k + 1)) + (1u << k);
+  if (c <= t) c += 2u << k;
+  return c;
+}
+
+// One wave-chunk: returns the wave's pairwise lane sum.
+double chunk_partial(const Plan& P, uint64_t ga) {
+  const int n = P.n, L = P.lay.L, m = P.lay.m;
+  const uint32_t T = 1u << m;
+  double lane_val[64];
+  if (P.kind != kWalkSkip) {
+    for (unsigned l = 0; l < 64; ++l) {
+      if (l >= (1u << L)) {
+        lane_val[l] = 0.0;
+        continue;
+      }
+      Lane s;
+      chunk_start(P, ga, l, s);
+      double acc;
+      if (P.kind == kWalkDense) {
+        acc = prod4(s.x, n);
+        for (uint32_t t = 1; t < T; ++t) {
+          const uint32_t k = __builtin_ctz(t);
+          const int neg = (t >> (k + 1)) & 1u;
+          const double* c = col_of(P, L + k, neg);
+          for (int j = 0; j < n; ++j) s.x[j] += c[j];
+          const double pr = prod4(s.x, n);
+          acc = (t & 1u) ? acc - pr : acc + pr;
+        }
+      } else {
+        suffix_all(s, n);
+        acc = s.U[0];
+        for (uint32_t t = 1; t < T; ++t) {
+          const uint32_t k = __builtin_ctz(t);
+          const int neg = (t >> (k + 1)) & 1u;
+          sparse_step(s, n, col_of(P, L + k, neg), P.nblk[L + k]);
+          acc = (t & 1u) ? acc - s.U[0] : acc + s.U[0];
+        }
+      }
+      const unsigned par = (unsigned)__builtin_popcount(l) & 1u;
+      if ((((unsigned)ga) ^ par) & 1u) acc = -acc;
+      lane_val[l] = acc;
+    }
+    return pairwise64(lane_val);
+  }
+  // SkipPer: all 64 lanes in lock-step, wave-uniform jumps (walk_skip.hip).
+  static thread_local Lane S[64];
+  double acc[64];
+  for (unsigned l = 0; l < 64; ++l) {
+    chunk_start(P, ga, l, S[l]);
+    suffix_all(S[l], n);
+    acc[l] = 0.0;
+  }
+  uint32_t t = 0;
+  for (;;) {
+    bool all_zero = true;
+    for (unsigned l = 0; l < 64; ++l) {
+      const double term = S[l].U[0];
+      acc[l] = (t & 1u) ? acc[l] - term : acc[l] + term;
+      if (term != 0.0) all_zero = false;
+    }
+    uint32_t next = t + 1;
+    if (all_zero) {
+      uint64_t zm = 0;
+      for (int r = 0; r < n; ++r)
+        if (S[0].x[r] == 0.0) zm |= 1ull << r;
+      zm &= P.umask;
+      if (zm) {
+        uint32_t target = t + 1;
+        while (zm) {
+          const int r = __builtin_ctzll(zm);
+          zm &= zm - 1;
+          uint64_t mm = P.rowmask[r];
+          uint32_t tr = T;
+          while (mm) {
+            const uint32_t k = __builtin_ctzll(mm);
+            mm &= mm - 1;
+            const uint32_t c = next_toggle(t, k);
+            tr = c < tr ? c : tr;
+          }
+          target = tr > target ? tr : target;
+        }
+        next = target;
+      }
+    }
+    if (next >= T) break;
+    const uint32_t gn = next ^ (next >> 1);
+    uint32_t diff = (t ^ (t >> 1)) ^ gn;
+    do {
+      const uint32_t k = __builtin_ctz(diff);
+      diff &= diff - 1;
+      const int neg = ((gn >> k) & 1u) ^ 1u;
+      for (unsigned l = 0; l < 64; ++l) sparse_step(S[l], n, col_of(P, L + k, neg), P.nblk[L + k]);
+    } while (diff);
+    t = next;
+  }
+  for (unsigned l = 0; l < 64; ++l) {
+    const unsigned par = (unsigned)__builtin_popcount(l) & 1u;
+    double a = acc[l];
+    if ((((unsigned)ga) ^ par) & 1u) a = -a;
+    lane_val[l] = (l < (1u << L)) ? a : 0.0;
+  }
+  return pairwise64(lane_val);
+}
+
+}  // namespace
+
+double cpu_walk_range(const Plan& P, uint64_t c0, uint64_t c1, int threads) {
+  if (c1 <= c0) return 0.0;
+  const uint64_t count = c1 - c0;
+  std::vector<double> part(count, 0.0);
+  const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(threads, 1), count));
+  std::vector<std::thread> th;
+  for (int w = 0; w < T; ++w)
+    th.emplace_back([&, w]() {
+      for (uint64_t a = w; a < count; a += (uint64_t)T) part[a] = chunk_partial(P, c0 + a);
+    });
+  for (auto& t : th) t.join();
+  // same 64-way zero-padded pairwise passes as launch_pairwise_reduce
+  while (part.size() > 1) {
+    const size_t groups = (part.size() + 63) / 64;
+    std::vector<double> nxt(groups);
+    for (size_t g = 0; g < groups; ++g) {
+      double v[64];
+      for (int l = 0; l < 64; ++l) {
+        const size_t i = g * 64 + l;
+        v[l] = i < part.size() ? part[i] : 0.0;
+      }
+      nxt[g] = pairwise64(v);
+    }
+    part.swap(nxt);
+  }
+  return part[0];
+}
+
+}  // namespace sup

@@ -1,0 +1,41 @@
+// kernels.hpp — host-visible launch entry points of the gfx950 walk kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "walk_params.hpp"
+
+namespace sup {
+
+// Per-N-range launchers (one translation unit per range, see Makefile).
+#define SUP_DECL_RANGE(KIND, LO)                                                      \
+  hipError_t launch_##KIND##_##LO(int n, const WalkParams& p, int grid, hipStream_t s); \
+  hipError_t occupancy_##KIND##_##LO(int n, int* blocks_per_cu);
+SUP_DECL_RANGE(dense, 1)
+SUP_DECL_RANGE(dense, 17)
+SUP_DECL_RANGE(dense, 33)
+SUP_DECL_RANGE(dense, 49)
+SUP_DECL_RANGE(sparse, 1)
+SUP_DECL_RANGE(sparse, 17)
+SUP_DECL_RANGE(sparse, 33)
+SUP_DECL_RANGE(sparse, 49)
+SUP_DECL_RANGE(skip, 1)
+SUP_DECL_RANGE(skip, 17)
+SUP_DECL_RANGE(skip, 33)
+SUP_DECL_RANGE(skip, 49)
+#undef SUP_DECL_RANGE
+
+enum WalkKind { kWalkDense = 0, kWalkSparse = 1, kWalkSkip = 2 };
+
+// Launch the walk kernel of `kind` for matrix order n (1..64).
+hipError_t launch_walk(WalkKind kind, int n, const WalkParams& p, int grid, hipStream_t s);
+// Resident 256-thread blocks per CU for that kernel (occupancy API).
+hipError_t walk_occupancy(WalkKind kind, int n, int* blocks_per_cu);
+
+// Fixed-order pairwise reduction of `count` doubles into *out (64-way passes,
+// zero padded; mirrored by oracle/oracle.c orc_pairwise_reduce).  `scratch`
+// must hold ceil(count/64) + ceil(count/4096) + ... doubles.
+hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scratch, double* out,
+                                  hipStream_t s);
+uint64_t pairwise_scratch_size(uint64_t count);
+
+}  // namespace sup

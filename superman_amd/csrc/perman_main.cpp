@@ -1,0 +1,218 @@
+// perman_main.cpp — the `perman` command line, a drop-in for the reference's
+// v1 CLI (main.cu:325-600): same short/long options, same algorithm ids, same
+// "Result: <name> <perm> in <sec>" line (cout default precision), plus a
+// full-precision "Permanent: %.17e" line (the legacy line has ~6 digits).
+//
+// Extensions (v2 semantics, revised_perman/main.cpp:1298-1476): -l <dev>
+// first device, -k <reps> repetitions; -R combine multi-GPU partials with RCCL;
+// -v reference-style per-kernel / per-chunk timing lines.
+#include <getopt.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "../../include/superman.h"
+
+namespace {
+
+struct Cli {
+  bool generic = true, dense = true, approximation = false, gpu = false, cpu = false, grid_graph = false;
+  bool rccl = false, verbose = false;
+  int gpu_num = 2, threads = 16, perman_algo = 1, preprocessing = 0, device = 0, reps = 1;
+  std::string filename;
+};
+
+int fail(const char* what) {
+  std::fprintf(stderr, "perman: %s: %s\n", what, sup_last_error());
+  return 1;
+}
+
+void report(const std::string& name, double perm, double sec) {
+  std::cout << "Result: " << name << " " << perm << " in " << sec << std::endl;
+  std::printf("Permanent: %.17e\n", perm);
+  std::fflush(stdout);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Cli c;
+  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rv";
+  const struct option long_options[] = {{"binary", 0, NULL, 'b'},       {"sparse", 0, NULL, 's'},
+                                        {"preprocessing", 1, NULL, 'r'}, {"threads", 1, NULL, 't'},
+                                        {"file", 1, NULL, 'f'},          {"gpu", 0, NULL, 'g'},
+                                        {"device", 1, NULL, 'd'},        {"cpu", 0, NULL, 'c'},
+                                        {"approximation", 0, NULL, 'a'}, {"perman", 1, NULL, 'p'},
+                                        {"numOfTimes", 1, NULL, 'x'},    {"scaleIntervals", 1, NULL, 'y'},
+                                        {"scaleTimes", 1, NULL, 'z'},    {"grid", 0, NULL, 'i'},
+                                        {"gridm", 1, NULL, 'm'},         {"gridn", 1, NULL, 'n'},
+                                        {"gpu-id", 1, NULL, 'l'},        {"reps", 1, NULL, 'k'},
+                                        {"rccl", 0, NULL, 'R'},          {"verbose", 0, NULL, 'v'},
+                                        {NULL, 0, NULL, 0}};
+  int opt;
+  auto need_arg = [&](char o) -> bool {
+    if (optarg[0] == '-') {
+      std::fprintf(stderr, "Option -%c requires an argument.\n", o);
+      return false;
+    }
+    return true;
+  };
+  while ((opt = getopt_long(argc, argv, short_options, long_options, NULL)) != -1) {
+    switch (opt) {
+      case 'b': c.generic = false; break;
+      case 's': c.dense = false; break;
+      case 'r': if (!need_arg('t')) return 1; c.preprocessing = std::atoi(optarg); break;
+      case 't': if (!need_arg('t')) return 1; c.threads = std::atoi(optarg); break;
+      case 'f': if (!need_arg('f')) return 1; c.filename = optarg; break;
+      case 'a': c.approximation = true; break;
+      case 'g': c.gpu = true; break;
+      case 'd': if (!need_arg('d')) return 1; c.gpu_num = std::atoi(optarg); break;
+      case 'c': c.cpu = true; break;
+      case 'p': if (!need_arg('p')) return 1; c.perman_algo = std::atoi(optarg); break;
+      case 'x': case 'y': case 'z': case 'm': case 'n':
+        if (!need_arg((char)opt)) return 1;  // approximation / grid parameters: accepted, unused
+        break;
+      case 'i': c.grid_graph = true; break;
+      case 'l': if (!need_arg('l')) return 1; c.device = std::atoi(optarg); break;
+      case 'k': if (!need_arg('k')) return 1; c.reps = std::max(1, std::atoi(optarg)); break;
+      case 'R': c.rccl = true; break;
+      case 'v': c.verbose = true; break;
+      case '?': return 1;
+      default: std::abort();
+    }
+  }
+  if (!c.grid_graph && c.filename.empty()) {
+    std::fprintf(stderr, "Option -f is a required argument.\n");
+    return 1;
+  }
+  for (int i = optind; i < argc; ++i) std::printf("Non-option argument %s\n", argv[i]);
+  if (!c.cpu && !c.gpu) c.gpu = true;  // main.cu:482-484
+  if (c.grid_graph || c.approximation) {
+    std::fprintf(stderr,
+                 "perman: approximation (-a) and grid-graph (-i) modes are outside this engine's scope "
+                 "(exact Ryser / Gray-code path only; see DESIGN.md)\n");
+    return 2;
+  }
+
+  void* mat = nullptr;
+  sup_dtype t;
+  int n = 0, nnz = 0;
+  if (sup_read_matrix(c.filename.c_str(), c.generic ? 0 : 1, &mat, &t, &n, &nnz) != SUP_OK)
+    return fail("reading matrix");
+  // main.cu:512-518 / 544-550 / 577-583: preprocessing rewrites mat.
+  std::vector<int> rp(n), cp(n);
+  if (c.preprocessing == 1) {
+    if (sup_sort_order(mat, t, n, cp.data()) != SUP_OK) return fail("SortOrder");
+  } else if (c.preprocessing == 2) {
+    if (sup_skip_order(mat, t, n, rp.data(), cp.data()) != SUP_OK) return fail("SkipOrder");
+  }
+
+  sup_opts o;
+  sup_opts_init(&o);
+  o.gpu_num = c.gpu_num;
+  o.device_id = c.device;
+  o.threads = c.threads;
+  o.cpu_worker = (c.gpu && c.cpu) ? 1 : 0;
+  o.use_rccl = c.rccl ? 1 : 0;
+  o.verbose = c.verbose ? 1 : 0;
+
+  std::string name;
+  sup_kernel kern = SUP_KERNEL_DENSE;
+  sup_sched sched = SUP_SCHED_SINGLE;
+  bool on_gpu = c.gpu;
+  const int a = c.perman_algo;
+  if (on_gpu) {
+    // main.cu:30-143 GPU exact dispatch
+    if (c.dense) {
+      static const char* names[] = {"gpu_perman64_xglobal", "gpu_perman64_xlocal", "gpu_perman64_xshared",
+                                    "gpu_perman64_xshared_coalescing",
+                                    "gpu_perman64_xshared_coalescing_mshared"};
+      if (a >= 0 && a <= 4) {
+        name = names[a];
+      } else if (a == 5) {
+        name = "gpu_perman64_xshared_coalescing_mshared_multigpu";
+        sched = SUP_SCHED_STATIC;
+      } else if (a == 6) {
+        name = "gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks";
+        sched = SUP_SCHED_CHUNKS;
+      } else if (a == 66) {
+        name = "gpu_perman64_xshared_coalescing_mshared_multigpu_manual_distribution";
+        sched = SUP_SCHED_STATIC;
+        o.gpu_num = 4;  // main.cu:75 hard-codes 4 devices
+      } else {
+        std::cout << "Unknown Algorithm ID" << std::endl;
+        sup_free(mat);
+        return 0;
+      }
+    } else {
+      static const char* names[] = {"", "gpu_perman64_xlocal_sparse", "gpu_perman64_xshared_sparse",
+                                    "gpu_perman64_xshared_coalescing_sparse",
+                                    "gpu_perman64_xshared_coalescing_mshared_sparse"};
+      kern = SUP_KERNEL_SPARYSER;
+      if (a >= 1 && a <= 4) {
+        name = names[a];
+      } else if (a == 5) {
+        name = "gpu_perman64_xshared_coalescing_mshared_multigpu_sparse";
+        sched = SUP_SCHED_STATIC;
+      } else if (a == 6) {
+        name = "gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_sparse";
+        sched = SUP_SCHED_CHUNKS;
+      } else if (a == 7) {
+        name = "gpu_perman64_xshared_coalescing_mshared_skipper";
+        kern = SUP_KERNEL_SKIPPER;
+      } else if (a == 8) {
+        name = "gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper";
+        kern = SUP_KERNEL_SKIPPER;
+        sched = SUP_SCHED_CHUNKS;
+      } else if (a == 66) {
+        name = "gpu_perman64_xshared_coalescing_mshared_multigpu_sparse_manual_distribution";
+        sched = SUP_SCHED_STATIC;
+        o.gpu_num = 4;
+      } else {
+        std::cout << "Unknown Algorithm ID" << std::endl;
+        sup_free(mat);
+        return 0;
+      }
+    }
+    if (sched == SUP_SCHED_SINGLE) o.gpu_num = 1;
+  } else {
+    // main.cu:186-238 CPU exact dispatch (dense ignores -p, main.cu:188)
+    if (c.dense) {
+      name = "parallel_perman64";
+    } else if (a == 1) {
+      name = "parallel_perman64_sparse";
+      kern = SUP_KERNEL_SPARYSER;
+    } else if (a == 2 || a == 3) {
+      name = a == 2 ? "parallel_skip_perman64_w" : "parallel_skip_perman64_w_balanced";
+      kern = SUP_KERNEL_SKIPPER;
+    } else {
+      sup_free(mat);
+      return 0;  // the reference prints nothing for other sparse CPU ids
+    }
+  }
+
+  for (int r = 0; r < c.reps; ++r) {
+    double perm = 0.0;
+    sup_stats st;
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = on_gpu ? sup_perman(mat, t, n, kern, sched, &o, &perm, &st)
+                    : sup_perman_cpu(mat, t, n, kern, c.threads, &perm, &st);
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (rc != SUP_OK) {
+      sup_free(mat);
+      return fail(name.c_str());
+    }
+    report(name, perm, sec);
+    if (c.verbose)
+      std::printf("Stats: kernel_ms %.3f gray_steps %llu visited %llu devices %d lanes %d walk %d grid %d\n",
+                  st.kernel_ms, (unsigned long long)st.gray_steps, (unsigned long long)st.visited_steps,
+                  st.devices_used, st.lane_bits, st.walk_bits, st.grid);
+  }
+  sup_free(mat);
+  return 0;
+}

@@ -1,0 +1,80 @@
+// reduce.hip — deterministic pairwise reduction of per-wave-chunk partials,
+// plus the N-range dispatch of the walk kernels.
+//
+// The reference sums per-thread partials on the host in thread order after a
+// 2-4 MiB D2H copy per launch (gpu_exact_dense.cu:685-693).  Here the
+// partials stay in HBM and are folded on the device by 64-way pairwise passes
+// (one wave per 64 values, ascending-xor butterfly), so only 8 bytes leave the
+// device and the result does not depend on grid size or device count.
+#include "kernels.hpp"
+#include "walk_common.hpp"
+
+namespace sup {
+
+__global__ __launch_bounds__(kBlock) void pairwise64_pass(const double* __restrict__ in, uint64_t count,
+                                                          double* __restrict__ out, uint64_t groups) {
+  const uint64_t g = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  if (g >= groups) return;  // whole wave exits together (g is wave-uniform)
+  const uint64_t i = g * 64u + lane;
+  const double v = (i < count) ? in[i] : 0.0;
+  const double s = wave_sum(v);
+  if (lane == 0) out[g] = s;
+}
+
+uint64_t pairwise_scratch_size(uint64_t count) {
+  uint64_t total = 0;
+  while (count > 1) {
+    count = (count + 63) / 64;
+    total += count;
+  }
+  return total + 1;
+}
+
+hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scratch, double* out,
+                                  hipStream_t s) {
+  if (count == 0) return hipMemsetAsync(out, 0, sizeof(double), s);
+  if (count == 1) return hipMemcpyAsync(out, in, sizeof(double), hipMemcpyDeviceToDevice, s);
+  const double* src = in;
+  double* dst = scratch;
+  while (count > 1) {
+    const uint64_t groups = (count + 63) / 64;
+    const uint64_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
+    double* target = (groups == 1) ? out : dst;
+    hipLaunchKernelGGL(pairwise64_pass, dim3((unsigned)blocks), dim3(kBlock), 0, s, src, count, target, groups);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    src = target;
+    dst = target + groups;
+    count = groups;
+  }
+  return hipSuccess;
+}
+
+#define SUP_DISPATCH(KIND, FN, ...)                 \
+  if (n <= 16) return FN##_##KIND##_1(__VA_ARGS__);   \
+  if (n <= 32) return FN##_##KIND##_17(__VA_ARGS__);  \
+  if (n <= 48) return FN##_##KIND##_33(__VA_ARGS__);  \
+  return FN##_##KIND##_49(__VA_ARGS__);
+
+hipError_t launch_walk(WalkKind kind, int n, const WalkParams& p, int grid, hipStream_t s) {
+  if (n < 1 || n > 64) return hipErrorInvalidValue;
+  switch (kind) {
+    case kWalkDense: { SUP_DISPATCH(dense, launch, n, p, grid, s) }
+    case kWalkSparse: { SUP_DISPATCH(sparse, launch, n, p, grid, s) }
+    case kWalkSkip: { SUP_DISPATCH(skip, launch, n, p, grid, s) }
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t walk_occupancy(WalkKind kind, int n, int* blocks_per_cu) {
+  if (n < 1 || n > 64) return hipErrorInvalidValue;
+  switch (kind) {
+    case kWalkDense: { SUP_DISPATCH(dense, occupancy, n, blocks_per_cu) }
+    case kWalkSparse: { SUP_DISPATCH(sparse, occupancy, n, blocks_per_cu) }
+    case kWalkSkip: { SUP_DISPATCH(skip, occupancy, n, blocks_per_cu) }
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace sup

@@ -1,0 +1,146 @@
+// walk_common.hpp — device-side building blocks of the gfx950 Ryser walk kernels.
+//
+// Work decomposition.  The reference walks the Gray index
+// space i in [1, 2^(n-1)) with one contiguous range per GPU thread
+// (gpu_exact_dense.cu:350-396).  Here the n-1 Gray bits are split into
+//   engine bits [0, L)        -> the 64 lanes of a wave (lane l owns pattern l),
+//   engine bits [L, L+m)      -> a Gray walk of 2^m steps that every lane of the
+//                                wave performs in lock-step (flipped column is
+//                                wave-uniform: k = ctz(t), computed on the SALU),
+//   engine bits [L+m, n-1)    -> the wave-chunk index a; subset part = gray(a).
+// A wave-chunk a therefore covers exactly the subsets {gray(i)} of the aligned
+// reference index block [a*2^(L+m), (a+1)*2^(L+m)) — so chunk partial sums
+// are comparable with the reference chunk helpers (gpu_exact_dense.cu:6-69).
+//
+// Because the flipped column is wave-uniform, the column is read with scalar
+// loads (s_load_dwordx16 into SGPRs) and consumed as the SGPR operand of
+// v_add_f64: no LDS traffic and no VALU address work on the hot loop.  X lives
+// in VGPRs (n fp64 values per lane).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "walk_params.hpp"
+
+namespace sup {
+
+// Constant address space pointer: uniform loads through it become s_load.
+typedef const __attribute__((address_space(4))) double cdbl;
+typedef const __attribute__((address_space(4))) int cint;
+
+// Hide a uniform address from LLVM's loop-invariant code motion: otherwise the
+// k = 0 columns (constant addresses) are hoisted out of the walk and pinned in
+// SGPRs, which spills.  "+s" keeps the value wave-uniform and in SGPRs.
+__device__ __forceinline__ cdbl* opaque_c(const double* base, uint32_t byte_off) {
+  uint64_t a = (uint64_t)base + byte_off;
+  asm volatile("" : "+s"(a));
+  return (cdbl*)a;
+}
+__device__ __forceinline__ cint* opaque_i(const int* base, uint32_t byte_off) {
+  uint64_t a = (uint64_t)base + byte_off;
+  asm volatile("" : "+s"(a));
+  return (cint*)a;
+}
+
+// x[LO..HI) += col[LO..HI)   (col wave-uniform -> SGPR operands)
+template <int N, int LO, int HI>
+__device__ __forceinline__ void add_rows(double (&x)[N], cdbl* col) {
+#pragma unroll
+  for (int j = LO; j < HI; ++j) x[j] += col[j];
+}
+
+// Full-column update.  Columns longer than 32 doubles are consumed in two
+// pieces with a scheduling fence between them so at most 64 SGPRs of column
+// data are live (SGPR budget is 102 per wave).
+template <int N>
+__device__ __forceinline__ void add_col(double (&x)[N], cdbl* col) {
+  if constexpr (N <= 32) {
+    add_rows<N, 0, N>(x, col);
+  } else {
+    add_rows<N, 0, 32>(x, col);
+    __builtin_amdgcn_sched_barrier(0);
+    add_rows<N, 32, N>(x, col);
+  }
+}
+
+// Canonical dense product (mirrored bit-for-bit by oracle/oracle.c
+// orc_engine_prod): four strided partial products p_r = x_r * x_{r+4} * ...,
+// combined as (p0*p1)*(p2*p3).  Missing partials are 1.0 (folded away).
+template <int N>
+__device__ __forceinline__ double prod4(const double (&x)[N]) {
+  double p0 = x[0];
+  double p1 = N > 1 ? x[1 < N ? 1 : 0] : 1.0;
+  double p2 = N > 2 ? x[2 < N ? 2 : 0] : 1.0;
+  double p3 = N > 3 ? x[3 < N ? 3 : 0] : 1.0;
+#pragma unroll
+  for (int j = 4; j < N; j += 4) {
+    p0 *= x[j];
+    if (j + 1 < N) p1 *= x[j + 1 < N ? j + 1 : 0];
+    if (j + 2 < N) p2 *= x[j + 2 < N ? j + 2 : 0];
+    if (j + 3 < N) p3 *= x[j + 3 < N ? j + 3 : 0];
+  }
+  return (p0 * p1) * (p2 * p3);
+}
+
+// Product of the rows of 8-row block b (rows [8b, min(8b+8, N))):
+// ((x0*x1)*(x2*x3)) * ((x4*x5)*(x6*x7)), missing rows = 1.0.
+template <int N, int B>
+__device__ __forceinline__ double bprod8(const double (&x)[N]) {
+  constexpr int r0 = 8 * B;
+  auto v = [&](int i) -> double { return (r0 + i < N) ? x[(r0 + i < N) ? r0 + i : 0] : 1.0; };
+  return ((v(0) * v(1)) * (v(2) * v(3))) * ((v(4) * v(5)) * (v(6) * v(7)));
+}
+
+// 64-lane pairwise sum.  Offsets ascend (xor 1, 2, ..., 32), so lane 0 ends
+// with the pairwise tree ((v0+v1)+(v2+v3))+... ; every lane holds the same
+// value (IEEE addition is commutative).  Mirrored by oracle/oracle.c
+// orc_pairwise64.
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 1; off <= 32; off <<= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Dynamic wave-chunk queue: lane 0 takes the next chunk, the wave shares it.
+// Which wave computes a chunk does not affect the result: every chunk writes
+// its own slot of chunk_out, reduced afterwards in a fixed pairwise order.
+__device__ __forceinline__ uint32_t next_chunk(unsigned int* counter) {
+  uint32_t a = 0;
+  if ((threadIdx.x & 63) == 0) a = atomicAdd(counter, 1u);
+  return __builtin_amdgcn_readfirstlane(a);
+}
+
+// Lane-bit initialisation: x += col(e) on the lanes whose bit e is set.
+// The column is wave-uniform (SGPR operands).  fma(sel, c, x) with sel in
+// {0.0, 1.0} rounds exactly like x + (sel ? c : 0.0) for finite c — one VALU
+// op per element and no divergent control flow.
+template <int N>
+__device__ __forceinline__ void add_col_masked(double (&x)[N], cdbl* col, bool on) {
+  const double sel = on ? 1.0 : 0.0;
+#pragma unroll
+  for (int j = 0; j < N; ++j) x[j] = __builtin_fma(sel, col[j], x[j]);
+}
+
+// Start state of lane `lane` in wave-chunk `ga`:
+//   x = x0 + sum_{b in gray(ga)} col(L+m+b) + sum_{e in lane, e < L} col(e)
+// applied in exactly this order (ascending b, then ascending e); mirrored by
+// oracle/oracle.c orc_engine_start.
+template <int N>
+__device__ __forceinline__ void chunk_start(double (&x)[N], const WalkParams& p, uint64_t ga,
+                                            uint32_t lane) {
+  constexpr int NP = pad8(N);
+  cdbl* x0 = opaque_c(p.x0, 0);
+#pragma unroll
+  for (int j = 0; j < N; ++j) x[j] = x0[j];
+  uint64_t h = ga ^ (ga >> 1);
+  const uint32_t hb = (uint32_t)(p.L + p.m);
+  while (h) {
+    const uint32_t b = (uint32_t)__builtin_ctzll(h);
+    h &= h - 1;
+    add_col<N>(x, opaque_c(p.cols, (2u * (hb + b)) * NP * 8u));
+  }
+  for (int e = 0; e < p.L; ++e)
+    add_col_masked<N>(x, opaque_c(p.cols, (2u * e) * NP * 8u), (lane >> e) & 1u);
+}
+
+}  // namespace sup

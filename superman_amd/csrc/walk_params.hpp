@@ -1,0 +1,31 @@
+// walk_params.hpp — launch parameters shared by host and the gfx950 walk kernels.
+#pragma once
+#include <stdint.h>
+
+namespace sup {
+
+constexpr int kBlock = 256;  // threads per workgroup (4 waves)
+constexpr int kWavesPerBlock = kBlock / 64;
+
+// Pad n up to a multiple of 8 doubles (64 B) so every column starts on an
+// s_load_dwordx16 boundary.
+constexpr int pad8(int n) { return (n + 7) & ~7; }
+
+struct WalkParams {
+  const double* cols;              // signed column table: entry (2*e + neg) * NP + j, e = engine bit
+  const double* x0;                // NP doubles: Nijenhuis-Wilf start vector (rows in engine order)
+  const int* nblk;                 // sparse kernels: per engine bit, # of 8-row blocks the prefix touches
+  const uint64_t* rowmask;         // skipper: per row, walk-bit mask of the columns touching the row
+  unsigned long long chunk_begin;  // first wave-chunk (global index)
+  unsigned long long chunk_count;  // wave-chunks in this launch
+  int L;                           // lane bits (<= 6)
+  int m;                           // walk bits
+  int n;                           // matrix order (runtime copy, for tables)
+  int pad_;
+  unsigned long long umask;        // skipper: bit r set <=> row r is lane-uniform (no lane column touches it)
+  double* chunk_out;               // [chunk_count] per-wave-chunk partial sums
+  unsigned int* counter;           // dynamic wave-chunk queue head (zeroed before launch)
+  unsigned int* visited;           // optional [chunk_count]: product evaluations per chunk (skipper)
+};
+
+}  // namespace sup

@@ -1,0 +1,177 @@
+// walk_skip.hip — SkipPer walk for gfx950 (wave-uniform zero-row skipping).
+//
+// Replaces kernel_xshared_coalescing_mshared_skipper (reference
+// gpu_exact_sparse.cu:555-670; CPU form revised_perman/cpu_algos.hpp:1035-1213).
+// The reference lets every GPU thread jump independently: when x_r == 0 for the
+// last zero row r, the term stays 0 until a column of row r flips, so it jumps
+// i to the next toggle of any such column (gpu_exact_sparse.cu:648-666).
+// Independent per-thread jumps diverge on a 64-wide SIMD.  Here the jump is
+// taken by the whole wave, and only on rows whose value is the same on every
+// lane ("lane-uniform" rows: rows no lane column touches — SkipOrder puts the
+// sparsest columns on the lane bits, so most rows qualify):
+//   * a step's products are checked with one ballot; only if all 64 lanes are
+//     zero are the lane-uniform rows scanned for an exact zero;
+//   * the wave jumps to the LATEST next-toggle over all zero uniform rows
+//     (the product is zero until every one of them has changed), which is at
+//     least the reference's jump (it uses only the last zero row);
+//   * skipped terms are exactly zero (x_r stays exactly 0 until a column of
+//     row r flips), so the sum is unchanged.
+// Rows are prefix-blocked exactly as in walk_sparse.hip.
+#include "walk_common.hpp"
+#include "kernels.hpp"
+
+namespace sup {
+
+template <int B, int NB, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < NB) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, NB>(f);
+  }
+}
+template <int B, class F>
+__device__ __forceinline__ void static_for_down(F&& f) {
+  if constexpr (B >= 0) {
+    f(std::integral_constant<int, B>{});
+    static_for_down<B - 1>(f);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void skip_step(double (&x)[N], double (&U)[(N + 7) / 8 + 1], cdbl* col, int nb) {
+  constexpr int NB = (N + 7) / 8;
+  static_for<0, NB>([&](auto Bc) {
+    constexpr int b = decltype(Bc)::value;
+    constexpr int lo = 8 * b;
+    constexpr int hi = (8 * b + 8 < N) ? 8 * b + 8 : N;
+    if (b < nb) add_rows<N, lo, hi>(x, col);
+  });
+  static_for_down<NB - 1>([&](auto Bc) {
+    constexpr int b = decltype(Bc)::value;
+    if (b < nb) U[b] = bprod8<N, b>(x) * U[b + 1];
+  });
+}
+
+// Next walk index t' > t at which walk bit k toggles (ctz(t') == k).
+__device__ __forceinline__ uint32_t next_toggle(uint32_t t, uint32_t k) {
+  const uint32_t period = 2u << k;
+  uint32_t c = ((t >> (k + 1)) << (k + 1)) + (1u << k);
+  if (c <= t) c += period;
+  return c;
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
+  constexpr int NP = pad8(N);
+  constexpr int NB = (N + 7) / 8;
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool lane_valid = lane < (1u << p.L);
+  const uint32_t lane_par = __builtin_popcount(lane) & 1u;
+  const uint32_t T = 1u << p.m;
+  const uint32_t offL = 2u * (uint32_t)p.L * NP * 8u;
+  const uint32_t Lb = (uint32_t)p.L;
+  const uint64_t umask = p.umask;  // lane-uniform rows
+
+  for (uint32_t a = next_chunk(p.counter); a < p.chunk_count; a = next_chunk(p.counter)) {
+    const uint64_t ga = p.chunk_begin + a;
+    double x[N];
+    chunk_start<N>(x, p, ga, lane);
+    double U[NB + 1];
+    U[NB] = 1.0;
+    static_for_down<NB - 1>([&](auto Bc) {
+      constexpr int b = decltype(Bc)::value;
+      U[b] = bprod8<N, b>(x) * U[b + 1];
+    });
+    double acc = 0.0;
+    uint32_t visited = 0;
+    uint32_t t = 0;
+    while (true) {
+      // state t: X is valid for walk index t
+      ++visited;
+      const double term = U[0];
+      acc = (t & 1u) ? acc - term : acc + term;
+      uint32_t next = t + 1;
+      if (__builtin_amdgcn_ballot_w64(term != 0.0) == 0) {
+        // every lane is zero: look for exact zeros on lane-uniform rows.  Those
+        // rows hold the same value on every lane, so lane 0's view decides.
+        uint32_t zlo = 0, zhi = 0;
+#pragma unroll
+        for (int r = 0; r < N; ++r) {
+          if (r < 32) zlo |= (x[r] == 0.0) ? (1u << (r & 31)) : 0u;
+          else zhi |= (x[r] == 0.0) ? (1u << (r & 31)) : 0u;
+        }
+        uint64_t zm = ((uint64_t)__builtin_amdgcn_readfirstlane(zhi) << 32) |
+                      (uint64_t)__builtin_amdgcn_readfirstlane(zlo);
+        zm &= umask;
+        if (zm) {
+          // each zero row r stays zero until one of its walk columns toggles
+          // (or for the rest of the chunk if it has none); the product is zero
+          // until the last of those toggles.
+          uint32_t target = t + 1;
+          while (zm) {
+            const uint32_t r = (uint32_t)__builtin_ctzll(zm);
+            zm &= zm - 1;
+            uint64_t mm = ((const __attribute__((address_space(4))) uint64_t*)p.rowmask)[r];
+            uint32_t tr = T;
+            while (mm) {
+              const uint32_t k = (uint32_t)__builtin_ctzll(mm);
+              mm &= mm - 1;
+              const uint32_t c = next_toggle(t, k);
+              tr = c < tr ? c : tr;
+            }
+            target = tr > target ? tr : target;
+          }
+          next = target;
+        }
+      }
+      if (next >= T) break;
+      // Gray move t -> next: flip the differing walk bits in ascending order
+      // (exactly one bit for an ordinary step; several after a jump).
+      const uint32_t gn = next ^ (next >> 1);
+      uint32_t diff = (t ^ (t >> 1)) ^ gn;
+      do {
+        const uint32_t k = (uint32_t)__builtin_ctz(diff);
+        diff &= diff - 1;
+        const uint32_t neg = ((gn >> k) & 1u) ^ 1u;
+        const int nbk = opaque_i(p.nblk, (Lb + k) * 4u)[0];
+        skip_step<N>(x, U, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nbk);
+      } while (diff);
+      t = next;
+    }
+    if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;
+    const double part = wave_sum(lane_valid ? acc : 0.0);
+    if (lane == 0) {
+      p.chunk_out[a] = part;
+      if (p.visited) p.visited[a] = visited;
+    }
+  }
+}
+
+template <int N, int HI>
+static hipError_t launch_rec(int n, const WalkParams& p, int grid, hipStream_t s) {
+  if (n == N) {
+    hipLaunchKernelGGL(walk_skip<N>, dim3(grid), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
+  }
+  if constexpr (N < HI) return launch_rec<N + 1, HI>(n, p, grid, s);
+  return hipErrorInvalidValue;
+}
+
+template <int N, int HI>
+static hipError_t occ_rec(int n, int* blocks_per_cu) {
+  if (n == N) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_skip<N>, kBlock, 0);
+  if constexpr (N < HI) return occ_rec<N + 1, HI>(n, blocks_per_cu);
+  return hipErrorInvalidValue;
+}
+
+#define SUP_CAT2(a, b) a##b
+#define SUP_CAT(a, b) SUP_CAT2(a, b)
+
+hipError_t SUP_CAT(launch_skip_, SUP_N_LO)(int n, const WalkParams& p, int grid, hipStream_t s) {
+  return launch_rec<SUP_N_LO, SUP_N_HI>(n, p, grid, s);
+}
+hipError_t SUP_CAT(occupancy_skip_, SUP_N_LO)(int n, int* blocks_per_cu) {
+  return occ_rec<SUP_N_LO, SUP_N_HI>(n, blocks_per_cu);
+}
+
+}  // namespace sup

@@ -1,0 +1,109 @@
+"""The C-ABI boundary: library loads, exports every symbol include/superman.h
+declares, reports errors through codes + sup_last_error, and the GPU entry
+points refuse to run without a device (no CPU fallback)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, fixture_path
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "superman.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(sup_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_exports_every_declared_symbol(sup):
+    lib = sup._lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(sup._lib.EXPORTS) == syms
+
+
+def test_exports_visible_to_nm(sup):
+    out = subprocess.run(["nm", "-D", "--defined-only", sup._lib.LIB_PATH], capture_output=True, text=True).stdout
+    for s in header_symbols():
+        assert re.search(rf"\bT {s}$", out, re.M), s
+
+
+def test_library_holds_gfx950_code(sup):
+    # the fat binary embeds code objects for amdgcn-amd-amdhsa--gfx950 only
+    data = open(sup._lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    for other in (b"--gfx906", b"--gfx90a", b"--gfx942"):
+        assert other not in data
+
+
+def test_error_codes(sup):
+    lib = sup._lib.load()
+    out = C.c_double()
+    a = np.ones((3, 3))
+    rc = lib.sup_perman_cpu(a.ctypes.data, 2, 0, 0, 1, C.byref(out), None)
+    assert rc == -1 and b"outside" in lib.sup_last_error()
+    rc = lib.sup_perman_cpu(a.ctypes.data, 2, 65, 0, 1, C.byref(out), None)
+    assert rc == -1
+    rc = lib.sup_perman_cpu(None, 2, 3, 0, 1, C.byref(out), None)
+    assert rc == -1
+    with pytest.raises(ValueError):
+        sup.perman(np.ones((2, 3)))
+    with pytest.raises(sup.SupError):
+        sup.perman(np.ones((3, 3)), algo=9)
+
+
+def test_partial_range_validation(sup):
+    if sup.device_count() > 0:
+        pytest.skip("GPU present: covered by the gpu tests")
+    with pytest.raises(sup.SupError) as e:
+        sup.partial(np.ones((10, 10)), 3, 64)
+    assert e.value.code == -1
+
+
+def test_gpu_entry_points_fail_loudly_without_device(sup):
+    if sup.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(sup.SupError) as e:
+        sup.perman(np.ones((8, 8)), algo=4)
+    assert e.value.code == -2  # SUP_ENODEV: never a silent CPU fallback
+    with pytest.raises(sup.SupError):
+        sup.gpu_perman64_xshared_coalescing_mshared_skipper(np.ones((8, 8)))
+
+
+def test_cli_cpu_mode(sup):
+    exe = sup._lib.PERMAN_BIN
+    r = subprocess.run([exe, "-f", fixture_path("synth/12_0.50_int"), "-c", "-t", "4"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert lines[0].startswith("Result: parallel_perman64 ")
+    val = float(lines[1].split()[1])
+    a, _, _ = sup.read_matrix(fixture_path("synth/12_0.50_int"))
+    assert val == sup.perman_cpu(a, "dense", 2)
+
+
+def test_cli_rejects_out_of_scope_and_missing_file(sup):
+    exe = sup._lib.PERMAN_BIN
+    r = subprocess.run([exe, "-f", fixture_path("synth/12_0.50_int"), "-a"], capture_output=True, text=True)
+    assert r.returncode == 2
+    r = subprocess.run([exe, "-c"], capture_output=True, text=True)
+    assert r.returncode == 1 and "required" in r.stderr
+    r = subprocess.run([exe, "-f", "/nonexistent", "-c"], capture_output=True, text=True)
+    assert r.returncode == 1
+
+
+def test_cli_sparse_cpu_ids(sup):
+    exe = sup._lib.PERMAN_BIN
+    f = fixture_path("synth/16_0.20_int")
+    outs = {}
+    for p, name in ((1, "parallel_perman64_sparse"), (2, "parallel_skip_perman64_w"),
+                    (3, "parallel_skip_perman64_w_balanced")):
+        r = subprocess.run([exe, "-f", f, "-c", "-s", "-r2", f"-p{p}", "-t2"], capture_output=True, text=True)
+        assert r.returncode == 0 and r.stdout.startswith(f"Result: {name} "), r.stdout + r.stderr
+        outs[p] = float(r.stdout.splitlines()[1].split()[1])
+    assert abs(outs[1] - outs[3]) <= 1e-12 * abs(outs[1])

@@ -1,0 +1,199 @@
+"""GPU parity: the gfx950 kernels, called through the C ABI, against the oracle.
+
+* bit-exact against the oracle's mirror of the engine schedule (same fp64
+  operations in the same order) — dense, SpaRyser, SkipPer;
+* within fp64 tolerance of the reference's own results (golden.json) and of
+  the reference algorithm restated in oracle/ (orc_ref_*);
+* chunk partials against the reference chunk helpers' semantics
+  (gpu_exact_dense.cu:6-69 cpu_perman64 over [start, end));
+* at full benchmark size (n = 40), size-independent properties: bitwise row
+  scaling by powers of two, chunk-partial additivity, permutation invariance.
+"""
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import fixture_path, rel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu(sup):
+    if sup.device_count() < 1:
+        pytest.fail("no HIP device visible: -m gpu tests must run on the MI355X box")
+
+
+def _partial_layout(sup, n, s, e):
+    """Layout sup_partial uses for [s, e): the default one, with the walk
+    shortened until a wave-chunk divides both ends (capi.cpp sup_partial)."""
+    L, m, _ = sup.layout(n)
+    space = 1 << (n - 1)
+    al = min((n - 1) if v in (0, space) else (v & -v).bit_length() - 1 for v in (s, e))
+    return L, min(m, al - L)
+
+
+def _synth(sup, golden):
+    names = sorted({k.split("|")[0] for k in golden if k.startswith("synth/")})
+    return [(nm, sup.read_matrix(fixture_path(nm))[0]) for nm in names]
+
+
+KINDS = [("dense", 4, False), ("sparse", 4, True), ("skip", 7, True)]
+
+
+@pytest.mark.parametrize("kind,algo,sparse", KINDS)
+def test_bitexact_vs_engine_mirror(sup, orc, golden, kind, algo, sparse):
+    for name, a in _synth(sup, golden):
+        if kind == "skip":
+            a = sup.skip_order(a)[0]
+        got, st = sup.perman(a, algo=algo, sparse=sparse, return_stats=True)
+        want = orc.engine_perman(a, kind, 4)
+        assert got == want, (name, kind, got, want)
+        assert st["devices_used"] == 1 and st["kernel_ms"] > 0.0
+
+
+@pytest.mark.parametrize("kind,algo,sparse", KINDS)
+def test_matches_reference_goldens(sup, golden, kind, algo, sparse):
+    for name, a in _synth(sup, golden):
+        q = golden.get(f"{name}|dense_q|r0|b0|t4")
+        f = golden[f"{name}|dense|r0|b0|t4"]
+        b = sup.skip_order(a)[0] if kind == "skip" else a
+        got = sup.perman(b, algo=algo, sparse=sparse)
+        ref = q if q is not None else f
+        # as close to the quad golden as the reference's own fp64 result (or 1e-13)
+        assert abs(got - ref) <= max(4 * abs(f - ref), 1e-13 * abs(ref), 1e-12), (name, got, f, q)
+
+
+def test_known_answers(sup):
+    for n in (1, 2, 3, 7, 8, 12, 20, 24):
+        for algo, sparse in ((4, False), (4, True), (7, True)):
+            assert sup.perman(np.ones((n, n)), algo=algo, sparse=sparse) == pytest.approx(math.factorial(n),
+                                                                                          rel=1e-13)
+    p = np.eye(22)[np.random.default_rng(2).permutation(22)]
+    assert sup.perman(p) == 1.0
+    assert sup.perman(p, algo=7, sparse=True) == 1.0
+    z = np.random.default_rng(3).random((18, 18))
+    z[:, 5] = 0
+    assert sup.perman(z) == 0.0 and sup.perman(z, algo=4, sparse=True) == 0.0
+
+
+@pytest.mark.parametrize("name", ["int__30_0.50_0", "double__30_0.50_0", "float__30_0.50_0",
+                                  "double__30_0.20_0", "int__30_0.20_0"])
+def test_corpus_n30(sup, orc, golden, name):
+    a, typ, _ = sup.read_matrix(fixture_path(name))
+    got = sup.perman(a, algo=4)
+    assert got == orc.engine_perman(a, "dense", 16)
+    q = golden.get(f"{name}|dense_q|r0|b0|t8")
+    f = golden[f"{name}|dense|r0|b0|t8"]
+    assert rel(got, q if q is not None else f) < 1e-8
+    if q is not None:
+        assert abs(got - q) <= max(2 * abs(f - q), 1e-14 * abs(q))
+
+
+def test_sparse_orders_corpus(sup, orc, golden):
+    for name in ("double__30_0.20_0", "int__30_0.20_0"):
+        a, _, _ = sup.read_matrix(fixture_path(name))
+        s1 = sup.sort_order(a)[0]
+        s2 = sup.skip_order(a)[0]
+        g1 = sup.perman(s1, algo=4, sparse=True)
+        g2 = sup.perman(s2, algo=7, sparse=True)
+        assert g1 == orc.engine_perman(s1, "sparse", 16)
+        assert g2 == orc.engine_perman(s2, "skip", 16)
+        ref = golden.get(f"{name}|dense_q|r0|b0|t8", golden[f"{name}|sparse|r1|b0|t8"])
+        assert rel(g1, ref) < 1e-8 and rel(g2, ref) < 1e-8
+
+
+def test_partials_match_reference_chunk_helper(sup, orc):
+    # cpu_perman64 (gpu_exact_dense.cu:6-69) returns sum_{i in [s,e)} (-1)^i prod x(gray(i))
+    a, _, _ = sup.read_matrix(fixture_path("synth/22_0.50_double"))
+    n = 22
+    end = 1 << (n - 1)
+    for s, e in ((1 << 12, 1 << 14), (1 << 18, (1 << 18) + (1 << 16)), (1 << 20, end)):
+        got = sup.partial(a, s, e)
+        want = orc.ref_dense_partial(a, s, e, 4)
+        assert rel(got, want) < 1e-10, (s, e, got, want)
+        L, ml = _partial_layout(sup, n, s, e)
+        mir, _ = orc.engine_range(a, "dense", s >> (L + ml), e >> (L + ml), L, ml, True, 4)
+        assert got == mir
+    # index 0 carries the p0 term
+    x0, p0 = orc.nw_start(a)
+    g0 = sup.partial(a, 0, 64)
+    assert rel(g0, p0 + orc.ref_dense_partial(a, 1, 64, 1)) < 1e-12
+    with pytest.raises(sup.SupError):
+        sup.partial(a, 3, 64)
+
+
+@pytest.mark.parametrize("kind", ["sparse", "skip"])
+def test_sparse_partials(sup, orc, kind):
+    a, _, _ = sup.read_matrix(fixture_path("synth/22_0.20_int"))
+    a = sup.skip_order(a)[0]
+    s, e = 1 << 14, 1 << 17
+    got = sup.partial(a, s, e, kernel=kind)
+    fn = orc.ref_sparse_partial if kind == "sparse" else orc.ref_skip_partial
+    assert rel(got, fn(a, s, e, 4)) < 1e-9
+
+
+def test_schedulers_agree_bitwise(sup):
+    # -p4 / -p5 / -p6 and the reference-named wrappers give identical bits
+    # (fixed pairwise reduction over aligned power-of-two chunk ranges)
+    a, _, _ = sup.read_matrix(fixture_path("double__30_0.50_0"))
+    r4 = sup.perman(a, 4)
+    assert sup.perman(a, 5, gpu_num=1) == r4
+    assert sup.perman(a, 6, gpu_num=1) == r4
+    assert sup.perman(a, 6, gpu_num=1, chunk_log2=3) == r4
+    assert sup.gpu_perman64_xshared_coalescing_mshared(a) == r4
+    for algo in (0, 1, 2, 3):
+        assert sup.perman(a, algo) == r4
+
+
+def test_hybrid_cpu_worker(sup):
+    a, _, _ = sup.read_matrix(fixture_path("synth/22_0.50_double"))
+    r4 = sup.perman(a, 4)
+    r, st = sup.perman(a, 6, gpu_num=1, cpu=True, threads=4, chunk_log2=2, return_stats=True)
+    assert r == r4  # CPU worker items are bit-identical to GPU items
+
+
+def test_int_float_double_storage(sup):
+    rng = np.random.default_rng(11)
+    ai = rng.integers(0, 6, (21, 21)).astype(np.int32)
+    assert sup.perman(ai) == sup.perman(ai.astype(np.float64)) == sup.perman(ai.astype(np.float32))
+
+
+def test_n40_properties(sup):
+    # full benchmark size: properties that hold independent of a CPU oracle
+    a, _, _ = sup.read_matrix(fixture_path("double__40_0.50_0"))
+    r = sup.perman(a)
+    assert np.isfinite(r) and r > 0  # permanent of a nonnegative matrix
+    b = a.copy()
+    b[7] *= 2.0
+    b[31] *= 0.5
+    b[0] *= 4.0
+    assert sup.perman(b) == r * 4.0  # power-of-two row scaling is exact
+    # chunk partials add up (each aligned range is a subtree of the fixed reduction)
+    n = 40
+    q = 1 << (n - 3)
+    parts = [sup.partial(a, k * q, (k + 1) * q) for k in range(4)]
+    tot = ((parts[0] + parts[1]) + (parts[2] + parts[3]))
+    assert sup.partial(a, 0, 4 * q) == tot
+    # column permutation invariance (rounding-level)
+    perm = np.random.default_rng(5).permutation(n)
+    assert rel(sup.perman(a[:, perm]), r) < 1e-9
+
+
+def test_cli_gpu(sup, orc):
+    exe = sup._lib.PERMAN_BIN
+    f = fixture_path("double__30_0.50_0")
+    r = subprocess.run([exe, "-f", f, "-g", "-p4"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("Result: gpu_perman64_xshared_coalescing_mshared ")
+    val = float(r.stdout.splitlines()[1].split()[1])
+    a, _, _ = sup.read_matrix(f)
+    assert val == sup.perman(a)
+    r = subprocess.run([exe, "-f", fixture_path("int__30_0.20_0"), "-s", "-r2", "-p7"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "skipper" in r.stdout
+    r = subprocess.run([exe, "-f", f, "-g", "-p6", "-d1", "-v"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ChunkID" in r.stdout
