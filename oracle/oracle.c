@@ -395,6 +395,7 @@ void orc_engine_layout(int n, int* L, int* m, int* h) {
   int rest = nb - l;
   int mm = rest < 10 ? rest : 10;
   if (rest - 20 > mm) mm = rest - 20;
+  if (mm > 31) mm = 31;
   *L = l;
   *m = mm;
   *h = rest - mm;

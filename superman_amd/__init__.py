@@ -99,7 +99,7 @@ def layout(n: int) -> tuple[int, int, int]:
     nb = n - 1
     L = min(6, nb)
     rest = nb - L
-    m = max(min(rest, 10), rest - 20)
+    m = min(max(min(rest, 10), rest - 20), 31)
     return L, m, rest - m
 
 

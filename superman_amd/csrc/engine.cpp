@@ -77,6 +77,7 @@ Layout default_layout(int n) {
   // chunk queue balances a whole MI355X (~5k resident waves) to < 1 %.
   int m = rest < 10 ? rest : 10;
   if (rest - 20 > m) m = rest - 20;
+  if (m > 31) m = 31;  // 32-bit walk index in the kernels (n > 58 only)
   l.m = m;
   l.h = rest - m;
   return l;
@@ -297,7 +298,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     SUP_HIP(walk_occupancy(P.kind, P.n, &b));
     occ = b > 0 ? b : 1;
   }
-  const uint64_t waves_needed = count;
+  const uint64_t waves_needed = (count + kGroup - 1) / kGroup;  // one chunk group per wave at a time
   uint64_t grid = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
   const uint64_t resident = (uint64_t)c->cus * (uint64_t)occ;
   if (grid > resident) grid = resident;
@@ -317,6 +318,12 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   p.chunk_out = c->d_chunk;
   p.counter = c->d_counter;
   p.visited = visited ? c->d_visited : nullptr;
+  p.nb_lo = p.nb_hi = 0;
+  for (int k = 0; k < P.lay.m && k < 32; ++k) {
+    const uint64_t v = (uint64_t)(P.nblk[P.lay.L + k] & 15);
+    if (k < 16) p.nb_lo |= v << (4 * k);
+    else p.nb_hi |= v << (4 * (k - 16));
+  }
 
   SUP_HIP(hipEventRecord(c->ev0, s));
   SUP_HIP(launch_walk(P.kind, P.n, p, (int)grid, s));

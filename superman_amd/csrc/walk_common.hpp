@@ -101,6 +101,113 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// nblk of walk bit k (sparse kernels), unpacked on the SALU.
+__device__ __forceinline__ int nb_of(const WalkParams& p, uint32_t k) {
+  const uint64_t w = k < 16 ? p.nb_lo : p.nb_hi;
+  return (int)((w >> ((k & 15u) * 4u)) & 15u);
+}
+
+// Column rows [LO, HI) (LO a multiple of 8) fetched with scalar loads into
+// `c`, all issued before any use.  The empty asm pins every 8-double piece at
+// this point, so the loads are not sunk into the (uniform) branches that
+// consume them — one s_waitcnt per step instead of one per row block.
+typedef double dbl8 __attribute__((ext_vector_type(8)));
+template <int N, int LO, int HI>
+__device__ __forceinline__ void fetch_rows(cdbl* col, double (&c)[N]) {
+  typedef const __attribute__((address_space(4))) dbl8 cdbl8;
+  constexpr int B0 = LO / 8, P = (HI - LO + 7) / 8;  // P <= 4 pieces of 8 doubles
+  static_assert(P >= 1 && P <= 4, "fetch_rows handles 1..4 pieces");
+  cdbl8* v = (cdbl8*)col;
+  dbl8 t0 = v[B0], t1, t2, t3;
+  if constexpr (P > 1) t1 = v[B0 + 1];
+  if constexpr (P > 2) t2 = v[B0 + 2];
+  if constexpr (P > 3) t3 = v[B0 + 3];
+  // one pin for all pieces -> a single s_waitcnt
+  if constexpr (P == 1) asm volatile("" : "+s"(t0));
+  if constexpr (P == 2) asm volatile("" : "+s"(t0), "+s"(t1));
+  if constexpr (P == 3) asm volatile("" : "+s"(t0), "+s"(t1), "+s"(t2));
+  if constexpr (P == 4) asm volatile("" : "+s"(t0), "+s"(t1), "+s"(t2), "+s"(t3));
+  auto put = [&](int piece, const dbl8& t) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = 8 * (B0 + piece) + i;
+      if (r < HI) c[(r < N) ? r : 0] = t[i];
+    }
+  };
+  put(0, t0);
+  if constexpr (P > 1) put(1, t1);
+  if constexpr (P > 2) put(2, t2);
+  if constexpr (P > 3) put(3, t3);
+}
+
+// ---- prefix-blocked rows (SpaRyser / SkipPer kernels) --------------------
+// Rows are kept in 8-row blocks with suffix products U[b] = prod_{rows >= 8b}
+// (U[NB] = 1).  Mirrored by oracle/oracle.c e_sparse_step / e_suffix.
+template <int N>
+struct Blocks {
+  static constexpr int NB = (N + 7) / 8;
+};
+
+template <int N, int B>
+__device__ __forceinline__ void blk_add(double (&x)[N], const double (&c)[N]) {
+  constexpr int lo = 8 * B, hi = (8 * B + 8 < N) ? 8 * B + 8 : N;
+#pragma unroll
+  for (int j = lo; j < hi; ++j) x[j] += c[j];
+}
+template <int N, int B>
+__device__ __forceinline__ void blk_prod(const double (&x)[N], double (&U)[Blocks<N>::NB + 1]) {
+  U[B] = bprod8<N, B>(x) * U[B + 1];
+}
+
+template <int N>
+__device__ __forceinline__ void suffix_all(const double (&x)[N], double (&U)[Blocks<N>::NB + 1]) {
+  U[Blocks<N>::NB] = 1.0;
+#pragma unroll
+  for (int b = Blocks<N>::NB - 1; b >= 0; --b) {
+    double v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (8 * b + i < N) ? x[(8 * b + i < N) ? 8 * b + i : 0] : 1.0;
+    U[b] = (((v[0] * v[1]) * (v[2] * v[3])) * ((v[4] * v[5]) * (v[6] * v[7]))) * U[b + 1];
+  }
+}
+
+// One walk step: add column `col` to the leading nb row blocks and refresh
+// their suffix products, top block first (U[b+1] is current when U[b] is
+// formed).  A fall-through switch = one uniform jump per half, and the column
+// rows are fetched up front (fetch_rows) so each half waits once.
+template <int B, int LO, class F>
+__device__ __forceinline__ void for_down(F&& f) {
+  if constexpr (B >= LO) {
+    f(std::integral_constant<int, B>{});
+    for_down<B - 1, LO>(f);
+  }
+}
+
+// Blocks are visited top-down in plain if-chains (structured control flow:
+// the x/U updates stay in place, no phi copies).  The column rows of each
+// half are fetched before the half's first branch.
+template <int N>
+__device__ __forceinline__ void sparse_step(double (&x)[N], double (&U)[Blocks<N>::NB + 1], cdbl* col, int nb) {
+  constexpr int NB = Blocks<N>::NB;
+  double c[N];
+  auto blk = [&](auto Bc) {
+    constexpr int b = decltype(Bc)::value;
+    if (nb > b) {
+      blk_add<N, b>(x, c);
+      blk_prod<N, b>(x, U);
+    }
+  };
+  if constexpr (NB > 4) {
+    if (nb > 4) {
+      fetch_rows<N, 32, N>(col, c);
+      for_down<NB - 1, 4>(blk);
+    }
+  }
+  constexpr int LOW = N < 32 ? N : 32;
+  fetch_rows<N, 0, LOW>(col, c);
+  for_down<(NB < 4 ? NB : 4) - 1, 0>(blk);
+}
+
 // Dynamic wave-chunk queue: lane 0 takes the next chunk, the wave shares it.
 // Which wave computes a chunk does not affect the result: every chunk writes
 // its own slot of chunk_out, reduced afterwards in a fixed pairwise order.

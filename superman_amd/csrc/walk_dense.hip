@@ -23,7 +23,11 @@ __global__ __launch_bounds__(kBlock) void walk_dense(WalkParams p) {
   const uint32_t T = 1u << p.m;
   const uint32_t offL = 2u * (uint32_t)p.L * NP * 8u;  // engine bit L = walk bit 0
 
-  for (uint32_t a = next_chunk(p.counter); a < p.chunk_count; a = next_chunk(p.counter)) {
+  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * kGroup < p.chunk_count; g = next_chunk(p.counter)) {
+   double keep = 0.0;  // lane j keeps the partial of chunk g*kGroup + j
+   for (uint32_t j = 0; j < (uint32_t)kGroup; ++j) {
+    const uint64_t a = (uint64_t)g * kGroup + j;
+    if (a >= p.chunk_count) break;
     const uint64_t ga = p.chunk_begin + a;
     double x[N];
     chunk_start<N>(x, p, ga, lane);
@@ -49,7 +53,11 @@ __global__ __launch_bounds__(kBlock) void walk_dense(WalkParams p) {
     // g(t) part is folded into the alternating signs above.
     if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;
     const double part = wave_sum(lane_valid ? acc : 0.0);
-    if (lane == 0) p.chunk_out[a] = part;
+    keep = (lane == j) ? part : keep;
+   }
+   // one 64-byte store per group (8 lanes x 8 B)
+   const uint64_t a = (uint64_t)g * kGroup + lane;
+   if (lane < (uint32_t)kGroup && a < p.chunk_count) p.chunk_out[a] = keep;
   }
 }
 

@@ -26,6 +26,13 @@ struct WalkParams {
   double* chunk_out;               // [chunk_count] per-wave-chunk partial sums
   unsigned int* counter;           // dynamic wave-chunk queue head (zeroed before launch)
   unsigned int* visited;           // optional [chunk_count]: product evaluations per chunk (skipper)
+  // sparse kernels: nblk of walk bit k packed as 4-bit fields, k < 16 in nb_lo,
+  // k >= 16 in nb_hi (kept in SGPRs: no memory round trip per step)
+  unsigned long long nb_lo, nb_hi;
 };
+
+// Wave-chunks are dequeued in groups of kGroup consecutive chunks so the
+// group's partials leave the wave as one 64-byte store.
+constexpr int kGroup = 8;
 
 }  // namespace sup

@@ -22,127 +22,99 @@
 
 namespace sup {
 
-template <int B, int NB, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < NB) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, NB>(f);
-  }
-}
-template <int B, class F>
-__device__ __forceinline__ void static_for_down(F&& f) {
-  if constexpr (B >= 0) {
-    f(std::integral_constant<int, B>{});
-    static_for_down<B - 1>(f);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void skip_step(double (&x)[N], double (&U)[(N + 7) / 8 + 1], cdbl* col, int nb) {
-  constexpr int NB = (N + 7) / 8;
-  static_for<0, NB>([&](auto Bc) {
-    constexpr int b = decltype(Bc)::value;
-    constexpr int lo = 8 * b;
-    constexpr int hi = (8 * b + 8 < N) ? 8 * b + 8 : N;
-    if (b < nb) add_rows<N, lo, hi>(x, col);
-  });
-  static_for_down<NB - 1>([&](auto Bc) {
-    constexpr int b = decltype(Bc)::value;
-    if (b < nb) U[b] = bprod8<N, b>(x) * U[b + 1];
-  });
-}
-
 // Next walk index t' > t at which walk bit k toggles (ctz(t') == k).
 __device__ __forceinline__ uint32_t next_toggle(uint32_t t, uint32_t k) {
-  const uint32_t period = 2u << k;
   uint32_t c = ((t >> (k + 1)) << (k + 1)) + (1u << k);
-  if (c <= t) c += period;
+  if (c <= t) c += 2u << k;
   return c;
 }
 
 template <int N>
 __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
   constexpr int NP = pad8(N);
-  constexpr int NB = (N + 7) / 8;
+  constexpr int NB = Blocks<N>::NB;
   const uint32_t lane = threadIdx.x & 63u;
   const bool lane_valid = lane < (1u << p.L);
   const uint32_t lane_par = __builtin_popcount(lane) & 1u;
   const uint32_t T = 1u << p.m;
   const uint32_t offL = 2u * (uint32_t)p.L * NP * 8u;
-  const uint32_t Lb = (uint32_t)p.L;
   const uint64_t umask = p.umask;  // lane-uniform rows
 
-  for (uint32_t a = next_chunk(p.counter); a < p.chunk_count; a = next_chunk(p.counter)) {
-    const uint64_t ga = p.chunk_begin + a;
-    double x[N];
-    chunk_start<N>(x, p, ga, lane);
-    double U[NB + 1];
-    U[NB] = 1.0;
-    static_for_down<NB - 1>([&](auto Bc) {
-      constexpr int b = decltype(Bc)::value;
-      U[b] = bprod8<N, b>(x) * U[b + 1];
-    });
-    double acc = 0.0;
-    uint32_t visited = 0;
-    uint32_t t = 0;
-    while (true) {
-      // state t: X is valid for walk index t
-      ++visited;
-      const double term = U[0];
-      acc = (t & 1u) ? acc - term : acc + term;
-      uint32_t next = t + 1;
-      if (__builtin_amdgcn_ballot_w64(term != 0.0) == 0) {
-        // every lane is zero: look for exact zeros on lane-uniform rows.  Those
-        // rows hold the same value on every lane, so lane 0's view decides.
-        uint32_t zlo = 0, zhi = 0;
+  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * kGroup < p.chunk_count; g = next_chunk(p.counter)) {
+    double keep = 0.0;
+    uint32_t vkeep = 0;
+    for (uint32_t j = 0; j < (uint32_t)kGroup; ++j) {
+      const uint64_t a = (uint64_t)g * kGroup + j;
+      if (a >= p.chunk_count) break;
+      const uint64_t ga = p.chunk_begin + a;
+      double x[N];
+      chunk_start<N>(x, p, ga, lane);
+      double U[NB + 1];
+      suffix_all<N>(x, U);
+      double acc = 0.0;
+      uint32_t visited = 0;
+      uint32_t t = 0;
+      while (true) {
+        // state t: X is valid for walk index t
+        ++visited;
+        const double term = U[0];
+        acc = (t & 1u) ? acc - term : acc + term;
+        uint32_t next = t + 1;
+        if (__builtin_amdgcn_ballot_w64(term != 0.0) == 0) {
+          // every lane is zero: look for exact zeros on lane-uniform rows.  Those
+          // rows hold the same value on every lane, so lane 0's view decides.
+          uint32_t zlo = 0, zhi = 0;
 #pragma unroll
-        for (int r = 0; r < N; ++r) {
-          if (r < 32) zlo |= (x[r] == 0.0) ? (1u << (r & 31)) : 0u;
-          else zhi |= (x[r] == 0.0) ? (1u << (r & 31)) : 0u;
-        }
-        uint64_t zm = ((uint64_t)__builtin_amdgcn_readfirstlane(zhi) << 32) |
-                      (uint64_t)__builtin_amdgcn_readfirstlane(zlo);
-        zm &= umask;
-        if (zm) {
-          // each zero row r stays zero until one of its walk columns toggles
-          // (or for the rest of the chunk if it has none); the product is zero
-          // until the last of those toggles.
-          uint32_t target = t + 1;
-          while (zm) {
-            const uint32_t r = (uint32_t)__builtin_ctzll(zm);
-            zm &= zm - 1;
-            uint64_t mm = ((const __attribute__((address_space(4))) uint64_t*)p.rowmask)[r];
-            uint32_t tr = T;
-            while (mm) {
-              const uint32_t k = (uint32_t)__builtin_ctzll(mm);
-              mm &= mm - 1;
-              const uint32_t c = next_toggle(t, k);
-              tr = c < tr ? c : tr;
-            }
-            target = tr > target ? tr : target;
+          for (int r = 0; r < N; ++r) {
+            if (r < 32) zlo |= (x[r] == 0.0) ? (1u << (r & 31)) : 0u;
+            else zhi |= (x[r] == 0.0) ? (1u << (r & 31)) : 0u;
           }
-          next = target;
+          uint64_t zm = ((uint64_t)__builtin_amdgcn_readfirstlane(zhi) << 32) |
+                        (uint64_t)__builtin_amdgcn_readfirstlane(zlo);
+          zm &= umask;
+          if (zm) {
+            // each zero row r stays zero until one of its walk columns toggles
+            // (or for the rest of the chunk if it has none); the product is
+            // zero until the last of those toggles.
+            uint32_t target = t + 1;
+            while (zm) {
+              const uint32_t r = (uint32_t)__builtin_ctzll(zm);
+              zm &= zm - 1;
+              uint64_t mm = ((const __attribute__((address_space(4))) uint64_t*)p.rowmask)[r];
+              uint32_t tr = T;
+              while (mm) {
+                const uint32_t k = (uint32_t)__builtin_ctzll(mm);
+                mm &= mm - 1;
+                const uint32_t c = next_toggle(t, k);
+                tr = c < tr ? c : tr;
+              }
+              target = tr > target ? tr : target;
+            }
+            next = target;
+          }
         }
+        if (next >= T) break;
+        // Gray move t -> next: flip the differing walk bits in ascending order
+        // (exactly one bit for an ordinary step; several after a jump).
+        const uint32_t gn = next ^ (next >> 1);
+        uint32_t diff = (t ^ (t >> 1)) ^ gn;
+        do {
+          const uint32_t k = (uint32_t)__builtin_ctz(diff);
+          diff &= diff - 1;
+          const uint32_t neg = ((gn >> k) & 1u) ^ 1u;
+          sparse_step<N>(x, U, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nb_of(p, k));
+        } while (diff);
+        t = next;
       }
-      if (next >= T) break;
-      // Gray move t -> next: flip the differing walk bits in ascending order
-      // (exactly one bit for an ordinary step; several after a jump).
-      const uint32_t gn = next ^ (next >> 1);
-      uint32_t diff = (t ^ (t >> 1)) ^ gn;
-      do {
-        const uint32_t k = (uint32_t)__builtin_ctz(diff);
-        diff &= diff - 1;
-        const uint32_t neg = ((gn >> k) & 1u) ^ 1u;
-        const int nbk = opaque_i(p.nblk, (Lb + k) * 4u)[0];
-        skip_step<N>(x, U, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nbk);
-      } while (diff);
-      t = next;
+      if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;
+      const double part = wave_sum(lane_valid ? acc : 0.0);
+      keep = (lane == j) ? part : keep;
+      vkeep = (lane == j) ? visited : vkeep;
     }
-    if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;
-    const double part = wave_sum(lane_valid ? acc : 0.0);
-    if (lane == 0) {
-      p.chunk_out[a] = part;
-      if (p.visited) p.visited[a] = visited;
+    const uint64_t a = (uint64_t)g * kGroup + lane;
+    if (lane < (uint32_t)kGroup && a < p.chunk_count) {
+      p.chunk_out[a] = keep;
+      if (p.visited) p.visited[a] = vkeep;
     }
   }
 }

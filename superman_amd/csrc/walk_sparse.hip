@@ -7,7 +7,7 @@
 // zero counter).  On gfx950 an fp64 divide is a ~10-instruction sequence, so
 // this kernel exploits sparsity structurally instead:
 //   * rows are ordered by the first walk column that touches them
-//     (host, engine.cpp plan_rows), so the rows touched by walk columns
+//     (host, engine.cpp make_plan), so the rows touched by walk columns
 //     0..k are the prefix [0, R_k);
 //   * X is kept in 8-row blocks with suffix products U[b] = prod_{rows >= 8b};
 //   * a step flipping walk column k updates and re-multiplies only the
@@ -21,87 +21,48 @@
 
 namespace sup {
 
-template <int B, int NB, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < NB) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, NB>(f);
-  }
-}
-template <int B, class F>
-__device__ __forceinline__ void static_for_down(F&& f) {
-  if constexpr (B >= 0) {
-    f(std::integral_constant<int, B>{});
-    static_for_down<B - 1>(f);
-  }
-}
-
-// Update the leading nb row blocks with column `col`, then refresh their
-// suffix products (descending b, so U[b+1] is current).
-template <int N>
-__device__ __forceinline__ void sparse_step(double (&x)[N], double (&U)[(N + 7) / 8 + 1], cdbl* col,
-                                            int nb) {
-  constexpr int NB = (N + 7) / 8;
-  static_for<0, NB>([&](auto Bc) {
-    constexpr int b = decltype(Bc)::value;
-    constexpr int lo = 8 * b;
-    constexpr int hi = (8 * b + 8 < N) ? 8 * b + 8 : N;
-    if (b < nb) {
-      add_rows<N, lo, hi>(x, col);
-    }
-  });
-  static_for_down<NB - 1>([&](auto Bc) {
-    constexpr int b = decltype(Bc)::value;
-    if (b < nb) U[b] = bprod8<N, b>(x) * U[b + 1];
-  });
-}
-
-template <int N>
-__device__ __forceinline__ void suffix_all(const double (&x)[N], double (&U)[(N + 7) / 8 + 1]) {
-  constexpr int NB = (N + 7) / 8;
-  U[NB] = 1.0;
-  static_for_down<NB - 1>([&](auto Bc) {
-    constexpr int b = decltype(Bc)::value;
-    U[b] = bprod8<N, b>(x) * U[b + 1];
-  });
-}
-
 template <int N>
 __global__ __launch_bounds__(kBlock) void walk_sparse(WalkParams p) {
   constexpr int NP = pad8(N);
-  constexpr int NB = (N + 7) / 8;
+  constexpr int NB = Blocks<N>::NB;
   const uint32_t lane = threadIdx.x & 63u;
   const bool lane_valid = lane < (1u << p.L);
   const uint32_t lane_par = __builtin_popcount(lane) & 1u;
   const uint32_t T = 1u << p.m;
   const uint32_t offL = 2u * (uint32_t)p.L * NP * 8u;
+  const int nb0 = nb_of(p, 0);
 
-  for (uint32_t a = next_chunk(p.counter); a < p.chunk_count; a = next_chunk(p.counter)) {
-    const uint64_t ga = p.chunk_begin + a;
-    double x[N];
-    chunk_start<N>(x, p, ga, lane);
-    double U[NB + 1];
-    suffix_all<N>(x, U);
-    double acc = U[0];
-    const int nb0 = opaque_i(p.nblk, (uint32_t)p.L * 4u)[0];  // walk bit 0
-    uint32_t t = 1;
-    for (; t + 1 < T; t += 2) {
-      sparse_step<N>(x, U, opaque_c(p.cols, offL + ((t >> 1) & 1u) * NP * 8u), nb0);
-      acc -= U[0];
-      const uint32_t u = t + 1;
-      const uint32_t k = (uint32_t)__builtin_ctz(u);
-      const uint32_t neg = (u >> (k + 1)) & 1u;
-      const int nbk = opaque_i(p.nblk, ((uint32_t)p.L + k) * 4u)[0];
-      sparse_step<N>(x, U, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nbk);
-      acc += U[0];
+  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * kGroup < p.chunk_count; g = next_chunk(p.counter)) {
+    double keep = 0.0;
+    for (uint32_t j = 0; j < (uint32_t)kGroup; ++j) {
+      const uint64_t a = (uint64_t)g * kGroup + j;
+      if (a >= p.chunk_count) break;
+      const uint64_t ga = p.chunk_begin + a;
+      double x[N];
+      chunk_start<N>(x, p, ga, lane);
+      double U[NB + 1];
+      suffix_all<N>(x, U);
+      double acc = U[0];
+      uint32_t t = 1;
+      for (; t + 1 < T; t += 2) {
+        sparse_step<N>(x, U, opaque_c(p.cols, offL + ((t >> 1) & 1u) * NP * 8u), nb0);
+        acc -= U[0];
+        const uint32_t u = t + 1;
+        const uint32_t k = (uint32_t)__builtin_ctz(u);
+        const uint32_t neg = (u >> (k + 1)) & 1u;
+        sparse_step<N>(x, U, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nb_of(p, k));
+        acc += U[0];
+      }
+      if (t < T) {
+        sparse_step<N>(x, U, opaque_c(p.cols, offL + ((t >> 1) & 1u) * NP * 8u), nb0);
+        acc -= U[0];
+      }
+      if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;
+      const double part = wave_sum(lane_valid ? acc : 0.0);
+      keep = (lane == j) ? part : keep;
     }
-    if (t < T) {
-      sparse_step<N>(x, U, opaque_c(p.cols, offL + ((t >> 1) & 1u) * NP * 8u), nb0);
-      acc -= U[0];
-    }
-    if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;
-    const double part = wave_sum(lane_valid ? acc : 0.0);
-    if (lane == 0) p.chunk_out[a] = part;
+    const uint64_t a = (uint64_t)g * kGroup + lane;
+    if (lane < (uint32_t)kGroup && a < p.chunk_count) p.chunk_out[a] = keep;
   }
 }
 

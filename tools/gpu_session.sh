@@ -1,8 +1,8 @@
 #!/bin/bash
 # One GPU session on the MI355X box: each step under its own time limit; stop
-# at the first crash/timeout (exit codes 124/134/137/139 or signals), keep
-# going after plain test failures (exit 1) so the bench still runs.
-# usage: tools/gpu_session.sh <tag> [steps...]   steps: test bench prof pmc
+# at the first crash/timeout (exit codes 124/134/137/139 or >128), keep going
+# after ordinary failures (test failures, a rejected counter name).
+# usage: tools/gpu_session.sh <tag> [steps...]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-run}; shift
@@ -14,8 +14,14 @@ run() {  # name seconds cmd...
   echo "== $name ($(date +%T))"
   timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
-  echo "   rc=$rc"; tail -5 "$OUT/$name.log"
-  case $rc in 0|1|5) return 0;; *) echo "STOP: $name exit $rc"; exit $rc;; esac
+  echo "   rc=$rc"; tail -4 "$OUT/$name.log"
+  if [ $rc -eq 124 ] || [ $rc -ge 128 ]; then echo "STOP: $name exit $rc"; exit $rc; fi
+  return 0
+}
+BENCH1="python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0"
+prof_pmc() {  # name counters...
+  local name=$1; shift
+  run "$name" 600 rocprofv3 --pmc "$@" --kernel-trace -d "$OUT/$name" -o run --output-format csv -- $BENCH1
 }
 rocm-smi --showproductname --showclocks > "$OUT/rocm_smi.log" 2>&1 || true
 for step in "$@"; do
@@ -25,9 +31,13 @@ for step in "$@"; do
     testall) run pytest_gpu 1200 python3 -m pytest tests -m gpu -q -p no:cacheprovider;;
     bench) run bench 600 python3 bench.py --steps 3 --warmup 1;;
     prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0;;
-    pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0
-           run pmcw 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw" -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0;;
+    list)  run counters 120 rocprofv3 -L;;
+    pmc)   prof_pmc pmc_fetch FETCH_SIZE
+           prof_pmc pmc_write WRITE_SIZE
+           prof_pmc pmc_sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT
+           prof_pmc pmc_lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY;;
     probe) run probe 300 python3 tools/probe.py;;
+    *) run "$step" 900 bash -c "$step";;
   esac
 done
 echo "== done"
