@@ -42,6 +42,17 @@ def parse():
     return ap.parse_args()
 
 
+def shard_bounds(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Reference Gray-index range [start, end) of this rank's shard: a
+    contiguous run of the 2^h wave-chunks (power-of-two aligned when world is
+    a power of two, so the all-reduced partials reproduce the 1-GPU bits)."""
+    import superman_amd as S
+    L, m, h = S.layout(n)
+    C = 1 << h
+    c0, c1 = C * rank // world, C * (rank + 1) // world
+    return c0 << (L + m), c1 << (L + m)
+
+
 def pmc_traffic(n: int):
     """HBM bytes per walk launch from the committed rocprofv3 PMC summary, if any."""
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
@@ -93,11 +104,7 @@ def main():
 
     a, typ, _ = S.read_matrix(args.matrix)
     n = a.shape[0]
-    L, m, h = S.layout(n)
-    C = 1 << h
-    c0, c1 = C * rank // world, C * (rank + 1) // world
-    cb = L + m
-    start, end = c0 << cb, c1 << cb
+    start, end = shard_bounds(n, rank, world)
     my_steps = end - start
     dev = local
 

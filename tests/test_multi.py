@@ -1,0 +1,81 @@
+"""N > 1 path on CPU: gloo, world_size 2 (and 4) — the bench's shard
+arithmetic and its single all-reduce reproduce the 1-device sum bit for bit.
+Each rank's shard is walked by the oracle's mirror of the engine schedule (the
+CPU stand-in for the GPU kernel, which is bit-identical to it)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, mat, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+
+    import bench
+    import oracle
+    import superman_amd as S
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = mat.shape[0]
+    start, end = bench.shard_bounds(n, rank, world)
+    L, m, _ = S.layout(n)
+    part, _ = oracle.engine_range(mat, "dense", start >> (L + m), end >> (L + m), L, m, True, 1)
+    t = torch.tensor([part], dtype=torch.float64)
+    dist.all_reduce(t)
+    el = torch.tensor([float(rank)], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        q.put(((4 * (n & 1) - 2) * float(t.item()), float(el.item()), (start, end)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_allreduce_matches_single(world, orc):
+    n = 22
+    mat = np.random.default_rng(5).random((n, n))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mat, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    got, max_rank, _ = res
+    assert max_rank == world - 1
+    want = orc.engine_perman(mat, "dense", 2)
+    if world == 2:
+        assert got == want  # bitwise: the two shards are the two top subtrees
+    else:
+        # the all-reduce's own summation order (ring / halving-doubling) differs
+        # from the pairwise tree only in the last combine steps: ulp level
+        assert abs(got - want) <= 4e-16 * world * abs(want)
+
+
+def test_shard_bounds_cover_space():
+    import bench
+    import superman_amd as S
+    for n in (8, 20, 33, 40):
+        for world in (1, 2, 3, 4, 8):
+            b = [bench.shard_bounds(n, r, world) for r in range(world)]
+            assert b[0][0] == 0 and b[-1][1] == 1 << (n - 1)
+            assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+            L, m, h = S.layout(n)
+            assert all(s % (1 << (L + m)) == 0 for s, _ in b)
