@@ -183,29 +183,57 @@ __device__ __forceinline__ void for_down(F&& f) {
   }
 }
 
-// Blocks are visited top-down in plain if-chains (structured control flow:
-// the x/U updates stay in place, no phi copies).  The column rows of each
-// half are fetched before the half's first branch.
-template <int N>
-__device__ __forceinline__ void sparse_step(double (&x)[N], double (&U)[Blocks<N>::NB + 1], cdbl* col, int nb) {
+// Nested form: `if (nb > B) { deeper blocks; block B }`, so a step touching
+// nb blocks pays ~nb uniform branches (not NB), blocks still run top-down,
+// and the control flow stays structured (x/U updated in place, no phi
+// copies).  Rows 0-15 are fetched before the first branch, rows 16-31 and
+// 32-63 inside the branch that first needs them.
+template <int N, int B>
+__device__ __forceinline__ void sparse_nest(double (&x)[N], double (&U)[Blocks<N>::NB + 1], cdbl* col, int nb,
+                                            double (&c)[N]) {
   constexpr int NB = Blocks<N>::NB;
-  double c[N];
-  auto blk = [&](auto Bc) {
-    constexpr int b = decltype(Bc)::value;
-    if (nb > b) {
-      blk_add<N, b>(x, c);
-      blk_prod<N, b>(x, U);
-    }
-  };
-  if constexpr (NB > 4) {
-    if (nb > 4) {
-      fetch_rows<N, 32, N>(col, c);
-      for_down<NB - 1, 4>(blk);
+  if constexpr (B < NB) {
+    if (nb > B) {
+      if constexpr (B == 2) fetch_rows<N, 16, (N < 32 ? N : 32)>(col, c);
+      if constexpr (B == 4) fetch_rows<N, 32, N>(col, c);
+      sparse_nest<N, B + 1>(x, U, col, nb, c);
+      blk_add<N, B>(x, c);
+      blk_prod<N, B>(x, U);
     }
   }
-  constexpr int LOW = N < 32 ? N : 32;
-  fetch_rows<N, 0, LOW>(col, c);
-  for_down<(NB < 4 ? NB : 4) - 1, 0>(blk);
+}
+
+template <int N>
+__device__ __forceinline__ void sparse_step(double (&x)[N], double (&U)[Blocks<N>::NB + 1], cdbl* col, int nb) {
+  double c[N];
+  fetch_rows<N, 0, (N < 16 ? N : 16)>(col, c);
+  sparse_nest<N, 1>(x, U, col, nb, c);
+  // block 0 always: nb == 0 only for an all-zero walk prefix, where adding the
+  // (zero) column leaves x and U unchanged
+  blk_add<N, 0>(x, c);
+  blk_prod<N, 0>(x, U);
+}
+
+// Same step with a compile-time block count (walk bit 0, the odd steps: half
+// of all steps) — straight-line code, only the rows it needs are fetched.
+template <int N, int NBS>
+__device__ __forceinline__ void sparse_step_static(double (&x)[N], double (&U)[Blocks<N>::NB + 1], cdbl* col) {
+  static_assert(NBS >= 0 && NBS <= Blocks<N>::NB, "block count out of range");
+  if constexpr (NBS > 0) {  // NBS == 0: all-zero walk column, x and U unchanged
+    double c[N];
+    constexpr int ROWS = (8 * NBS < N) ? 8 * NBS : N;
+    auto blk = [&](auto Bc) {
+      constexpr int b = decltype(Bc)::value;
+      blk_add<N, b>(x, c);
+      blk_prod<N, b>(x, U);
+    };
+    if constexpr (ROWS > 32) {
+      fetch_rows<N, 32, ROWS>(col, c);
+      for_down<NBS - 1, 4>(blk);
+    }
+    fetch_rows<N, 0, (ROWS < 32 ? ROWS : 32)>(col, c);
+    for_down<(NBS < 4 ? NBS : 4) - 1, 0>(blk);
+  }
 }
 
 // Dynamic wave-chunk queue: lane 0 takes the next chunk, the wave shares it.
