@@ -39,18 +39,20 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--matrix", default=os.path.join(ROOT, "tests", "fixtures", "double__40_0.50_0"))
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
+    ap.add_argument("--kernel", default="dense", choices=["dense", "dense_plain", "sparse", "skip"],
+                    help="dense = -p4/-p6 (engine picks plain or prefix-blocked walk); sparse/skip = -s paths")
+    ap.add_argument("--prep", type=int, default=0, choices=[0, 1, 2], help="-r: 1 SortOrder, 2 SkipOrder")
     return ap.parse_args()
 
 
-def shard_bounds(n: int, rank: int, world: int) -> tuple[int, int]:
-    """Reference Gray-index range [start, end) of this rank's shard: a
-    contiguous run of the 2^h wave-chunks (power-of-two aligned when world is
-    a power of two, so the all-reduced partials reproduce the 1-GPU bits)."""
+def shard_chunks(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Wave-chunk range [c0, c1) of this rank's shard (sup_perman_shard): a
+    contiguous run of the 2^h wave-chunks, power-of-two aligned when world is
+    a power of two (then the shards are subtrees of the fixed reduction)."""
     import superman_amd as S
     L, m, h = S.layout(n)
     C = 1 << h
-    c0, c1 = C * rank // world, C * (rank + 1) // world
-    return c0 << (L + m), c1 << (L + m)
+    return C * rank // world, C * (rank + 1) // world
 
 
 def pmc_traffic(n: int):
@@ -103,13 +105,18 @@ def main():
     import superman_amd as S
 
     a, typ, _ = S.read_matrix(args.matrix)
+    if args.prep == 1:
+        a = S.sort_order(a)[0]
+    elif args.prep == 2:
+        a = S.skip_order(a)[0]
     n = a.shape[0]
-    start, end = shard_bounds(n, rank, world)
-    my_steps = end - start
+    L, m, _ = S.layout(n)
+    c0, c1 = shard_chunks(n, rank, world)
+    my_steps = (c1 - c0) << (L + m)
     dev = local
 
     def step():
-        part, st = S.partial(a, start, end, device_id=dev, return_stats=True)
+        part, st = S.perman_shard(a, rank, world, kernel=args.kernel, device_id=dev, return_stats=True)
         if world > 1:
             t = torch.tensor([part], dtype=torch.float64, device=f"cuda:{local}")
             dist.all_reduce(t)  # RCCL over xGMI: the single data-path collective
@@ -142,6 +149,9 @@ def main():
     flops = 2.0 * n * my_steps  # n fp64 adds + n fp64 muls per Gray step
     achieved = flops / (k_ms * 1e-3) / 1e12
     traffic = pmc_traffic(n)
+    walk = {0: "walk_dense", 1: "walk_sparse", 2: "walk_skip"}[st["walk_kind"]]
+    fname = os.path.basename(args.matrix).replace("__", "/")
+    density = float((a != 0).sum()) / (n * n)
     rec = {
         "metric": METRIC,
         "value": value,
@@ -154,15 +164,20 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "reference corpus matrix double/40_0.50_0 (tests/fixtures/double__40_0.50_0)",
-        "config": {"workload": "dense Ryser/Gray-code exact permanent, n=40 d=0.50 (double/40_0.50_0), "
-                               "2^39 Gray steps per step",
-                   "n": n, "density": 0.5, "gray_steps_per_step": 1 << (n - 1),
+        "data": f"reference corpus matrix {fname} (tests/fixtures/{os.path.basename(args.matrix)})",
+        "config": {"workload": f"{args.kernel} Ryser/Gray-code exact permanent (-p4/-p6 path), n={n} "
+                               f"d={density:.2f} ({fname}), 2^{n - 1} Gray steps per step",
+                   "n": n, "density": round(density, 4), "gray_steps_per_step": 1 << (n - 1),
+                   "kernel_request": args.kernel, "preprocessing": args.prep,
                    "parallelism": f"dp{world}: contiguous wave-chunk shards + one RCCL all-reduce"},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": f"sup::walk_dense<{n}>", "kernel_ms_avg": k_ms,
-                     "algorithmic_flops_per_launch": flops},
+                     "kernel": f"sup::{walk}<{n}>", "kernel_ms_avg": k_ms,
+                     "algorithmic_flops_per_launch": flops,
+                     "flops_definition": "2n fp64 flops per Gray step (n adds + n muls, SURVEY 8(d)); the "
+                                         "prefix-blocked walk skips structural zeros, so it executes "
+                                         f"~{st['est_ops_per_step']:.1f} fp64 VALU ops per step instead of "
+                                         f"{2 * n + 1}; fp64 issue ceiling without FMA = 0.5 of peak"},
         "permanent": perm,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

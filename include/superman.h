@@ -58,9 +58,12 @@ typedef enum {
 
 /* ---- kernel family ------------------------------------------------------ */
 typedef enum {
-  SUP_KERNEL_DENSE = 0,     /* kernel_xshared_coalescing_mshared          gpu_exact_dense.cu:329-399  */
-  SUP_KERNEL_SPARYSER = 1,  /* kernel_xshared_coalescing_mshared_sparse   gpu_exact_sparse.cu:455-552 */
-  SUP_KERNEL_SKIPPER = 2    /* kernel_xshared_coalescing_mshared_skipper  gpu_exact_sparse.cu:555-670 */
+  SUP_KERNEL_DENSE = 0,       /* kernel_xshared_coalescing_mshared          gpu_exact_dense.cu:329-399.
+                                 The engine runs the plain dense walk, or the prefix-blocked walk when
+                                 its cost model says the matrix's zeros make that cheaper (same sum) */
+  SUP_KERNEL_SPARYSER = 1,    /* kernel_xshared_coalescing_mshared_sparse   gpu_exact_sparse.cu:455-552 */
+  SUP_KERNEL_SKIPPER = 2,     /* kernel_xshared_coalescing_mshared_skipper  gpu_exact_sparse.cu:555-670 */
+  SUP_KERNEL_DENSE_PLAIN = 3  /* always the plain dense walk (2n fp64 ops per Gray step)                */
 } sup_kernel;
 
 /* ---- multi-device scheduling policy -------------------------------------- */
@@ -95,6 +98,9 @@ typedef struct {
   int      grid;            /* blocks per launch (256 threads each) on each device             */
   int      chunks_done_cpu; /* queue items taken by the CPU worker                              */
   double   partials[16];    /* per-device partial sums (before the final combine)              */
+  int      walk_kind;       /* walk actually run: 0 dense, 1 prefix-blocked (SpaRyser), 2 SkipPer */
+  int      reserved_;
+  double   est_ops_per_step;/* cost model: fp64 VALU ops per Gray step and lane                 */
 } sup_stats;
 
 /* Fill `o` with defaults. */
@@ -126,6 +132,19 @@ int sup_perman(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched
  * (any power-of-two aligned chunk boundary >= 64 works), or end == 2^(n-1). */
 int sup_partial(const void* mat, sup_dtype t, int n, sup_kernel kernel,
                 uint64_t start, uint64_t end, const sup_opts* o, double* out, sup_stats* st);
+
+/* Shard `shard` of `nshards` of the engine's own enumeration of the full sum
+ * (same plan as sup_perman): the shards' partials add up to
+ * perm / (4(n&1)-2).  For one process per GPU (torch.distributed / MPI):
+ * each rank computes its shard on `o->device_id`, then one all-reduce. */
+int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int shard, int nshards,
+                     const sup_opts* o, double* out_partial, sup_stats* st);
+
+/* The plan sup_perman would run: walk kind (0 dense, 1 prefix/SpaRyser,
+ * 2 SkipPer), engine-bit -> column map (n-1 entries), lane and walk bits.
+ * For the test harness's bit-exact mirror of the enumeration. */
+int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, int* walk_kind, int* colmap,
+                  int* lane_bits, int* walk_bits);
 
 /* Explicit CPU algorithm for the CLI's `-c` mode (reference RunAlgo cpu
  * branch, main.cu:186-238): the same wave-chunk walk on `threads` host

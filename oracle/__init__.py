@@ -32,8 +32,8 @@ def load() -> C.CDLL:
         lib.orc_ref_sparse_partial.argtypes = [P, I, LL, LL, I]
         lib.orc_ref_skip.argtypes = [P, I, I, C.POINTER(U)]
         lib.orc_ref_skip_partial.argtypes = [P, I, LL, LL, I]
-        lib.orc_engine_range.argtypes = [P, I, I, I, I, I, U, U, I, C.POINTER(U)]
-        lib.orc_engine_perman.argtypes = [P, I, I, I]
+        lib.orc_engine_range.argtypes = [P, I, I, P, I, I, U, U, I, C.POINTER(U)]
+        lib.orc_engine_perman.argtypes = [P, I, I, P, I]
         lib.orc_nw_start.argtypes = [P, I, P, P]
         lib.orc_engine_layout.argtypes = [I, C.POINTER(I), C.POINTER(I), C.POINTER(I)]
         for f in ("orc_ref_dense", "orc_ref_dense_partial", "orc_ref_sparse", "orc_ref_sparse_partial",
@@ -100,23 +100,39 @@ def engine_layout(n: int) -> tuple[int, int, int]:
     return L.value, m.value, h.value
 
 
-KINDS = {"dense": 0, "sparse": 1, "skip": 2}
+KINDS = {"dense": 0, "sparse": 1, "skip": 2, 0: 0, 1: 1, 2: 2}
 
 
-def engine_range(a, kind: str, c0: int, c1: int, L: int, m: int, identity: bool = True,
-                 threads: int = 8) -> tuple[float, int]:
-    """Engine-schedule mirror over wave-chunks [c0, c1): (partial, visited)."""
+def _colmap(colmap):
+    if colmap is None:
+        return None, None
+    cm = np.ascontiguousarray(np.asarray(colmap, dtype=np.int32))
+    return cm, cm.ctypes.data
+
+
+def engine_range(a, kind, c0: int, c1: int, L: int, m: int, colmap=None, threads: int = 8) -> tuple[float, int]:
+    """Engine-schedule mirror over wave-chunks [c0, c1): (partial, visited).
+    colmap: engine bit -> matrix column (None = identity)."""
     a = _d(a)
     v = C.c_ulonglong(0)
-    r = load().orc_engine_range(a.ctypes.data, a.shape[0], KINDS[kind], int(identity), L, m, c0, c1, threads,
-                                C.byref(v))
+    keep, ptr = _colmap(colmap)
+    r = load().orc_engine_range(a.ctypes.data, a.shape[0], KINDS[kind], ptr, L, m, c0, c1, threads, C.byref(v))
     return r, v.value
 
 
-def engine_perman(a, kind: str = "dense", threads: int = 8) -> float:
-    """Full permanent enumerated exactly as the gfx950 kernels do (bit-exact mirror)."""
+def engine_perman(a, kind="dense", colmap=None, threads: int = 8) -> float:
+    """Full permanent enumerated exactly as the gfx950 kernels do (bit-exact
+    mirror), for walk `kind` and engine column map `colmap`."""
     a = _d(a)
-    return load().orc_engine_perman(a.ctypes.data, a.shape[0], KINDS[kind], threads)
+    keep, ptr = _colmap(colmap)
+    return load().orc_engine_perman(a.ctypes.data, a.shape[0], KINDS[kind], ptr, threads)
+
+
+def engine_perman_as(sup_module, a, kernel="dense", threads: int = 8) -> float:
+    """Mirror of exactly the plan the product runs for `kernel` (walk kind and
+    column map queried through the C ABI's sup_plan_info)."""
+    info = sup_module.plan_info(a, kernel)
+    return engine_perman(a, info["kind"], info["colmap"], threads)
 
 
 def exact_perman(a) -> Fraction:

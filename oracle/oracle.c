@@ -401,7 +401,7 @@ void orc_engine_layout(int n, int* L, int* m, int* h) {
   *h = rest - mm;
 }
 
-static void engine_plan(const double* a, int n, int kind, int identity, int L, int m, eplan* P) {
+static void engine_plan(const double* a, int n, int kind, const int* colmap, int L, int m, eplan* P) {
   memset(P, 0, sizeof(*P));
   P->n = n;
   P->NP = (n + 7) & ~7;
@@ -410,11 +410,7 @@ static void engine_plan(const double* a, int n, int kind, int identity, int L, i
   P->m = m;
   P->h = n - 1 - L - m;
   int nb = n - 1;
-  for (int e = 0; e < nb; ++e) P->colmap[e] = e;
-  if (!identity && kind == 1 && m > 0) {
-    for (int k = 0; k < m; ++k) P->colmap[L + k] = k;
-    for (int e = 0; e < L; ++e) P->colmap[e] = m + e;
-  }
+  for (int e = 0; e < nb; ++e) P->colmap[e] = colmap ? colmap[e] : e;
   for (int j = 0; j < n; ++j) P->rowperm[j] = j;
   if (kind != 0) {
     char placed[ORC_MAXN] = {0};
@@ -609,11 +605,12 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
 }
 
 /* Engine-mirror partial over wave-chunks [c0, c1) with layout (L, m).
- * kind: 0 dense, 1 SpaRyser, 2 SkipPer.  identity: engine bit e = column e. */
-double orc_engine_range(const double* a, int n, int kind, int identity, int L, int m, unsigned long long c0,
+ * kind: 0 dense, 1 SpaRyser (prefix blocks), 2 SkipPer.  colmap: engine bit e
+ * -> matrix column (n-1 entries; NULL = identity). */
+double orc_engine_range(const double* a, int n, int kind, const int* colmap, int L, int m, unsigned long long c0,
                         unsigned long long c1, int threads, unsigned long long* visited) {
   eplan* P = (eplan*)malloc(sizeof(eplan));
-  engine_plan(a, n, kind, identity, L, m, P);
+  engine_plan(a, n, kind, colmap, L, m, P);
   unsigned long long count = c1 > c0 ? c1 - c0 : 0;
   if (count == 0) {
     free(P);
@@ -646,10 +643,10 @@ double orc_engine_range(const double* a, int n, int kind, int identity, int L, i
   return r;
 }
 
-/* Full permanent with the engine's default layout and column map. */
-double orc_engine_perman(const double* a, int n, int kind, int threads) {
+/* Full permanent with the engine's default layout and the given column map. */
+double orc_engine_perman(const double* a, int n, int kind, const int* colmap, int threads) {
   int L, m, h;
   orc_engine_layout(n, &L, &m, &h);
-  double s = orc_engine_range(a, n, kind, 0, L, m, 0, 1ULL << h, threads, 0);
+  double s = orc_engine_range(a, n, kind, colmap, L, m, 0, 1ULL << h, threads, 0);
   return (4 * (n & 1) - 2) * s;
 }

@@ -19,7 +19,7 @@ from ._lib import (KERNEL_DENSE, KERNEL_SKIPPER, KERNEL_SPARYSER, SCHED_CHUNKS, 
                    SCHED_STATIC, SupError, SupOpts, SupStats)
 
 __all__ = [
-    "perman", "perman_cpu", "partial", "read_matrix", "sort_order", "skip_order", "compress",
+    "perman", "perman_cpu", "partial", "perman_shard", "plan_info", "read_matrix", "sort_order", "skip_order", "compress",
     "nw_start", "device_count", "layout", "SupError", "ALGOS_DENSE", "ALGOS_SPARSE",
     "gpu_perman64_xshared_coalescing_mshared",
     "gpu_perman64_xshared_coalescing_mshared_multigpu",
@@ -60,7 +60,8 @@ ALGOS_SPARSE = {
          SCHED_STATIC),
 }
 _KERNELS = {"dense": KERNEL_DENSE, "sparse": KERNEL_SPARYSER, "spa": KERNEL_SPARYSER,
-            "skipper": KERNEL_SKIPPER, "skip": KERNEL_SKIPPER}
+            "skipper": KERNEL_SKIPPER, "skip": KERNEL_SKIPPER, "dense_plain": _lib.KERNEL_DENSE_PLAIN}
+WALK_NAMES = {0: "dense", 1: "sparse", 2: "skip"}
 
 
 def _mat(a) -> tuple[np.ndarray, int, int]:
@@ -148,6 +149,30 @@ def partial(mat, start: int, end: int, kernel: str = "dense", gpu_num: int = 1, 
     _lib.check(lib.sup_partial(a.ctypes.data, dt, n, _KERNELS[kernel], int(start), int(end), C.byref(o),
                                C.byref(out), C.byref(st)), "partial")
     return (out.value, st.as_dict()) if return_stats else out.value
+
+
+def perman_shard(mat, shard: int, nshards: int, kernel: str = "dense", device_id: int = 0,
+                 return_stats: bool = False):
+    """Partial sum of shard `shard` of `nshards` of the engine's enumeration
+    (one process per GPU): the shards add up to perm / (4(n&1)-2)."""
+    a, dt, n = _mat(mat)
+    lib = _lib.load()
+    o = _opts(device_id=device_id)
+    out, st = C.c_double(0.0), SupStats()
+    _lib.check(lib.sup_perman_shard(a.ctypes.data, dt, n, _KERNELS[kernel], int(shard), int(nshards), C.byref(o),
+                                    C.byref(out), C.byref(st)), "perman_shard")
+    return (out.value, st.as_dict()) if return_stats else out.value
+
+
+def plan_info(mat, kernel: str = "dense") -> dict:
+    """The plan the engine runs for `kernel`: walk kind, column map, layout."""
+    a, dt, n = _mat(mat)
+    lib = _lib.load()
+    kind, L, m = C.c_int(), C.c_int(), C.c_int()
+    cm = np.zeros(max(n - 1, 1), np.int32)
+    _lib.check(lib.sup_plan_info(a.ctypes.data, dt, n, _KERNELS[kernel], C.byref(kind), cm.ctypes.data,
+                                 C.byref(L), C.byref(m)), "plan_info")
+    return {"kind": WALK_NAMES[kind.value], "colmap": cm[: n - 1].copy(), "L": L.value, "m": m.value}
 
 
 def nw_start(mat) -> tuple[np.ndarray, float]:

@@ -41,6 +41,8 @@ void fill_stats(sup_stats* st, const Plan& P, const SchedResult& r, double wall_
   st->grid = r.grid;
   st->chunks_done_cpu = r.cpu_items;
   for (size_t i = 0; i < r.dev_partials.size() && i < 16; ++i) st->partials[i] = r.dev_partials[i];
+  st->walk_kind = (int)P.kind;
+  st->est_ops_per_step = walk_cost(P);
 }
 
 }  // namespace
@@ -92,7 +94,7 @@ int sup_perman(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched
     lay.m = std::min(o.walk_log2, rest);
     lay.h = rest - lay.m;
   }
-  if ((rc = make_plan(A.data(), n, kind_of(kernel), false, lay, P))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, lay, P))) return rc;
   SchedResult r;
   if ((rc = schedule(P, sched, o, 0, P.lay.chunks(), r))) return rc;
   *out = (double)(4 * (n & 1) - 2) * r.total;  // gpu_exact_dense.cu:698
@@ -153,13 +155,54 @@ int sup_perman_cpu(const void* mat, sup_dtype t, int n, sup_kernel kernel, int t
   std::vector<double> A;
   if ((rc = to_double(mat, t, n, A))) return rc;
   Plan P;
-  if ((rc = make_plan(A.data(), n, kind_of(kernel), false, default_layout(n), P))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P))) return rc;
   SchedResult r;
   r.total = cpu_walk_range(P, 0, P.lay.chunks(), threads < 1 ? 1 : threads);
   r.visited = 1ull << (n - 1);
   *out = (double)(4 * (n & 1) - 2) * r.total;
   const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   fill_stats(st, P, r, wall, 1ull << (n - 1));
+  return SUP_OK;
+}
+
+int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int shard, int nshards,
+                     const sup_opts* o_in, double* out, sup_stats* st) {
+  auto t0 = std::chrono::steady_clock::now();
+  int rc = check_common(mat, n, out);
+  if (rc) return rc;
+  if (nshards < 1 || shard < 0 || shard >= nshards) {
+    set_error("shard index out of range");
+    return SUP_EINVAL;
+  }
+  sup_opts o;
+  if (o_in) o = *o_in;
+  else sup_opts_init(&o);
+  std::vector<double> A;
+  if ((rc = to_double(mat, t, n, A))) return rc;
+  Plan P;
+  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P))) return rc;
+  const uint64_t C = P.lay.chunks();
+  const uint64_t c0 = C * (uint64_t)shard / (uint64_t)nshards, c1 = C * (uint64_t)(shard + 1) / (uint64_t)nshards;
+  SchedResult r;
+  if ((rc = schedule(P, SUP_SCHED_SINGLE, o, c0, c1, r))) return rc;
+  *out = r.total;
+  const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  fill_stats(st, P, r, wall, (c1 - c0) << (P.lay.L + P.lay.m));
+  return SUP_OK;
+}
+
+int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, int* walk_kind, int* colmap, int* L,
+                  int* m) {
+  std::vector<double> A;
+  int rc = to_double(mat, t, n, A);
+  if (rc) return rc;
+  Plan P;
+  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P))) return rc;
+  if (walk_kind) *walk_kind = (int)P.kind;
+  if (colmap)
+    for (int e = 0; e < n - 1; ++e) colmap[e] = P.colmap[e];
+  if (L) *L = P.lay.L;
+  if (m) *m = P.lay.m;
   return SUP_OK;
 }
 

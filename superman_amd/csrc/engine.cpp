@@ -83,6 +83,69 @@ Layout default_layout(int n) {
   return l;
 }
 
+// Prefix cost of a walk order (VALU ops per Gray step):
+// walk bit k flips with frequency 2^-(k+1) and costs 8*nblk adds, 8*nblk muls
+// (7 in the block tree + 1 for the suffix chain) and one accumulate.
+static double prefix_cost(const double* A, int n, const std::vector<int>& walk) {
+  std::vector<char> placed(n, 0);
+  int R = 0;
+  double cost = 0.0, w = 0.5;
+  for (int c : walk) {
+    for (int i = 0; i < n; ++i)
+      if (!placed[i] && A[(size_t)i * n + c] != 0.0) placed[i] = 1, ++R;
+    const int nbk = (R + 7) / 8;
+    cost += w * (16.0 * nbk + 1.0);
+    w *= 0.5;
+  }
+  return cost;
+}
+
+// Walk-column order that keeps the row prefixes small: the first column is
+// tried exhaustively, the rest is greedy (fewest newly covered rows, then
+// fewest nonzeros, then lowest index); the order with the lowest prefix_cost
+// wins.  Column n-1 (Nijenhuis-Wilf) is never a walk column.
+std::vector<int> greedy_walk_order(const double* A, int n, int count) {
+  const int nb = n - 1;
+  count = std::min(count, nb);
+  std::vector<int> nnz(n, 0);
+  for (int c = 0; c < nb; ++c)
+    for (int i = 0; i < n; ++i) nnz[c] += A[(size_t)i * n + c] != 0.0;
+  auto greedy_from = [&](int first) {
+    std::vector<int> order{first};
+    std::vector<char> used(n, 0), placed(n, 0);
+    used[first] = 1;
+    for (int i = 0; i < n; ++i) placed[i] = A[(size_t)i * n + first] != 0.0;
+    while ((int)order.size() < count) {
+      int best = -1, bnew = 1 << 30;
+      for (int c = 0; c < nb; ++c) {
+        if (used[c]) continue;
+        int nw = 0;
+        for (int i = 0; i < n; ++i) nw += !placed[i] && A[(size_t)i * n + c] != 0.0;
+        if (nw < bnew || (nw == bnew && nnz[c] < nnz[best])) best = c, bnew = nw;
+      }
+      used[best] = 1;
+      order.push_back(best);
+      for (int i = 0; i < n; ++i) placed[i] |= A[(size_t)i * n + best] != 0.0;
+    }
+    return order;
+  };
+  std::vector<int> best;
+  double bcost = 1e300;
+  for (int f = 0; f < nb && count > 0; ++f) {
+    std::vector<int> o = greedy_from(f);
+    const double c = prefix_cost(A, n, o);
+    if (c < bcost) bcost = c, best = o;
+  }
+  return best;
+}
+
+double walk_cost(const Plan& P) {
+  if (P.kind == kWalkDense) return 2.0 * P.n + 1.0;
+  double cost = 0.0, w = 0.5;
+  for (int k = 0; k < P.lay.m; ++k, w *= 0.5) cost += w * (16.0 * P.nblk[P.lay.L + k] + 1.0);
+  return cost + w * 16.0 * ((P.n + 7) / 8);  // tail: the rest of the walk bits, bounded
+}
+
 int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const Layout& lay, Plan& P) {
   if (n < 1 || n > SUP_MAX_N) {
     set_error("n must be in [1, 64]");
@@ -100,10 +163,15 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
   P.colmap.resize(nb);
   for (int e = 0; e < nb; ++e) P.colmap[e] = e;
   if (!identity_map && kind == kWalkSparse && m > 0) {
-    // walk bits get the first (sparsest after SortOrder/SkipOrder) columns,
-    // lane bits the next L, the high bits keep their order.
-    for (int k = 0; k < m; ++k) P.colmap[L + k] = k;
-    for (int e = 0; e < L; ++e) P.colmap[e] = m + e;
+    // walk bits get the greedy prefix order (greedy_walk_order), lane bits
+    // the next L columns of that order, high bits the rest in matrix order.
+    std::vector<int> order = greedy_walk_order(A, n, m + L);
+    std::vector<char> used(n, 0);
+    for (int k = 0; k < m; ++k) P.colmap[L + k] = order[k], used[order[k]] = 1;
+    for (int e = 0; e < L; ++e) P.colmap[e] = order[m + e], used[order[m + e]] = 1;
+    int e = L + m;
+    for (int c = 0; c < nb; ++c)
+      if (!used[c]) P.colmap[e++] = c;
   }
 
   // ---- engine row order
@@ -164,6 +232,27 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
     P.rowmask[j] = rm;
   }
   return SUP_OK;
+}
+
+int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P) {
+  switch (kernel) {
+    case SUP_KERNEL_SKIPPER: return make_plan(A, n, kWalkSkip, false, lay, P);
+    case SUP_KERNEL_SPARYSER: return make_plan(A, n, kWalkSparse, false, lay, P);
+    case SUP_KERNEL_DENSE_PLAIN: return make_plan(A, n, kWalkDense, false, lay, P);
+    case SUP_KERNEL_DENSE: {
+      Plan d, s;
+      int rc = make_plan(A, n, kWalkDense, false, lay, d);
+      if (rc) return rc;
+      if (n >= 8 && (rc = make_plan(A, n, kWalkSparse, false, lay, s)) == SUP_OK && walk_cost(s) < walk_cost(d)) {
+        P = std::move(s);
+        return SUP_OK;
+      }
+      P = std::move(d);
+      return SUP_OK;
+    }
+  }
+  set_error("unknown sup_kernel");
+  return SUP_EINVAL;
 }
 
 double pairwise_host(const std::vector<double>& v) {

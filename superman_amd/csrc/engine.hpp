@@ -51,8 +51,21 @@ struct Plan {
 
 // Build a plan.  identity_map keeps engine bit e = column e (needed when a
 // chunk range must match reference Gray indices: sup_partial); otherwise the
-// sparse kernel puts its sparsest columns on the walk bits.
+// SpaRyser walk takes its walk columns in greedy_walk_order.
 int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const Layout& lay, Plan& P);
+
+// Walk-column order minimising the prefix-block cost (first `count` columns).
+std::vector<int> greedy_walk_order(const double* A, int n, int count);
+
+// Estimated fp64 VALU ops per Gray step of a plan (dense: 2n+1; prefix kernels:
+// sum_k 2^-(k+1) (16 nblk_k + 1)).
+double walk_cost(const Plan& P);
+
+// The plan sup_perman / sup_perman_shard run for this request: for
+// SUP_KERNEL_DENSE the engine takes the prefix-blocked walk whenever its cost
+// model is lower (same sum, structural zeros skipped); SUP_KERNEL_DENSE_PLAIN
+// forces the plain dense walk.
+int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P);
 
 struct RangeResult {
   double partial = 0.0;     // pairwise sum over the range's wave-chunks

@@ -50,7 +50,7 @@ def test_bitexact_vs_engine_mirror(sup, orc, golden, kind, algo, sparse):
         if kind == "skip":
             a = sup.skip_order(a)[0]
         got, st = sup.perman(a, algo=algo, sparse=sparse, return_stats=True)
-        want = orc.engine_perman(a, kind, 4)
+        want = orc.engine_perman_as(sup, a, kind, threads=4)
         assert got == want, (name, kind, got, want)
         assert st["devices_used"] == 1 and st["kernel_ms"] > 0.0
 
@@ -95,7 +95,7 @@ def test_known_answers(sup):
 def test_corpus_n30(sup, orc, golden, name):
     a, typ, _ = sup.read_matrix(fixture_path(name))
     got = sup.perman(a, algo=4)
-    assert got == orc.engine_perman(a, "dense", 16)
+    assert got == orc.engine_perman_as(sup, a, "dense", threads=16)
     q = golden.get(f"{name}|dense_q|r0|b0|t8")
     f = golden[f"{name}|dense|r0|b0|t8"]
     assert rel(got, q if q is not None else f) < 1e-8
@@ -110,8 +110,8 @@ def test_sparse_orders_corpus(sup, orc, golden):
         s2 = sup.skip_order(a)[0]
         g1 = sup.perman(s1, algo=4, sparse=True)
         g2 = sup.perman(s2, algo=7, sparse=True)
-        assert g1 == orc.engine_perman(s1, "sparse", 16)
-        assert g2 == orc.engine_perman(s2, "skip", 16)
+        assert g1 == orc.engine_perman_as(sup, s1, "sparse", threads=16)
+        assert g2 == orc.engine_perman_as(sup, s2, "skip", threads=16)
         ref = golden.get(f"{name}|dense_q|r0|b0|t8", golden[f"{name}|sparse|r1|b0|t8"])
         assert rel(g1, ref) < 1e-8 and rel(g2, ref) < 1e-8
 
@@ -126,7 +126,7 @@ def test_partials_match_reference_chunk_helper(sup, orc):
         want = orc.ref_dense_partial(a, s, e, 4)
         assert rel(got, want) < 1e-10, (s, e, got, want)
         L, ml = _partial_layout(sup, n, s, e)
-        mir, _ = orc.engine_range(a, "dense", s >> (L + ml), e >> (L + ml), L, ml, True, 4)
+        mir, _ = orc.engine_range(a, "dense", s >> (L + ml), e >> (L + ml), L, ml, None, 4)
         assert got == mir
     # index 0 carries the p0 term
     x0, p0 = orc.nw_start(a)

@@ -79,7 +79,7 @@ def test_cpu_walk_bitexact_vs_oracle_mirror(sup, orc, kind):
             if kind == "skip":
                 a, _, _ = sup.skip_order(a)
             got = sup.perman_cpu(a, kind, threads=3)
-            want = orc.engine_perman(a, kind, 2)
+            want = orc.engine_perman_as(sup, a, kind, threads=2)
             assert got == want or (np.isnan(got) and np.isnan(want)), (n, d, got, want)
 
 

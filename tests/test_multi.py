@@ -32,15 +32,15 @@ def _worker(rank, world, port, mat, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n = mat.shape[0]
-    start, end = bench.shard_bounds(n, rank, world)
-    L, m, _ = S.layout(n)
-    part, _ = oracle.engine_range(mat, "dense", start >> (L + m), end >> (L + m), L, m, True, 1)
+    c0, c1 = bench.shard_chunks(n, rank, world)
+    info = S.plan_info(mat, "dense")  # the plan sup_perman_shard runs
+    part, _ = oracle.engine_range(mat, info["kind"], c0, c1, info["L"], info["m"], info["colmap"], 1)
     t = torch.tensor([part], dtype=torch.float64)
     dist.all_reduce(t)
     el = torch.tensor([float(rank)], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     if rank == 0:
-        q.put(((4 * (n & 1) - 2) * float(t.item()), float(el.item()), (start, end)))
+        q.put(((4 * (n & 1) - 2) * float(t.item()), float(el.item()), (c0, c1)))
     dist.destroy_process_group()
 
 
@@ -60,7 +60,8 @@ def test_sharded_allreduce_matches_single(world, orc):
         assert p.exitcode == 0
     got, max_rank, _ = res
     assert max_rank == world - 1
-    want = orc.engine_perman(mat, "dense", 2)
+    import superman_amd as S
+    want = orc.engine_perman_as(S, mat, "dense", threads=2)
     if world == 2:
         assert got == want  # bitwise: the two shards are the two top subtrees
     else:
@@ -69,13 +70,14 @@ def test_sharded_allreduce_matches_single(world, orc):
         assert abs(got - want) <= 4e-16 * world * abs(want)
 
 
-def test_shard_bounds_cover_space():
+def test_shard_chunks_cover_space():
     import bench
     import superman_amd as S
     for n in (8, 20, 33, 40):
         for world in (1, 2, 3, 4, 8):
-            b = [bench.shard_bounds(n, r, world) for r in range(world)]
-            assert b[0][0] == 0 and b[-1][1] == 1 << (n - 1)
-            assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
             L, m, h = S.layout(n)
-            assert all(s % (1 << (L + m)) == 0 for s, _ in b)
+            b = [bench.shard_chunks(n, r, world) for r in range(world)]
+            assert b[0][0] == 0 and b[-1][1] == 1 << h
+            assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+            if world in (1, 2, 4, 8) and (1 << h) >= world:
+                assert all((c1 - c0) == (1 << h) // world for c0, c1 in b)
