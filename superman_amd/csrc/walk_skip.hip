@@ -63,14 +63,10 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
         if (__builtin_amdgcn_ballot_w64(term != 0.0) == 0) {
           // every lane is zero: look for exact zeros on lane-uniform rows.  Those
           // rows hold the same value on every lane, so lane 0's view decides.
-          uint32_t zlo = 0, zhi = 0;
+          // v_cmp straight into an SGPR mask per row (no VGPR temporaries)
+          uint64_t zm = 0;
 #pragma unroll
-          for (int r = 0; r < N; ++r) {
-            if (r < 32) zlo |= (x[r] == 0.0) ? (1u << (r & 31)) : 0u;
-            else zhi |= (x[r] == 0.0) ? (1u << (r & 31)) : 0u;
-          }
-          uint64_t zm = ((uint64_t)__builtin_amdgcn_readfirstlane(zhi) << 32) |
-                        (uint64_t)__builtin_amdgcn_readfirstlane(zlo);
+          for (int r = 0; r < N; ++r) zm |= (__builtin_amdgcn_ballot_w64(x[r] == 0.0) & 1ull) << r;
           zm &= umask;
           if (zm) {
             // each zero row r stays zero until one of its walk columns toggles
