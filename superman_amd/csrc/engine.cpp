@@ -387,9 +387,12 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     SUP_HIP(walk_occupancy(P.kind, P.n, &b));
     occ = b > 0 ? b : 1;
   }
-  const uint64_t waves_needed = (count + kGroup - 1) / kGroup;  // one chunk group per wave at a time
+  const uint64_t resident = (uint64_t)c->cus * (uint64_t)occ;  // resident blocks
+  const uint64_t res_waves = resident * kWavesPerBlock;
+  unsigned group = 8;
+  while (group > 1 && count / ((uint64_t)group * res_waves) < 32) group >>= 1;
+  const uint64_t waves_needed = (count + group - 1) / group;  // one chunk group per wave at a time
   uint64_t grid = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
-  const uint64_t resident = (uint64_t)c->cus * (uint64_t)occ;
   if (grid > resident) grid = resident;
   if (grid < 1) grid = 1;
 
@@ -407,6 +410,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   p.chunk_out = c->d_chunk;
   p.counter = c->d_counter;
   p.visited = visited ? c->d_visited : nullptr;
+  p.group = group;
   p.nb_lo = p.nb_hi = 0;
   for (int k = 0; k < P.lay.m && k < 32; ++k) {
     const uint64_t v = (uint64_t)(P.nblk[P.lay.L + k] & 15);

@@ -32,10 +32,10 @@ __global__ __launch_bounds__(kBlock) void walk_sparse(WalkParams p) {
   const uint32_t offL = 2u * (uint32_t)p.L * NP * 8u;
   const int nb0 = nb_of(p, 0);
 
-  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * kGroup < p.chunk_count; g = next_chunk(p.counter)) {
+  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {
     double keep = 0.0;
-    for (uint32_t j = 0; j < (uint32_t)kGroup; ++j) {
-      const uint64_t a = (uint64_t)g * kGroup + j;
+    for (uint32_t j = 0; j < (uint32_t)p.group; ++j) {
+      const uint64_t a = (uint64_t)g * p.group + j;
       if (a >= p.chunk_count) break;
       const uint64_t ga = p.chunk_begin + a;
       double x[N];
@@ -61,8 +61,8 @@ __global__ __launch_bounds__(kBlock) void walk_sparse(WalkParams p) {
       const double part = wave_sum(lane_valid ? acc : 0.0);
       keep = (lane == j) ? part : keep;
     }
-    const uint64_t a = (uint64_t)g * kGroup + lane;
-    if (lane < (uint32_t)kGroup && a < p.chunk_count) p.chunk_out[a] = keep;
+    const uint64_t a = (uint64_t)g * p.group + lane;
+    if (lane < (uint32_t)p.group && a < p.chunk_count) p.chunk_out[a] = keep;
   }
 }
 

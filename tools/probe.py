@@ -43,3 +43,18 @@ for path, prep in (("double__32_0.50_0", 0), ("double__36_0.20_0", 1), ("double_
         m = S.skip_order(m)[0]
     for kernel in ("dense_plain", "dense", "sparse") + (("skip",) if prep == 2 else ()):
         run(f"{path} r{prep}", m, kernel)
+
+# strong-scaling rehearsal on one GPU: the 8 shards of the n=40 bench, one by one
+m, _, _ = S.read_matrix("tests/fixtures/double__40_0.50_0")
+full = S.perman_shard(m, 0, 1)
+parts, times = [], []
+for world in (2, 4, 8):
+    parts, times = [], []
+    for r in range(world):
+        v, st = S.perman_shard(m, r, world, return_stats=True)
+        parts.append(v)
+        times.append(st["kernel_ms"])
+    import math
+    tot = math.fsum(parts)
+    print(f"shards={world}: kernel ms per shard min {min(times):.1f} max {max(times):.1f} "
+          f"(1-GPU {1152.0 if False else 0:.0f}) sum rel-diff vs full {abs(tot - full) / abs(full):.2e}", flush=True)
