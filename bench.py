@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
     ap.add_argument("--kernel", default="dense", choices=["dense", "dense_plain", "sparse", "skip"],
                     help="dense = -p4/-p6 (engine picks plain or prefix-blocked walk); sparse/skip = -s paths")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="all ranks on device 0 over gloo: rehearse the N-rank path on a one-GPU box")
     ap.add_argument("--prep", type=int, default=0, choices=[0, 1, 2], help="-r: 1 SortOrder, 2 SkipOrder")
     return ap.parse_args()
 
@@ -99,9 +101,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # --rehearse: every rank on device 0 with gloo (multi-rank rehearsal on a
+    # one-GPU box); the real N-GPU run uses one device per rank and RCCL.
+    dev = 0 if args.rehearse else local
+    tdev = "cpu" if args.rehearse else f"cuda:{dev}"
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev)
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     import superman_amd as S
 
     a, typ, _ = S.read_matrix(args.matrix)
@@ -113,12 +122,11 @@ def main():
     L, m, _ = S.layout(n)
     c0, c1 = shard_chunks(n, rank, world)
     my_steps = (c1 - c0) << (L + m)
-    dev = local
 
     def step():
         part, st = S.perman_shard(a, rank, world, kernel=args.kernel, device_id=dev, return_stats=True)
         if world > 1:
-            t = torch.tensor([part], dtype=torch.float64, device=f"cuda:{local}")
+            t = torch.tensor([part], dtype=torch.float64, device=tdev)
             dist.all_reduce(t)  # RCCL over xGMI: the single data-path collective
             part = float(t.item())
         return (4 * (n & 1) - 2) * part, st
@@ -139,7 +147,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
