@@ -6,10 +6,9 @@ matrix double/40_0.50_0 (n = 40, d = 0.5), dense walk (-p4/-p6 path), all
 2^39 Gray steps per "step".  With N ranks (one process per GPU, launched by
 torch.distributed.run) the 2^h wave-chunks are split into N contiguous
 power-of-two-aligned shards; each rank walks its shard through the C ABI
-(sup_partial) and one RCCL all-reduce (torch.distributed, backend nccl)
-sums the fp64 partials — the only data-path collective.  Weak per-job
-scaling is NOT used: total work per step is fixed (the permanent), so
-scaling is "strong".
+(sup_perman_shard) and one RCCL all-reduce (torch.distributed, backend nccl)
+sums the fp64 partials — the only data-path collective.  Total work per
+step is fixed (one permanent), so scaling is "strong".
 
 Prints ONE JSON line on rank 0 (driver contract), including the roofline of
 the walk kernel (hipEvents on its own stream, measured inside the library)
@@ -59,7 +58,7 @@ def shard_chunks(n: int, rank: int, world: int) -> tuple[int, int]:
 
 def pmc_traffic(n: int):
     """HBM bytes per walk launch from the committed rocprofv3 PMC summary, if any."""
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc*.json"), recursive=True), reverse=True):
         try:
             d = json.load(open(p))
             if d.get("n") == n and "hbm_bytes_per_launch" in d:

@@ -84,7 +84,7 @@ def _opts(gpu_num=1, device_id=0, threads=16, cpu=False, walk_log2=0, chunk_log2
     lib.sup_opts_init(C.byref(o))
     o.gpu_num, o.device_id, o.threads = int(gpu_num), int(device_id), int(threads)
     o.cpu_worker, o.walk_log2, o.chunk_log2 = int(bool(cpu)), int(walk_log2), int(chunk_log2)
-    o.use_rccl, o.verbose = int(bool(use_rccl)), int(bool(verbose))
+    o.use_rccl, o.verbose = int(use_rccl), int(bool(verbose))  # use_rccl=2: RCCL even on one device
     return o
 
 

@@ -546,7 +546,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
       out.grid = std::max(out.grid, rr[g].grid);
     }
     out.devices = G;
-    if (G > 1 && o.use_rccl) {
+    if ((G > 1 && o.use_rccl) || o.use_rccl == 2) {  // 2: also on one device (exercises RCCL)
       rc = rccl_allreduce_partials(devs, out.dev_partials, &out.total);
       if (rc) return rc;
     } else {
@@ -633,7 +633,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     out.grid = std::max(out.grid, dev_grid[g]);
   }
   out.dev_partials = dev_sum;
-  if (G > 1 && o.use_rccl && !o.cpu_worker) {
+  if (((G > 1 && o.use_rccl) || o.use_rccl == 2) && !o.cpu_worker) {
     rc = rccl_allreduce_partials(devs, dev_sum, &out.total);
     if (rc) return rc;
   } else {

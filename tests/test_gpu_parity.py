@@ -159,6 +159,28 @@ def test_schedulers_agree_bitwise(sup):
         assert sup.perman(a, algo) == r4
 
 
+def test_rccl_combine_single_device(sup):
+    # in-process RCCL path (ncclCommInitAll + ncclAllReduce) of -p5/-p6 -R,
+    # exercised on one device: the all-reduce of one partial is the identity
+    a, _, _ = sup.read_matrix(fixture_path("synth/22_0.50_double"))
+    r4 = sup.perman(a, 4)
+    assert sup.perman(a, 5, gpu_num=1, use_rccl=2) == r4
+    assert sup.perman(a, 6, gpu_num=1, use_rccl=2) == r4
+
+
+def test_shards_sum_to_full(sup):
+    # sup_perman_shard: the bench's per-rank unit; 2^k shards are subtrees of
+    # the fixed reduction, so pairing them reproduces the single-launch bits
+    a, _, _ = sup.read_matrix(fixture_path("double__30_0.50_0"))
+    full = sup.perman_shard(a, 0, 1)
+    for world in (2, 4, 8):
+        parts = [sup.perman_shard(a, r, world) for r in range(world)]
+        while len(parts) > 1:
+            parts = [parts[i] + parts[i + 1] for i in range(0, len(parts), 2)]
+        assert parts[0] == full
+    assert -2 * full == sup.perman(a, 4)  # n even: perm = -2 * sum
+
+
 def test_hybrid_cpu_worker(sup):
     a, _, _ = sup.read_matrix(fixture_path("synth/22_0.50_double"))
     r4 = sup.perman(a, 4)
