@@ -83,7 +83,8 @@ typedef struct {
   int block_dim;      /* 0 = auto (256); the engine only supports 256                         */
   int walk_log2;      /* 0 = auto; Gray steps walked per wave-chunk = 2^walk_log2            */
   int chunk_log2;     /* 0 = auto; for SUP_SCHED_CHUNKS: wave-chunks per queue item = 2^x    */
-  int use_rccl;       /* multi-device: combine per-device partials with one RCCL all-reduce  */
+  int use_rccl;       /* 1: multi-device partials combined by one RCCL all-reduce (bit-     */
+                      /*    identical to the host combine); 2: also with a single device    */
   int verbose;        /* print per-device / per-chunk timing lines like the reference        */
 } sup_opts;
 

@@ -446,8 +446,16 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
 }
 
 // ------------------------------------------------------------------ RCCL --
-int rccl_allreduce_partials(const std::vector<int>& devs, std::vector<double>& vals, double* out) {
+// Combine per-device partials over RCCL without giving up the fixed reduction
+// order: device g contributes a vector that is zero outside the slots it owns
+// (its own partial, or the chunk items it dequeued).  Every slot then has one
+// nonzero addend, so the all-reduce SUM is exact whatever ring order RCCL
+// uses, and the caller folds the merged vector with the same pairwise tree
+// as the host path: -R results are bit-identical to the host combine.
+int rccl_allreduce_partials(const std::vector<int>& devs, const std::vector<std::vector<double>>& contrib,
+                            std::vector<double>& merged) {
   const int G = (int)devs.size();
+  const size_t len = merged.size();
   std::vector<ncclComm_t> comms(G);
   ncclResult_t nr = ncclCommInitAll(comms.data(), G, devs.data());
   if (nr != ncclSuccess) {
@@ -458,9 +466,9 @@ int rccl_allreduce_partials(const std::vector<int>& devs, std::vector<double>& v
   std::vector<hipStream_t> st(G, nullptr);
   int rc = SUP_OK;
   for (int g = 0; g < G && rc == SUP_OK; ++g) {
-    if (hipSetDevice(devs[g]) != hipSuccess || hipMalloc(&buf[g], sizeof(double)) != hipSuccess ||
-        hipStreamCreate(&st[g]) != hipSuccess ||
-        hipMemcpy(buf[g], &vals[g], sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+    if (contrib[g].size() != len || hipSetDevice(devs[g]) != hipSuccess ||
+        hipMalloc(&buf[g], len * sizeof(double)) != hipSuccess || hipStreamCreate(&st[g]) != hipSuccess ||
+        hipMemcpy(buf[g], contrib[g].data(), len * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
       set_error("RCCL staging buffer setup failed");
       rc = SUP_EHIP;
     }
@@ -468,7 +476,7 @@ int rccl_allreduce_partials(const std::vector<int>& devs, std::vector<double>& v
   if (rc == SUP_OK) {
     ncclGroupStart();
     for (int g = 0; g < G; ++g) {
-      nr = ncclAllReduce(buf[g], buf[g], 1, ncclFloat64, ncclSum, comms[g], st[g]);
+      nr = ncclAllReduce(buf[g], buf[g], len, ncclFloat64, ncclSum, comms[g], st[g]);
       if (nr != ncclSuccess) break;
     }
     ncclResult_t ge = ncclGroupEnd();
@@ -482,7 +490,9 @@ int rccl_allreduce_partials(const std::vector<int>& devs, std::vector<double>& v
       if (hipSetDevice(devs[g]) != hipSuccess || hipStreamSynchronize(st[g]) != hipSuccess) rc = SUP_EHIP;
     }
     (void)hipSetDevice(devs[0]);
-    if (hipMemcpy(out, buf[0], sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) rc = SUP_EHIP;
+    if (hipMemcpy(merged.data(), buf[0], len * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+      rc = SUP_EHIP;
+    if (rc) set_error("RCCL all-reduce completion failed");
   }
   for (int g = 0; g < G; ++g) {
     (void)hipSetDevice(devs[g]);
@@ -547,8 +557,12 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     }
     out.devices = G;
     if ((G > 1 && o.use_rccl) || o.use_rccl == 2) {  // 2: also on one device (exercises RCCL)
-      rc = rccl_allreduce_partials(devs, out.dev_partials, &out.total);
+      std::vector<std::vector<double>> contrib(G, std::vector<double>(G, 0.0));
+      for (int g = 0; g < G; ++g) contrib[g][g] = out.dev_partials[g];
+      std::vector<double> merged(G, 0.0);
+      rc = rccl_allreduce_partials(devs, contrib, merged);
       if (rc) return rc;
+      out.total = pairwise_host(merged);
     } else {
       out.total = pairwise_host(out.dev_partials);
     }
@@ -568,6 +582,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   }
   const uint64_t nitems = (total + item - 1) / item;
   std::vector<double> ipart(nitems, 0.0);
+  std::vector<int> owner(nitems, 0);
   std::vector<double> dev_ms(G + 1, 0.0);
   std::vector<uint64_t> dev_vis(G + 1, 0);
   std::vector<int> dev_grid(G + 1, 0);
@@ -596,6 +611,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
         std::printf("ChunkID %llu is DONE by kernel%d in %f\n", (unsigned long long)it, devs[g], s);
       }
       ipart[it] = r.partial;
+      owner[it] = g;
       dev_sum[g] += r.partial;
       dev_ms[g] += r.kernel_ms;
       dev_vis[g] += r.visited;
@@ -634,8 +650,13 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   }
   out.dev_partials = dev_sum;
   if (((G > 1 && o.use_rccl) || o.use_rccl == 2) && !o.cpu_worker) {
-    rc = rccl_allreduce_partials(devs, dev_sum, &out.total);
+    // device g owns the items it dequeued; the others contribute 0 there
+    std::vector<std::vector<double>> contrib(G, std::vector<double>(nitems, 0.0));
+    for (uint64_t it = 0; it < nitems; ++it) contrib[owner[it]][it] = ipart[it];
+    std::vector<double> merged(nitems, 0.0);
+    rc = rccl_allreduce_partials(devs, contrib, merged);
     if (rc) return rc;
+    out.total = pairwise_host(merged);
   } else {
     out.total = pairwise_host(ipart);
   }

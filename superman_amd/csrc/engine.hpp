@@ -95,8 +95,10 @@ struct SchedResult {
 int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uint64_t c1,
              SchedResult& out);
 
-// All-reduce (sum, fp64) of one value per device over RCCL, in one process.
-int rccl_allreduce_partials(const std::vector<int>& devs, std::vector<double>& vals, double* out);
+// All-reduce (sum, fp64) over RCCL, in one process, of per-device vectors with
+// disjoint supports (exact in any order); merged = the slot-wise sum.
+int rccl_allreduce_partials(const std::vector<int>& devs, const std::vector<std::vector<double>>& contrib,
+                            std::vector<double>& merged);
 
 // CPU worker: the same wave-chunk walk on host threads (used for `-c` and for
 // the hybrid `-c -g` chunk queue).  Bit-identical to the dense/sparse kernels.

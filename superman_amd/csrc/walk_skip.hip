@@ -54,45 +54,38 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
       double acc = 0.0;
       uint32_t visited = 0;
       uint32_t t = 0;
-      while (true) {
-        // state t: X is valid for walk index t
-        ++visited;
-        const double term = U[0];
-        acc = (t & 1u) ? acc - term : acc + term;
-        uint32_t next = t + 1;
-        if (__builtin_amdgcn_ballot_w64(term != 0.0) == 0) {
-          // every lane is zero: look for exact zeros on lane-uniform rows.  Those
-          // rows hold the same value on every lane, so lane 0's view decides.
-          // v_cmp straight into an SGPR mask per row (no VGPR temporaries)
-          uint64_t zm = 0;
+      // Zero check after visiting state t (X valid for t, term added): if
+      // every lane's term is zero and some lane-uniform row is exactly zero,
+      // returns the index to continue from (X moved there), else t + 1 with
+      // X untouched (the caller takes the ordinary single-bit step).
+      auto jump = [&](uint32_t t) -> uint32_t {
+        // v_cmp straight into an SGPR mask per row (no VGPR temporaries);
+        // lane-uniform rows hold the same value on every lane, so lane 0 decides
+        uint64_t zm = 0;
 #pragma unroll
-          for (int r = 0; r < N; ++r) zm |= (__builtin_amdgcn_ballot_w64(x[r] == 0.0) & 1ull) << r;
-          zm &= umask;
-          if (zm) {
-            // each zero row r stays zero until one of its walk columns toggles
-            // (or for the rest of the chunk if it has none); the product is
-            // zero until the last of those toggles.
-            uint32_t target = t + 1;
-            while (zm) {
-              const uint32_t r = (uint32_t)__builtin_ctzll(zm);
-              zm &= zm - 1;
-              uint64_t mm = ((const __attribute__((address_space(4))) uint64_t*)p.rowmask)[r];
-              uint32_t tr = T;
-              while (mm) {
-                const uint32_t k = (uint32_t)__builtin_ctzll(mm);
-                mm &= mm - 1;
-                const uint32_t c = next_toggle(t, k);
-                tr = c < tr ? c : tr;
-              }
-              target = tr > target ? tr : target;
-            }
-            next = target;
+        for (int r = 0; r < N; ++r) zm |= (__builtin_amdgcn_ballot_w64(x[r] == 0.0) & 1ull) << r;
+        zm &= umask;
+        if (!zm) return t + 1;
+        // each zero row r stays zero until one of its walk columns toggles (or
+        // for the rest of the chunk if it has none); the product is zero until
+        // the last of those toggles
+        uint32_t target = t + 1;
+        while (zm) {
+          const uint32_t r = (uint32_t)__builtin_ctzll(zm);
+          zm &= zm - 1;
+          uint64_t mm = ((const __attribute__((address_space(4))) uint64_t*)p.rowmask)[r];
+          uint32_t tr = T;
+          while (mm) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(mm);
+            mm &= mm - 1;
+            const uint32_t c = next_toggle(t, k);
+            tr = c < tr ? c : tr;
           }
+          target = tr > target ? tr : target;
         }
-        if (next >= T) break;
-        // Gray move t -> next: flip the differing walk bits in ascending order
-        // (exactly one bit for an ordinary step; several after a jump).
-        const uint32_t gn = next ^ (next >> 1);
+        if (target == t + 1 || target >= T) return target;
+        // Gray move t -> target: flip the differing walk bits in ascending order
+        const uint32_t gn = target ^ (target >> 1);
         uint32_t diff = (t ^ (t >> 1)) ^ gn;
         do {
           const uint32_t k = (uint32_t)__builtin_ctz(diff);
@@ -100,7 +93,26 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
           const uint32_t neg = ((gn >> k) & 1u) ^ 1u;
           sparse_step<N>(x, U, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nb_of(p, k));
         } while (diff);
-        t = next;
+        return target | 0x80000000u;  // flag: X already moved
+      };
+      for (;;) {
+        // visit state t.  acc +/- term as one fma with an exact +-1 factor
+        // (bit-identical to the add/sub, no per-lane select)
+        ++visited;
+        acc = __builtin_fma((t & 1u) ? -1.0 : 1.0, U[0], acc);
+        if (__builtin_amdgcn_ballot_w64(U[0] != 0.0) == 0) {
+          const uint32_t nx = jump(t);
+          if (nx & 0x80000000u) {
+            t = nx & 0x7fffffffu;
+            continue;
+          }
+          if (nx >= T) break;
+        }
+        if (++t >= T) break;
+        // ordinary single-bit Gray step to t
+        const uint32_t k = (uint32_t)__builtin_ctz(t);
+        const uint32_t neg = (t >> (k + 1)) & 1u;
+        sparse_step<N>(x, U, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nb_of(p, k));
       }
       if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;
       const double part = wave_sum(lane_valid ? acc : 0.0);

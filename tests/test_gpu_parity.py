@@ -161,11 +161,16 @@ def test_schedulers_agree_bitwise(sup):
 
 def test_rccl_combine_single_device(sup):
     # in-process RCCL path (ncclCommInitAll + ncclAllReduce) of -p5/-p6 -R,
-    # exercised on one device: the all-reduce of one partial is the identity
+    # exercised on one device.  The all-reduced buffer has one slot per device
+    # (-p5) or per queue item (-p6), each with a single nonzero addend, so the
+    # merged vector is folded by the host's pairwise tree: bit-identical.
     a, _, _ = sup.read_matrix(fixture_path("synth/22_0.50_double"))
     r4 = sup.perman(a, 4)
     assert sup.perman(a, 5, gpu_num=1, use_rccl=2) == r4
     assert sup.perman(a, 6, gpu_num=1, use_rccl=2) == r4
+    assert sup.perman(a, 6, gpu_num=1, use_rccl=2, chunk_log2=2) == r4
+    b = sup.skip_order(a)[0]
+    assert sup.perman(b, 8, sparse=True, gpu_num=1, use_rccl=2) == sup.perman(b, 7, sparse=True)
 
 
 def test_shards_sum_to_full(sup):
@@ -213,6 +218,33 @@ def test_n40_properties(sup):
     # column permutation invariance (rounding-level)
     perm = np.random.default_rng(5).permutation(n)
     assert rel(sup.perman(a[:, perm]), r) < 1e-9
+
+
+@pytest.mark.parametrize("typ", ["int", "double"])
+def test_config5_n44(sup, orc, typ):
+    # BASELINE config 5 (n = 44, d = 0.15, synthetic: tests/fixtures/gen_config5.py).
+    # Aligned 2^23-step ranges against the reference chunk helpers restated
+    # (cpu_perman64_sparse / _skipper, gpu_exact_sparse.cu:6-191) and bit-exact
+    # against the engine mirror; the full 2^43 walk through properties.
+    a, _, _ = sup.read_matrix(fixture_path(f"synth44_0.15_{typ}"))
+    b = sup.skip_order(a)[0]
+    n, q = 44, 1 << 23
+    for k in (1, 777, 1 << 19, (1 << 20) - 1):
+        s, e = k * q, (k + 1) * q
+        for kind, fn in (("sparse", orc.ref_sparse_partial), ("skip", orc.ref_skip_partial)):
+            got = sup.partial(b, s, e, kernel=kind)
+            assert rel(got, fn(b, s, e, 8)) < 1e-9, (kind, k)
+            L, ml = _partial_layout(sup, n, s, e)
+            mir, _ = orc.engine_range(b, kind, s >> (L + ml), e >> (L + ml), L, ml, None, 8)
+            assert got == mir, (kind, k)
+    r_sp = sup.perman(b, algo=4, sparse=True)
+    r_sk, st = sup.perman(b, algo=8, sparse=True, return_stats=True)
+    assert np.isfinite(r_sp) and r_sp > 0 and rel(r_sk, r_sp) < 1e-9
+    if typ == "int":
+        assert st["visited_steps"] < 0.5 * 2.0 ** 43  # SkipPer jumps over exact-zero rows
+    c = b.astype(np.float64)
+    c[5] *= 2.0
+    assert sup.perman(c, algo=4, sparse=True) == 2.0 * r_sp  # power-of-two row scaling is exact
 
 
 def test_cli_gpu(sup, orc):

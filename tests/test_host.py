@@ -111,3 +111,19 @@ def test_nw_start_matches_oracle(sup, orc):
     x, p = sup.nw_start(a)
     xo, po = orc.nw_start(a)
     assert np.array_equal(x, xo) and p == po
+
+
+def test_config5_fixtures_reproducible(sup, tmp_path):
+    # BASELINE config 5 has no reference file: the committed inputs must be
+    # exactly what tests/fixtures/gen_config5.py generates
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_config5", os.path.join(FIX, "gen_config5.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    for typ in ("int", "double"):
+        a, _ = g.generate(44, 0.15, typ)
+        g.write_v1(str(tmp_path / typ), a, typ)
+        assert open(tmp_path / typ).read() == open(fixture_path(f"synth44_0.15_{typ}")).read()
+        b, t, _ = sup.read_matrix(fixture_path(f"synth44_0.15_{typ}"))
+        assert t == typ and np.array_equal(a, b)
+        assert (b != 0).any(0).all() and (b != 0).any(1).all()

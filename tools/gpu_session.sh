@@ -10,7 +10,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 run() {  # name seconds cmd...
-  local name=$1 secs=$2; shift 2
+  local name=${1//[^A-Za-z0-9_.-]/_} secs=$2; shift 2
   echo "== $name ($(date +%T))"
   timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?

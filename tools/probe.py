@@ -34,16 +34,22 @@ def run(label, m, kernel, reps=2):
           flush=True)
 
 
+only = sys.argv[1:]  # optional subset of fixture names
 for path, prep in (("double__32_0.50_0", 0), ("double__36_0.20_0", 1), ("double__40_0.50_0", 0),
-                   ("int__36_0.20_0", 2)):
+                   ("int__36_0.20_0", 2), ("synth44_0.15_int", 2), ("synth44_0.15_double", 2)):
+    if only and path not in only:
+        continue
     m, _, _ = S.read_matrix(os.path.join("tests/fixtures", path))
     if prep == 1:
         m = S.sort_order(m)[0]
     if prep == 2:
         m = S.skip_order(m)[0]
-    for kernel in ("dense_plain", "dense", "sparse") + (("skip",) if prep == 2 else ()):
-        run(f"{path} r{prep}", m, kernel)
+    for kernel in (("sparse", "skip") if m.shape[0] > 40 else
+                   ("dense_plain", "dense", "sparse") + (("skip",) if prep == 2 else ())):
+        run(f"{path} r{prep}", m, kernel, reps=1 if m.shape[0] > 40 else 2)
 
+if only:
+    sys.exit(0)
 # strong-scaling rehearsal on one GPU: the 8 shards of the n=40 bench, one by one
 m, _, _ = S.read_matrix("tests/fixtures/double__40_0.50_0")
 full = S.perman_shard(m, 0, 1)
