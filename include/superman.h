@@ -48,6 +48,9 @@ extern "C" {
 #define SUP_EUNSUPPORTED (-7)  /* algorithm id / option combination not provided         */
 
 #define SUP_MAX_N 64           /* 64-bit Gray index: reference limit algo.h:752,781      */
+#define SUP_MAX_READ_N 4096    /* MatrixMarket input and sup_decompose: larger matrices
+                                  are accepted when the -o reductions shrink every leaf
+                                  to <= SUP_MAX_N                                       */
 
 /* ---- storage type of the input matrix (reference template parameter T) -- */
 typedef enum {
@@ -100,7 +103,7 @@ typedef struct {
   int      chunks_done_cpu; /* queue items taken by the CPU worker                              */
   double   partials[16];    /* per-device partial sums (before the final combine)              */
   int      walk_kind;       /* walk actually run: 0 dense, 1 prefix-blocked (SpaRyser), 2 SkipPer */
-  int      reserved_;
+  int      leaves;          /* permanents computed: 1, or the leaf count of sup_perman_reduced   */
   double   est_ops_per_step;/* cost model: fp64 VALU ops per Gray step and lane                 */
 } sup_stats;
 
@@ -219,6 +222,50 @@ int sup_sort_order(void* mat, sup_dtype t, int n, int* colperm);
 /* SkipOrder: greedy min-degree column order, rows in first-touch order;
  * rewrites mat in place.  (util.h:621-684) */
 int sup_skip_order(void* mat, sup_dtype t, int n, int* rowperm, int* colperm);
+
+/* MatrixMarket coordinate file (revised_perman/read_matrix.hpp:11-157 and
+ * main.cpp:1515-1580): banner "%%MatrixMarket matrix coordinate <type>
+ * <symmetry>", '%' comments, "M N nz", 1-based "i j [v]" entries.  real ->
+ * SUP_FLOAT64; integer / pattern (or binary) -> SUP_INT32; pattern or binary
+ * entries are 1; symmetric and skew-symmetric files mirror every off-diagonal
+ * entry with the SAME value (as the reference does); complex, array format
+ * and non-square matrices are rejected (SUP_EIO).  nnz_lines = nz from the
+ * size line.  n may be up to SUP_MAX_READ_N (for sup_perman_reduced).
+ * sup_read_matrix also accepts MatrixMarket files (detected by the banner),
+ * so the CLI's -f takes either format. */
+int sup_read_mtx(const char* path, int binary, void** mat, sup_dtype* t, int* n, int* nnz_lines);
+
+/* ------------------------------------------------------------------------ *
+ * Reductions in front of the engine (reference v2
+ * -o / -u, revised_perman/main.cpp:993-1264, util.h:1138-1593).
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int compress;           /* -o: remove degree-1/2 rows+columns, then expand rows/columns of
+                             degree < max_deg while n > min_n (d1/d2/d34 recursion)            */
+  double scale_threshold; /* -u <t>: scale rows/columns to sums t before each permanent and
+                             divide the factors out afterwards; <= 0 = off                      */
+  int min_n;              /* recursion stops at n <= min_n (reference: 30)                      */
+  int max_deg;            /* expand only while the minimum degree < max_deg (reference: 5)      */
+  int preprocessing;      /* -r applied to every leaf: 0 none, 1 SortOrder, 2 SkipOrder         */
+} sup_reduce_opts;
+void sup_reduce_opts_init(sup_reduce_opts* r);
+
+/* Leaf permanent callback: perm of the n x n fp64 row-major matrix a. */
+typedef int (*sup_leaf_fn)(const double* a, int n, void* user, double* out_perm);
+
+/* Reduce `mat` and combine fn(leaf) over the expansion tree (left + right,
+ * scale factors divided out).  No device work of its own: fn decides how each
+ * leaf is computed.  *n_leaves = number of fn calls.  n <= SUP_MAX_READ_N;
+ * a leaf larger than SUP_MAX_N fails with SUP_EUNSUPPORTED. */
+int sup_decompose(const void* mat, sup_dtype t, int n, const sup_reduce_opts* r, sup_leaf_fn fn, void* user,
+                  double* out, int* n_leaves);
+
+/* sup_decompose with every leaf computed by the engine: sup_perman (on_cpu =
+ * 0) or sup_perman_cpu (on_cpu = 1, o->threads threads) after r->preprocessing.
+ * st accumulates over the leaves (kernel_ms, wall_ms, gray_steps, visited_steps,
+ * leaves); the other fields describe the last leaf. */
+int sup_perman_reduced(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched sched, const sup_opts* o,
+                       int on_cpu, const sup_reduce_opts* r, double* out, sup_stats* st);
 
 #ifdef __cplusplus
 }

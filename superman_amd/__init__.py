@@ -15,11 +15,12 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import (KERNEL_DENSE, KERNEL_SKIPPER, KERNEL_SPARYSER, SCHED_CHUNKS, SCHED_SINGLE,
-                   SCHED_STATIC, SupError, SupOpts, SupStats)
+from ._lib import (KERNEL_DENSE, KERNEL_SKIPPER, KERNEL_SPARYSER, LEAF_FN, SCHED_CHUNKS, SCHED_SINGLE,
+                   SCHED_STATIC, SupError, SupOpts, SupReduceOpts, SupStats)
 
 __all__ = [
-    "perman", "perman_cpu", "partial", "perman_shard", "plan_info", "read_matrix", "sort_order", "skip_order", "compress",
+    "perman", "perman_cpu", "partial", "perman_shard", "plan_info", "read_matrix", "read_mtx", "sort_order",
+    "skip_order", "compress", "decompose", "perman_reduced",
     "nw_start", "device_count", "layout", "SupError", "ALGOS_DENSE", "ALGOS_SPARSE",
     "gpu_perman64_xshared_coalescing_mshared",
     "gpu_perman64_xshared_coalescing_mshared_multigpu",
@@ -64,7 +65,7 @@ _KERNELS = {"dense": KERNEL_DENSE, "sparse": KERNEL_SPARYSER, "spa": KERNEL_SPAR
 WALK_NAMES = {0: "dense", 1: "sparse", 2: "skip"}
 
 
-def _mat(a) -> tuple[np.ndarray, int, int]:
+def _mat(a, max_n: int = 64) -> tuple[np.ndarray, int, int]:
     a = np.asarray(a)
     if a.dtype not in _DT:
         a = a.astype(np.float64)
@@ -72,8 +73,8 @@ def _mat(a) -> tuple[np.ndarray, int, int]:
     if a.ndim != 2 or a.shape[0] != a.shape[1]:
         raise ValueError(f"expected a square matrix, got shape {a.shape}")
     n = a.shape[0]
-    if not 1 <= n <= 64:
-        raise ValueError(f"n = {n} outside [1, 64] (64-bit Gray index)")
+    if not 1 <= n <= max_n:
+        raise ValueError(f"n = {n} outside [1, {max_n}]" + (" (64-bit Gray index)" if max_n == 64 else ""))
     return a, _DT[a.dtype], n
 
 
@@ -186,7 +187,8 @@ def nw_start(mat) -> tuple[np.ndarray, float]:
 
 
 def read_matrix(path: str, binary: bool = False) -> tuple[np.ndarray, str, int]:
-    """v1 matrix file -> (matrix, type name, nnz from the header) (util.h:343-358)."""
+    """v1 matrix file -> (matrix, type name, nnz from the header) (util.h:343-358).
+    MatrixMarket files (detected by their banner) are read as by read_mtx."""
     lib = _lib.load()
     p, t, n, nnz = C.c_void_p(), C.c_int(), C.c_int(), C.c_int()
     _lib.check(lib.sup_read_matrix(path.encode(), int(bool(binary)), C.byref(p), C.byref(t), C.byref(n),
@@ -269,3 +271,79 @@ def gpu_perman64_xshared_coalescing_mshared_skipper(mat, grid_dim=2048, block_di
 def gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper(mat, gpu_num, cpu=False, threads=16,
                                                                        grid_dim=2048, block_dim=256):
     return perman(mat, 8, sparse=True, gpu_num=gpu_num, cpu=cpu, threads=threads)
+
+
+def _reduce_opts(compress=True, scale=None, min_n=30, max_deg=5, preprocessing=0) -> SupReduceOpts:
+    lib = _lib.load()
+    r = SupReduceOpts()
+    lib.sup_reduce_opts_init(C.byref(r))
+    r.compress = int(bool(compress))
+    r.scale_threshold = float(scale) if scale else 0.0
+    r.min_n, r.max_deg, r.preprocessing = int(min_n), int(max_deg), int(preprocessing)
+    return r
+
+
+def decompose(mat, leaf, compress: bool = True, scale=None, min_n: int = 30, max_deg: int = 5):
+    """Reductions of the reference's -o / -u (revised_perman/main.cpp:993-1264)
+    with a Python leaf function: returns (perm, leaves) where perm combines
+    leaf(A_leaf) over the d1/d2/d34 expansion tree and divides scale factors
+    out, and leaves lists every leaf matrix handed to `leaf`."""
+    a, dt, n = _mat(mat, 4096)
+    lib = _lib.load()
+    seen, err = [], []
+
+    def cb(ptr, k, _user, out):
+        try:
+            m = np.ctypeslib.as_array(ptr, shape=(k * k,)).reshape(k, k).copy()
+            seen.append(m)
+            out[0] = float(leaf(m))
+            return 0
+        except Exception as e:  # surfaced after the C call returns
+            err.append(e)
+            return -1
+
+    fn = LEAF_FN(cb)
+    r = _reduce_opts(compress, scale, min_n, max_deg)
+    out, nl = C.c_double(0.0), C.c_int(0)
+    rc = lib.sup_decompose(a.ctypes.data, dt, n, C.byref(r), fn, None, C.byref(out), C.byref(nl))
+    if err:
+        raise err[0]
+    _lib.check(rc, "decompose")
+    return out.value, seen
+
+
+def perman_reduced(mat, algo: int = 4, sparse: bool = False, compress: bool = True, scale=None,
+                   preprocessing: int = 0, gpu_num: int = 1, cpu: bool = False, threads: int = 16,
+                   device_id: int = 0, min_n: int = 30, max_deg: int = 5, return_stats: bool = False):
+    """-o / -u front end: reduce the matrix, then run the algorithm `algo` on
+    every leaf (after -r `preprocessing`) on the GPU, or on host threads with
+    cpu=True (the CLI's -c)."""
+    table = ALGOS_SPARSE if sparse else ALGOS_DENSE
+    if algo not in table:
+        raise SupError(-7, "perman_reduced", f"unknown algorithm id {algo}")
+    _, kernel, sched = table[algo]
+    if sched == SCHED_SINGLE:
+        gpu_num = 1
+    a, dt, n = _mat(mat, 4096)
+    lib = _lib.load()
+    o = _opts(gpu_num, device_id, threads)
+    r = _reduce_opts(compress, scale, min_n, max_deg, preprocessing)
+    out, st = C.c_double(0.0), SupStats()
+    _lib.check(lib.sup_perman_reduced(a.ctypes.data, dt, n, kernel, sched, C.byref(o), int(bool(cpu)), C.byref(r),
+                                      C.byref(out), C.byref(st)), "perman_reduced")
+    return (out.value, st.as_dict()) if return_stats else out.value
+
+
+def read_mtx(path: str, binary: bool = False) -> tuple[np.ndarray, str, int]:
+    """MatrixMarket coordinate file -> (matrix, type name, nz lines) (read_matrix.hpp:11-157)."""
+    lib = _lib.load()
+    p, t, n, nnz = C.c_void_p(), C.c_int(), C.c_int(), C.c_int()
+    _lib.check(lib.sup_read_mtx(path.encode(), int(bool(binary)), C.byref(p), C.byref(t), C.byref(n),
+                                C.byref(nnz)), f"read_mtx({path})")
+    try:
+        dtype = _NP[t.value]
+        buf = (C.c_char * (n.value * n.value * np.dtype(dtype).itemsize)).from_address(p.value)
+        m = np.frombuffer(buf, dtype=dtype).reshape(n.value, n.value).copy()
+    finally:
+        lib.sup_free(p)
+    return m, _TYPE_NAME[t.value], nnz.value

@@ -43,7 +43,8 @@ EXPORTS = [
     "sup_gpu_perman64_xshared_coalescing_mshared_skipper",
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper",
     "sup_read_matrix", "sup_free", "sup_count_nnz", "sup_compress",
-    "sup_sort_order", "sup_skip_order",
+    "sup_sort_order", "sup_skip_order", "sup_read_mtx",
+    "sup_reduce_opts_init", "sup_decompose", "sup_perman_reduced",
 ]
 
 
@@ -56,13 +57,24 @@ class SupOpts(C.Structure):
     ]
 
 
+class SupReduceOpts(C.Structure):
+    _fields_ = [
+        ("compress", C.c_int), ("scale_threshold", C.c_double), ("min_n", C.c_int),
+        ("max_deg", C.c_int), ("preprocessing", C.c_int),
+    ]
+
+
+# int (*sup_leaf_fn)(const double* a, int n, void* user, double* out_perm)
+LEAF_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int, C.c_void_p, C.POINTER(C.c_double))
+
+
 class SupStats(C.Structure):
     _fields_ = [
         ("kernel_ms", C.c_double), ("wall_ms", C.c_double),
         ("gray_steps", C.c_uint64), ("visited_steps", C.c_uint64),
         ("devices_used", C.c_int), ("lane_bits", C.c_int), ("walk_bits", C.c_int),
         ("grid", C.c_int), ("chunks_done_cpu", C.c_int), ("partials", C.c_double * 16),
-        ("walk_kind", C.c_int), ("reserved_", C.c_int), ("est_ops_per_step", C.c_double),
+        ("walk_kind", C.c_int), ("leaves", C.c_int), ("est_ops_per_step", C.c_double),
     ]
 
     def as_dict(self) -> dict:
@@ -128,8 +140,14 @@ def _declare(lib: C.CDLL) -> None:
     lib.sup_compress.argtypes = [P, I, I, P, P, P, P, P, P]
     lib.sup_sort_order.argtypes = [P, I, I, P]
     lib.sup_skip_order.argtypes = [P, I, I, P, P]
+    lib.sup_read_mtx.argtypes = [C.c_char_p, I, C.POINTER(P), C.POINTER(I), C.POINTER(I), C.POINTER(I)]
+    lib.sup_reduce_opts_init.argtypes = [C.POINTER(SupReduceOpts)]
+    lib.sup_reduce_opts_init.restype = None
+    lib.sup_decompose.argtypes = [P, I, I, C.POINTER(SupReduceOpts), LEAF_FN, P, C.POINTER(D), C.POINTER(I)]
+    lib.sup_perman_reduced.argtypes = [P, I, I, I, I, C.POINTER(SupOpts), I, C.POINTER(SupReduceOpts),
+                                       C.POINTER(D), C.POINTER(SupStats)]
     for name in EXPORTS:
-        if name not in ("sup_opts_init", "sup_free", "sup_last_error"):
+        if name not in ("sup_opts_init", "sup_free", "sup_last_error", "sup_reduce_opts_init"):
             getattr(lib, name).restype = I
 
 

@@ -42,6 +42,7 @@ void fill_stats(sup_stats* st, const Plan& P, const SchedResult& r, double wall_
   st->chunks_done_cpu = r.cpu_items;
   for (size_t i = 0; i < r.dev_partials.size() && i < 16; ++i) st->partials[i] = r.dev_partials[i];
   st->walk_kind = (int)P.kind;
+  st->leaves = 1;
   st->est_ops_per_step = walk_cost(P);
 }
 
@@ -255,6 +256,71 @@ int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper(const
                                                                            int cpu, int threads, int, int,
                                                                            double* out) {
   return run_ref(mat, t, nov, SUP_KERNEL_SKIPPER, SUP_SCHED_CHUNKS, gpu_num, cpu, threads, out);
+}
+
+
+// ---- reductions + engine (sup_decompose with engine leaves) ----------------
+namespace {
+struct LeafCtx {
+  sup_kernel kernel;
+  sup_sched sched;
+  sup_opts o;
+  int on_cpu;
+  int preprocessing;
+  sup_stats acc;
+  bool first = true;
+};
+
+int engine_leaf(const double* a, int n, void* user, double* out) {
+  LeafCtx& c = *(LeafCtx*)user;
+  std::vector<double> m(a, a + (size_t)n * n);
+  std::vector<int> rp(n), cp(n);
+  int rc = SUP_OK;
+  // main.cpp:983-988: every leaf's CSR/CSC is built with the -r order
+  if (c.preprocessing == 1) rc = sup_sort_order(m.data(), SUP_FLOAT64, n, cp.data());
+  else if (c.preprocessing == 2) rc = sup_skip_order(m.data(), SUP_FLOAT64, n, rp.data(), cp.data());
+  if (rc) return rc;
+  sup_stats st;
+  rc = c.on_cpu ? sup_perman_cpu(m.data(), SUP_FLOAT64, n, c.kernel, c.o.threads, out, &st)
+                : sup_perman(m.data(), SUP_FLOAT64, n, c.kernel, c.sched, &c.o, out, &st);
+  if (rc) return rc;
+  if (c.first) {
+    c.acc = st;
+    c.first = false;
+  } else {
+    const sup_stats prev = c.acc;
+    c.acc = st;
+    c.acc.kernel_ms += prev.kernel_ms;
+    c.acc.wall_ms += prev.wall_ms;
+    c.acc.gray_steps += prev.gray_steps;
+    c.acc.visited_steps += prev.visited_steps;
+    c.acc.leaves += prev.leaves;
+  }
+  return SUP_OK;
+}
+}  // namespace
+
+int sup_perman_reduced(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched sched, const sup_opts* o_in,
+                       int on_cpu, const sup_reduce_opts* r_in, double* out, sup_stats* st) {
+  LeafCtx c;
+  c.kernel = kernel;
+  c.sched = sched;
+  if (o_in) c.o = *o_in;
+  else sup_opts_init(&c.o);
+  c.on_cpu = on_cpu;
+  sup_reduce_opts r;
+  if (r_in) r = *r_in;
+  else sup_reduce_opts_init(&r);
+  c.preprocessing = r.preprocessing;
+  std::memset(&c.acc, 0, sizeof(c.acc));
+  int leaves = 0;
+  const int rc = sup_decompose(mat, t, n, &r, engine_leaf, &c, out, &leaves);
+  if (rc) return rc;
+  if (st) {
+    *st = c.acc;
+    st->leaves = leaves;
+  }
+  return SUP_OK;
 }
 
 }  // extern "C"

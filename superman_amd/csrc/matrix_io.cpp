@@ -1,6 +1,7 @@
 // matrix_io.cpp — host preprocessing on the hot path:
 // v1 matrix reader, CSR/CSC, SortOrder, SkipOrder.
 #include <algorithm>
+#include <cctype>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -36,6 +37,107 @@ using namespace sup;
 
 extern "C" {
 
+// MatrixMarket coordinate reader: mmio banner checks as revised_perman/
+// main.cpp:1522-1575, entries as read_matrix.hpp:11-157 (1-based, '%' lines
+// skipped, symmetric / skew files mirrored with the same value, pattern or -b
+// entries = 1, later duplicates overwrite earlier ones).
+int sup_read_mtx(const char* path, int binary, void** mat, sup_dtype* t, int* n, int* nnz_lines) {
+  if (!path || !mat || !t || !n) {
+    set_error("null argument");
+    return SUP_EINVAL;
+  }
+  std::ifstream in(path);
+  if (!in) {
+    set_error(std::string("cannot open matrix file ") + path);
+    return SUP_EIO;
+  }
+  std::string line;
+  if (!std::getline(in, line)) {
+    set_error("empty matrix file");
+    return SUP_EIO;
+  }
+  std::istringstream ban(line);
+  std::string tag, object, format, field, symmetry;
+  ban >> tag >> object >> format >> field >> symmetry;
+  auto lower = [](std::string v) {
+    for (auto& ch : v) ch = (char)std::tolower((unsigned char)ch);
+    return v;
+  };
+  object = lower(object), format = lower(format), field = lower(field), symmetry = lower(symmetry);
+  if (tag != "%%MatrixMarket") {
+    set_error("Could not process Matrix Market Banner");
+    return SUP_EIO;
+  }
+  if (object != "matrix") {
+    set_error("SUPerman only supports matrices");
+    return SUP_EIO;
+  }
+  if (format != "coordinate") {
+    set_error("SUPerman only supports mtx (coordinate) format");
+    return SUP_EIO;
+  }
+  if (field == "complex" || (field != "real" && field != "integer" && field != "pattern")) {
+    set_error("unsupported MatrixMarket field '" + field + "' (real, integer or pattern)");
+    return SUP_EIO;
+  }
+  const bool sym = symmetry == "symmetric" || symmetry == "skew-symmetric";
+  if (!sym && symmetry != "general") {
+    set_error("unsupported MatrixMarket symmetry '" + symmetry + "'");
+    return SUP_EIO;
+  }
+  const bool pattern = field == "pattern";
+  while (in.peek() == '%') std::getline(in, line);  // read_matrix.hpp:23
+  long M = 0, N = 0, nz = 0;
+  if (!(in >> M >> N >> nz)) {
+    set_error("Matrix size cannot be read");
+    return SUP_EIO;
+  }
+  if (M != N) {
+    set_error("SUPerman only works with nxn matrices");
+    return SUP_EIO;
+  }
+  if (M < 1 || M > SUP_MAX_READ_N || nz < 0) {
+    set_error("matrix order " + std::to_string(M) + " outside [1, " + std::to_string(SUP_MAX_READ_N) + "]");
+    return SUP_EIO;
+  }
+  const int nov = (int)M;
+  const sup_dtype dt = (field == "real" && !binary) ? SUP_FLOAT64 : SUP_INT32;  // main.cpp:1589,1821
+  void* m = std::calloc((size_t)nov * nov, esize(dt));
+  if (!m) {
+    set_error("out of host memory");
+    return SUP_ENOMEM;
+  }
+  auto put = [&](int i, int j, double v) {
+    if (dt == SUP_INT32) at<int32_t>(m, nov, i, j) = (int32_t)v;
+    else at<double>(m, nov, i, j) = v;
+  };
+  for (long e = 0; e < nz; ++e) {
+    long x, y;
+    double v = 1.0;
+    bool ok = (bool)(in >> x >> y);
+    if (ok && !pattern) ok = (bool)(in >> v);
+    if (!ok) {
+      std::free(m);
+      set_error("MatrixMarket file ends after " + std::to_string(e) + " of " + std::to_string(nz) + " entries");
+      return SUP_EIO;
+    }
+    if (x < 1 || x > nov || y < 1 || y > nov) {
+      std::free(m);
+      set_error("entry (" + std::to_string(x) + "," + std::to_string(y) + ") outside the " + std::to_string(nov) +
+                "x" + std::to_string(nov) + " matrix (1-based)");
+      return SUP_EIO;
+    }
+    if (pattern || binary) v = 1.0;
+    put((int)x - 1, (int)y - 1, v);
+    if (sym && x != y) put((int)y - 1, (int)x - 1, v);
+  }
+  *mat = m;
+  *t = dt;
+  *n = nov;
+  if (nnz_lines) *nnz_lines = (int)nz;
+  return SUP_OK;
+}
+
 // util.h:343-358 ReadMatrix + main.cu:494-498 header parse.
 int sup_read_matrix(const char* path, int binary, void** mat, sup_dtype* t, int* n, int* nnz_header) {
   if (!path || !mat || !t || !n) {
@@ -52,6 +154,10 @@ int sup_read_matrix(const char* path, int binary, void** mat, sup_dtype* t, int*
   if (!std::getline(in, line)) {
     set_error("empty matrix file");
     return SUP_EIO;
+  }
+  if (line.rfind("%%MatrixMarket", 0) == 0) {
+    in.close();
+    return sup_read_mtx(path, binary, mat, t, n, nnz_header);
   }
   {
     std::istringstream iss(line);

@@ -4,8 +4,10 @@
 // full-precision "Permanent: %.17e" line (the legacy line has ~6 digits).
 //
 // Extensions (v2 semantics, revised_perman/main.cpp:1298-1476): -l <dev>
-// first device, -k <reps> repetitions; -R combine multi-GPU partials with RCCL;
-// -v reference-style per-kernel / per-chunk timing lines.
+// first device, -k <reps> repetitions, -o compression (d1/d2 singletons, then
+// the d1/d2/d34 expansion while n > 30), -u <t> scaling; MatrixMarket input
+// (detected by its banner, read as main.cpp:1515-1615).  Own additions: -R
+// combine multi-GPU partials with RCCL; -v per-kernel / per-chunk timing.
 #include <getopt.h>
 
 #include <chrono>
@@ -22,8 +24,9 @@ namespace {
 
 struct Cli {
   bool generic = true, dense = true, approximation = false, gpu = false, cpu = false, grid_graph = false;
-  bool rccl = false, verbose = false;
+  bool rccl = false, verbose = false, compression = false;
   int gpu_num = 2, threads = 16, perman_algo = 1, preprocessing = 0, device = 0, reps = 1;
+  double scaling = -1.0;
   std::string filename;
 };
 
@@ -42,7 +45,7 @@ void report(const std::string& name, double perm, double sec) {
 
 int main(int argc, char** argv) {
   Cli c;
-  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rv";
+  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rvou:";
   const struct option long_options[] = {{"binary", 0, NULL, 'b'},       {"sparse", 0, NULL, 's'},
                                         {"preprocessing", 1, NULL, 'r'}, {"threads", 1, NULL, 't'},
                                         {"file", 1, NULL, 'f'},          {"gpu", 0, NULL, 'g'},
@@ -53,6 +56,7 @@ int main(int argc, char** argv) {
                                         {"gridm", 1, NULL, 'm'},         {"gridn", 1, NULL, 'n'},
                                         {"gpu-id", 1, NULL, 'l'},        {"reps", 1, NULL, 'k'},
                                         {"rccl", 0, NULL, 'R'},          {"verbose", 0, NULL, 'v'},
+                                        {"compression", 0, NULL, 'o'},   {"scaling", 1, NULL, 'u'},
                                         {NULL, 0, NULL, 0}};
   int opt;
   auto need_arg = [&](char o) -> bool {
@@ -82,6 +86,11 @@ int main(int argc, char** argv) {
       case 'k': if (!need_arg('k')) return 1; c.reps = std::max(1, std::atoi(optarg)); break;
       case 'R': c.rccl = true; break;
       case 'v': c.verbose = true; break;
+      case 'o': c.compression = true; break;  // revised_perman/main.cpp:1462
+      case 'u':                                // main.cpp:1465 (atoi)
+        if (!need_arg('u')) return 1;
+        c.scaling = (double)std::atoi(optarg);
+        break;
       case '?': return 1;
       default: std::abort();
     }
@@ -104,11 +113,18 @@ int main(int argc, char** argv) {
   int n = 0, nnz = 0;
   if (sup_read_matrix(c.filename.c_str(), c.generic ? 0 : 1, &mat, &t, &n, &nnz) != SUP_OK)
     return fail("reading matrix");
-  // main.cu:512-518 / 544-550 / 577-583: preprocessing rewrites mat.
+  // main.cu:512-518 / 544-550 / 577-583: preprocessing rewrites mat (with
+  // -o / -u it is applied to every leaf of the reductions instead).
+  const bool reduce = c.compression || c.scaling > 0.0;
+  sup_reduce_opts ro;
+  sup_reduce_opts_init(&ro);
+  ro.compress = c.compression ? 1 : 0;
+  ro.scale_threshold = c.scaling > 0.0 ? c.scaling : 0.0;
+  ro.preprocessing = c.preprocessing;
   std::vector<int> rp(n), cp(n);
-  if (c.preprocessing == 1) {
+  if (!reduce && c.preprocessing == 1) {
     if (sup_sort_order(mat, t, n, cp.data()) != SUP_OK) return fail("SortOrder");
-  } else if (c.preprocessing == 2) {
+  } else if (!reduce && c.preprocessing == 2) {
     if (sup_skip_order(mat, t, n, rp.data(), cp.data()) != SUP_OK) return fail("SkipOrder");
   }
 
@@ -200,8 +216,9 @@ int main(int argc, char** argv) {
     double perm = 0.0;
     sup_stats st;
     auto t0 = std::chrono::steady_clock::now();
-    int rc = on_gpu ? sup_perman(mat, t, n, kern, sched, &o, &perm, &st)
-                    : sup_perman_cpu(mat, t, n, kern, c.threads, &perm, &st);
+    int rc = reduce   ? sup_perman_reduced(mat, t, n, kern, sched, &o, on_gpu ? 0 : 1, &ro, &perm, &st)
+             : on_gpu ? sup_perman(mat, t, n, kern, sched, &o, &perm, &st)
+                      : sup_perman_cpu(mat, t, n, kern, c.threads, &perm, &st);
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (rc != SUP_OK) {
       sup_free(mat);
@@ -209,9 +226,9 @@ int main(int argc, char** argv) {
     }
     report(name, perm, sec);
     if (c.verbose)
-      std::printf("Stats: kernel_ms %.3f gray_steps %llu visited %llu devices %d lanes %d walk %d grid %d\n",
+      std::printf("Stats: kernel_ms %.3f gray_steps %llu visited %llu devices %d lanes %d walk %d grid %d leaves %d\n",
                   st.kernel_ms, (unsigned long long)st.gray_steps, (unsigned long long)st.visited_steps,
-                  st.devices_used, st.lane_bits, st.walk_bits, st.grid);
+                  st.devices_used, st.lane_bits, st.walk_bits, st.grid, st.leaves);
   }
   sup_free(mat);
   return 0;

@@ -29,6 +29,18 @@ __device__ __forceinline__ uint32_t next_toggle(uint32_t t, uint32_t k) {
   return c;
 }
 
+// x[rows of blocks < nb] += col (jump path: adds only, products refreshed once)
+template <int N, int B>
+__device__ __forceinline__ void add_nest(double (&x)[N], cdbl* col, int nb) {
+  if constexpr (B < Blocks<N>::NB) {
+    if (nb > B) {
+#pragma unroll
+      for (int j = 8 * B; j < 8 * B + 8 && j < N; ++j) x[j] += col[j];
+      add_nest<N, B + 1>(x, col, nb);
+    }
+  }
+}
+
 template <int N>
 __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
   constexpr int NP = pad8(N);
@@ -84,15 +96,21 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
           target = tr > target ? tr : target;
         }
         if (target == t + 1 || target >= T) return target;
-        // Gray move t -> target: flip the differing walk bits in ascending order
+        // Gray move t -> target: add the differing walk columns in ascending
+        // bit order (each to its nblk leading blocks), then refresh all suffix
+        // products once.  Bit-identical to one sparse_step per bit: block b's
+        // x is final after the last bit with nblk > b, and that step formed
+        // U[b] from it and the final U[b+1] — the same expression suffix_all
+        // evaluates on the final x.
         const uint32_t gn = target ^ (target >> 1);
         uint32_t diff = (t ^ (t >> 1)) ^ gn;
         do {
           const uint32_t k = (uint32_t)__builtin_ctz(diff);
           diff &= diff - 1;
           const uint32_t neg = ((gn >> k) & 1u) ^ 1u;
-          sparse_step<N>(x, U, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nb_of(p, k));
+          add_nest<N, 0>(x, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nb_of(p, k));
         } while (diff);
+        suffix_all<N>(x, U);
         return target | 0x80000000u;  // flag: X already moved
       };
       for (;;) {

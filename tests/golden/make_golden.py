@@ -11,9 +11,17 @@ into oracle/_ref/ref_v2):
   skip     parallel_skip_perman64_w_balanced       cpu_algos.hpp:1035
   order    the reference's SortOrder / SkipOrder rewrite of the matrix (util.h:813, 964)
 
-Inputs: (a) copies of reference corpus files (tests/fixtures/*, data only) and
-(b) small synthetic matrices in the same v1 format, generated here with a
-fixed seed (tests/fixtures/synth/*).
+  read     the reference's MatrixMarket reader (mmio.c + read_matrix.hpp) — stored
+           as sha256 of the fp64 matrix bytes
+  reduce   the -o / -u driver (main.cpp:993-1259, restated in the harness) over the
+           reference's own d1compress / d2compress / d34compress / scalesk
+           (util.h), leaves by parallel_perman64<double,double>
+  leaves   the same reductions' leaf matrices — stored as count + sha256
+
+Inputs: (a) copies of reference corpus files (tests/fixtures/*, data only,
+including the MatrixMarket files under tests/fixtures/mtx/) and (b) small
+synthetic matrices in the same v1 format, generated here with a fixed seed
+(tests/fixtures/synth/*).
 
 usage: python tests/golden/make_golden.py [--quick]
 """
@@ -88,6 +96,68 @@ def ref(path: str, algo: str, threads: int = 8, binary: int = 0, prep: int = 0) 
     return r.stdout.strip()
 
 
+MTX_DIRS = ["revised_perman/matrices", "revised_perman/elektrik_matrices/known_perman"]
+# (file, min_n, scale threshold or -1): reductions whose leaves / result are pinned
+MTX_REDUCE = [("Tina_DisCog_p.mtx", 30, -1), ("Trefethen_20_s.mtx", 30, -1), ("can_24_ps.mtx", 20, -1),
+              ("can_24_ps.mtx", 20, 4), ("ibm32_p.mtx", 30, -1), ("ibm32_p.mtx", 20, -1), ("ibm32_p.mtx", 20, 4),
+              ("mycielskian5_ps.mtx", 20, -1), ("mycielskian5_ps.mtx", 20, 4), ("chesapeake.mtx", 20, -1),
+              ("chesapeake.mtx", 30, -1), ("will57.mtx", 30, -1), ("dwt_59.mtx", 30, -1)]
+MTX_PERM_REDUCE = [("Tina_DisCog_p.mtx", 30, -1), ("Trefethen_20_s.mtx", 30, -1), ("can_24_ps.mtx", 20, -1),
+                   ("can_24_ps.mtx", 20, 4), ("ibm32_p.mtx", 20, -1), ("ibm32_p.mtx", 20, 4),
+                   ("mycielskian5_ps.mtx", 20, -1), ("mycielskian5_ps.mtx", 20, 4), ("chesapeake.mtx", 20, -1)]
+
+
+def leaves_digest(text: str) -> dict:
+    """count + sha256 of the fp64 bytes of every leaf (harness 'leaves' output)."""
+    import hashlib
+    lines = text.strip().splitlines()
+    h, sizes, i = hashlib.sha256(), [], 0
+    while i < len(lines) and lines[i].startswith("leaf"):
+        k = int(lines[i].split()[1])
+        m = np.array([[float(x) for x in ln.split()] for ln in lines[i + 1:i + 1 + k]], dtype=np.float64)
+        h.update(np.ascontiguousarray(m.reshape(k, k)).tobytes())
+        sizes.append(k)
+        i += 1 + k
+    return {"count": len(sizes), "sha256": h.hexdigest(), "max_n": max(sizes) if sizes else 0}
+
+
+def mtx_goldens(gold: dict, put) -> None:
+    import glob
+    import hashlib
+    dst = os.path.join(FIX, "mtx")
+    os.makedirs(dst, exist_ok=True)
+    for d in MTX_DIRS:
+        for f in sorted(glob.glob(os.path.join(REF, d, "*.mtx"))):
+            if not os.path.exists(os.path.join(dst, os.path.basename(f))):
+                shutil.copy(f, dst)
+    for f in sorted(glob.glob(os.path.join(dst, "*.mtx"))):
+        name = "mtx/" + os.path.basename(f)
+        for b in (0, 1):
+            key = f"{name}|read|b{b}|sha256"
+            if key not in gold:
+                txt = ref(f, "read", 1, b)
+                m = np.array([[float(x) for x in ln.split()] for ln in txt.splitlines()], dtype=np.float64)
+                put(key, hashlib.sha256(np.ascontiguousarray(m).tobytes()).hexdigest())
+                put(f"{name}|read|b{b}|n", int(m.shape[0]))
+        n = int([ln for ln in open(f) if not ln.startswith("%")][0].split()[0])
+        key = f"{name}|dense|r0|b0|t8"
+        if n <= 30 and key not in gold:
+            put(key, float(ref(f, "dense", 8).split()[0]))
+    for fn, min_n, thr in MTX_REDUCE:
+        key = f"mtx/{fn}|leaves|n{min_n}|u{thr}"
+        if key not in gold:
+            r = subprocess.run([REF_V2, os.path.join(dst, fn), "leaves", "1", "0", "0", str(min_n), str(thr)],
+                               capture_output=True, text=True, check=True)
+            put(key, leaves_digest(r.stdout))
+    for fn, min_n, thr in MTX_PERM_REDUCE:
+        key = f"mtx/{fn}|reduce|n{min_n}|u{thr}|t8"
+        if key not in gold:
+            r = subprocess.run([REF_V2, os.path.join(dst, fn), "reduce", "8", "0", "0", str(min_n), str(thr)],
+                               capture_output=True, text=True, check=True)
+            put(key, float(r.stdout.split()[0]))
+            print(key, r.stdout.strip(), flush=True)
+
+
 def main() -> None:
     quick = "--quick" in sys.argv
     if not os.path.exists(REF_V2):
@@ -107,6 +177,7 @@ def main() -> None:
         with open(OUT, "w") as f:
             json.dump(gold, f, indent=1, sort_keys=True)
 
+    mtx_goldens(gold, put)
     names = synth()
     for name in names:
         p = os.path.join(FIX, name)

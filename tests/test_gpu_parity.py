@@ -261,3 +261,46 @@ def test_cli_gpu(sup, orc):
     assert r.returncode == 0 and "skipper" in r.stdout
     r = subprocess.run([exe, "-f", f, "-g", "-p6", "-d1", "-v"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ChunkID" in r.stdout
+
+
+# (pores_1_r.mtx is left out: entries of both signs up to 2.5e7 cancel so
+# badly in fp64 Ryser that neither the reference nor this engine keeps a
+# correct digit — 9.9e139 vs 5.3e138)
+MTX_DIRECT = ["Tina_DisCog_p.mtx", "Trefethen_20_s.mtx", "can_24_ps.mtx", "mycielskian5_ps.mtx", "ex5_rs.mtx",
+              "GD02_a_p.mtx", "Ragusa16.mtx", "Ragusa18.mtx"]
+
+
+@pytest.mark.parametrize("name", MTX_DIRECT)
+def test_mtx_direct_vs_reference(sup, golden, name):
+    # MatrixMarket inputs (revised_perman/matrices) on the dense GPU path vs the
+    # reference CPU (parallel_perman64<double>) on the reference reader's matrix
+    a, _, _ = sup.read_matrix(fixture_path("mtx/" + name))
+    want = golden[f"mtx/{name}|dense|r0|b0|t8"]
+    got = sup.perman(a)
+    if want == 0.0:
+        assert abs(got) <= 1e-6 * max(1.0, float(np.prod(np.abs(a).sum(1))) ** 0.5)
+    else:
+        assert rel(got, want) < 1e-8, (name, got, want)
+
+
+@pytest.mark.parametrize("algo,sparse,prep", [(4, False, 0), (4, True, 1), (7, True, 2), (6, False, 0)])
+def test_reduced_gpu_vs_reference(sup, golden, algo, sparse, prep):
+    # -o / -u with every leaf on the GPU vs the reference's reductions + CPU
+    for name, min_n, thr in [("can_24_ps.mtx", 20, -1), ("can_24_ps.mtx", 20, 4), ("ibm32_p.mtx", 20, -1),
+                             ("ibm32_p.mtx", 20, 4), ("mycielskian5_ps.mtx", 20, -1), ("Tina_DisCog_p.mtx", 30, -1)]:
+        a, _, _ = sup.read_matrix(fixture_path("mtx/" + name))
+        got, st = sup.perman_reduced(a, algo=algo, sparse=sparse, preprocessing=prep, compress=True,
+                                     scale=thr if thr > 0 else None, min_n=min_n, return_stats=True)
+        assert rel(got, golden[f"mtx/{name}|reduce|n{min_n}|u{thr}|t8"]) < 1e-10, (name, algo, prep)
+        assert st["leaves"] == golden[f"mtx/{name}|leaves|n{min_n}|u{thr}"]["count"]
+
+
+def test_chesapeake(sup):
+    # n = 39 pattern matrix (elektrik_matrices/known_perman): directly on the
+    # GPU; the reference's older SpaRyser runs report 1.31734973e13 (their
+    # float-X results spread ~1e-5: sparyser/RealResults/chesapeake.mtx.a3s1.out)
+    a, _, _ = sup.read_matrix(fixture_path("mtx/chesapeake.mtx"))
+    r = sup.perman(a)
+    assert r == pytest.approx(13173497329080.0, rel=2e-5)
+    assert abs(r - round(r)) < 1e-3 * abs(r) ** 0.5  # an integer, up to fp64 rounding of the sum
+    assert rel(sup.perman(a, algo=4, sparse=True), r) < 1e-12
