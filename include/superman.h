@@ -267,6 +267,41 @@ int sup_decompose(const void* mat, sup_dtype t, int n, const sup_reduce_opts* r,
 int sup_perman_reduced(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched sched, const sup_opts* o,
                        int on_cpu, const sup_reduce_opts* r, double* out, sup_stats* st);
 
+/* ------------------------------------------------------------------------ *
+ * Randomized estimators (reference -a, main.cu:77-103,
+ * 156-183, 193-243).  Both estimate the permanent of the 0/1 nonzero pattern,
+ * as the reference's do.  method 0: Rasmussen (kernel_rasmussen,
+ * gpu_approximation_dense.cu:155-229; CPU algo.h:270-366); method 1:
+ * scaling-guided importance sampling (kernel_approximation,
+ * gpu_approximation_dense.cu:231-371; CPU algo.h:472-560) with Sinkhorn
+ * passes every scale_intervals steps (-y, default 4), scale_times passes each
+ * (-z, default 5).  `samples` (-x, default 100000) is rounded up to a multiple
+ * of 64.  Randomness is Philox4x32-10 keyed by `seed`, counter (sample, step):
+ * the estimate is a function of (matrix, method, samples, seed) only — the same
+ * on the CPU (on_cpu = 1, o->threads threads), on one GPU or on o->gpu_num
+ * GPUs (+ o->cpu_worker), which is how the reference's _multigpucpu_chunks
+ * forms (gpu_approximation_dense.cu:411-525, 573-700) map here.  n <= 1024.
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  double   mean;           /* the estimate                                      */
+  double   std_error;      /* sample standard deviation / sqrt(samples)         */
+  double   zero_fraction;  /* samples that hit a dead end (estimate 0)          */
+  uint64_t samples;        /* samples drawn (multiple of 64)                    */
+  double   kernel_ms;      /* device time (max over devices)                    */
+  double   wall_ms;
+  int      devices;
+  int      reserved_;
+  int64_t  cpu_blocks;     /* 64-sample blocks computed on host threads         */
+} sup_approx_result;
+
+int sup_approx(const void* mat, sup_dtype t, int n, int method, uint64_t samples, int scale_intervals,
+               int scale_times, uint64_t seed, const sup_opts* o, int on_cpu, sup_approx_result* res);
+
+/* Grid graph of the -i mode (util.h:403-520 gridGraph2compressed): the
+ * bipartite adjacency (nov = m*n/2, one of m, n even) whose permanent is the
+ * number of domino tilings of the m x n board; *mat from malloc (sup_free). */
+int sup_grid_graph(int m, int n, int** mat, int* nov);
+
 #ifdef __cplusplus
 }
 #endif

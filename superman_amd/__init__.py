@@ -16,11 +16,11 @@ import numpy as np
 
 from . import _lib
 from ._lib import (KERNEL_DENSE, KERNEL_SKIPPER, KERNEL_SPARYSER, LEAF_FN, SCHED_CHUNKS, SCHED_SINGLE,
-                   SCHED_STATIC, SupError, SupOpts, SupReduceOpts, SupStats)
+                   SCHED_STATIC, SupApproxResult, SupError, SupOpts, SupReduceOpts, SupStats)
 
 __all__ = [
     "perman", "perman_cpu", "partial", "perman_shard", "plan_info", "read_matrix", "read_mtx", "sort_order",
-    "skip_order", "compress", "decompose", "perman_reduced",
+    "skip_order", "compress", "decompose", "perman_reduced", "approx", "grid_graph", "ALGOS_APPROX",
     "nw_start", "device_count", "layout", "SupError", "ALGOS_DENSE", "ALGOS_SPARSE",
     "gpu_perman64_xshared_coalescing_mshared",
     "gpu_perman64_xshared_coalescing_mshared_multigpu",
@@ -347,3 +347,44 @@ def read_mtx(path: str, binary: bool = False) -> tuple[np.ndarray, str, int]:
     finally:
         lib.sup_free(p)
     return m, _TYPE_NAME[t.value], nnz.value
+
+
+# main.cu:77-103 / 156-183 (GPU) and 193-243 (CPU) approximation dispatch:
+# algo id -> (method, multi-device form)
+ALGOS_APPROX = {1: ("rasmussen", False), 2: ("approximation", False), 3: ("rasmussen", True),
+                4: ("approximation", True)}
+
+
+def approx(mat, algo: int = 1, samples: int = 100000, scale_intervals: int = 4, scale_times: int = 5,
+           seed: int = 1, gpu_num: int = 1, cpu: bool = False, cpu_worker: bool = False, threads: int = 16,
+           device_id: int = 0, return_stats: bool = False):
+    """Randomized estimate of the permanent of the 0/1 pattern of `mat` (the
+    reference's -a mode): algo 1/3 Rasmussen, 2/4 scaling-guided sampling;
+    3/4 are the multi-device forms (gpu_num devices, + a CPU worker with
+    cpu_worker).  cpu=True runs on host threads (the CLI's -c -a).  The
+    estimate depends only on (mat, algo's method, samples, seed)."""
+    if algo not in ALGOS_APPROX:
+        raise SupError(-7, "approx", f"unknown approximation id {algo}")
+    method, multi = ALGOS_APPROX[algo]
+    a, dt, n = _mat(mat, 1024)
+    lib = _lib.load()
+    o = _opts(gpu_num if multi else 1, device_id, threads)
+    o.cpu_worker = int(bool(cpu_worker and multi))
+    r = SupApproxResult()
+    _lib.check(lib.sup_approx(a.ctypes.data, dt, n, 0 if method == "rasmussen" else 1, int(samples),
+                              int(scale_intervals), int(scale_times), int(seed), C.byref(o), int(bool(cpu)),
+                              C.byref(r)), "approx")
+    return (r.mean, r.as_dict()) if return_stats else r.mean
+
+
+def grid_graph(m: int, n: int) -> np.ndarray:
+    """Bipartite adjacency of the m x n grid graph (util.h:403-520); its
+    permanent is the number of domino tilings of the board."""
+    lib = _lib.load()
+    p, nov = C.POINTER(C.c_int)(), C.c_int()
+    _lib.check(lib.sup_grid_graph(int(m), int(n), C.byref(p), C.byref(nov)), "grid_graph")
+    try:
+        a = np.ctypeslib.as_array(p, shape=(nov.value * nov.value,)).reshape(nov.value, nov.value).copy()
+    finally:
+        lib.sup_free(C.cast(p, C.c_void_p))
+    return a.astype(np.int32)

@@ -44,7 +44,7 @@ EXPORTS = [
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper",
     "sup_read_matrix", "sup_free", "sup_count_nnz", "sup_compress",
     "sup_sort_order", "sup_skip_order", "sup_read_mtx",
-    "sup_reduce_opts_init", "sup_decompose", "sup_perman_reduced",
+    "sup_reduce_opts_init", "sup_decompose", "sup_perman_reduced", "sup_approx", "sup_grid_graph",
 ]
 
 
@@ -62,6 +62,17 @@ class SupReduceOpts(C.Structure):
         ("compress", C.c_int), ("scale_threshold", C.c_double), ("min_n", C.c_int),
         ("max_deg", C.c_int), ("preprocessing", C.c_int),
     ]
+
+
+class SupApproxResult(C.Structure):
+    _fields_ = [
+        ("mean", C.c_double), ("std_error", C.c_double), ("zero_fraction", C.c_double),
+        ("samples", C.c_uint64), ("kernel_ms", C.c_double), ("wall_ms", C.c_double),
+        ("devices", C.c_int), ("reserved_", C.c_int), ("cpu_blocks", C.c_int64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved_"}
 
 
 # int (*sup_leaf_fn)(const double* a, int n, void* user, double* out_perm)
@@ -140,6 +151,9 @@ def _declare(lib: C.CDLL) -> None:
     lib.sup_compress.argtypes = [P, I, I, P, P, P, P, P, P]
     lib.sup_sort_order.argtypes = [P, I, I, P]
     lib.sup_skip_order.argtypes = [P, I, I, P, P]
+    lib.sup_approx.argtypes = [P, I, I, I, C.c_uint64, I, I, C.c_uint64, C.POINTER(SupOpts), I,
+                               C.POINTER(SupApproxResult)]
+    lib.sup_grid_graph.argtypes = [I, I, C.POINTER(C.POINTER(C.c_int)), C.POINTER(I)]
     lib.sup_read_mtx.argtypes = [C.c_char_p, I, C.POINTER(P), C.POINTER(I), C.POINTER(I), C.POINTER(I)]
     lib.sup_reduce_opts_init.argtypes = [C.POINTER(SupReduceOpts)]
     lib.sup_reduce_opts_init.restype = None

@@ -7,7 +7,9 @@
 // first device, -k <reps> repetitions, -o compression (d1/d2 singletons, then
 // the d1/d2/d34 expansion while n > 30), -u <t> scaling; MatrixMarket input
 // (detected by its banner, read as main.cpp:1515-1615).  Own additions: -R
-// combine multi-GPU partials with RCCL; -v per-kernel / per-chunk timing.
+// combine multi-GPU partials with RCCL; -v per-kernel / per-chunk timing;
+// --seed (-S) the estimators' Philox seed (-a / -i; the reference seeds with
+// time(0), so its estimates are not reproducible).
 #include <getopt.h>
 
 #include <chrono>
@@ -27,6 +29,9 @@ struct Cli {
   bool rccl = false, verbose = false, compression = false;
   int gpu_num = 2, threads = 16, perman_algo = 1, preprocessing = 0, device = 0, reps = 1;
   double scaling = -1.0;
+  long number_of_times = 100000;  // main.cu:338-344 defaults
+  int scale_intervals = 4, scale_times = 5, gridm = 36, gridn = 36;
+  unsigned long long seed = 1;
   std::string filename;
 };
 
@@ -41,11 +46,77 @@ void report(const std::string& name, double perm, double sec) {
   std::fflush(stdout);
 }
 
+// main.cu:77-103, 156-183 (GPU) and 193-243 (CPU) approximation dispatch;
+// main.cu:250-320 RunPermanForGridGraphs (sparse names, -i -m -n).
+int run_approx(const Cli& c) {
+  void* mat = nullptr;
+  sup_dtype t = SUP_INT32;
+  int n = 0, nnz = 0;
+  if (c.grid_graph) {
+    int* g = nullptr;
+    if (sup_grid_graph(c.gridm, c.gridn, &g, &n) != SUP_OK) return fail("grid graph");
+    mat = g;
+  } else if (sup_read_matrix(c.filename.c_str(), c.generic ? 0 : 1, &mat, &t, &n, &nnz) != SUP_OK) {
+    return fail("reading matrix");
+  }
+  const bool sparse = c.grid_graph || !c.dense;
+  const int a = c.perman_algo;
+  std::string name;
+  int method = 0;
+  bool multi = false;
+  if (c.gpu) {
+    static const char* dn[] = {"", "gpu_perman64_rasmussen", "gpu_perman64_approximation",
+                               "gpu_perman64_rasmussen_multigpucpu_chunks",
+                               "gpu_perman64_approximation_multigpucpu_chunks"};
+    if (a < 1 || a > 4) {
+      std::cout << "Unknown Algorithm ID" << std::endl;
+      sup_free(mat);
+      return 0;
+    }
+    name = std::string(dn[a]) + (sparse ? "_sparse" : "");
+    method = (a == 2 || a == 4) ? 1 : 0;
+    multi = a >= 3;
+  } else {
+    if (a != 1 && a != 2) {
+      std::cout << "Unknown Algorithm ID" << std::endl;
+      sup_free(mat);
+      return 0;
+    }
+    name = std::string(a == 1 ? "rasmussen" : "approximation_perman64") + (sparse ? "_sparse" : "");
+    method = a - 1;
+  }
+  sup_opts o;
+  sup_opts_init(&o);
+  o.gpu_num = multi ? c.gpu_num : 1;
+  o.device_id = c.device;
+  o.threads = c.threads;
+  o.cpu_worker = (multi && c.cpu) ? 1 : 0;
+  for (int r = 0; r < c.reps; ++r) {
+    sup_approx_result res;
+    auto t0 = std::chrono::steady_clock::now();
+    const int rc = sup_approx(mat, t, n, method, (uint64_t)std::max(1L, c.number_of_times), c.scale_intervals,
+                              c.scale_times, c.seed + (unsigned long long)r, &o, c.gpu ? 0 : 1, &res);
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (rc != SUP_OK) {
+      sup_free(mat);
+      return fail(name.c_str());
+    }
+    const char* tag = c.grid_graph ? "Try" : "Result";
+    std::printf("Result: %s %2lf in %lf\n", name.c_str(), res.mean, sec);
+    std::cout << tag << ": " << name << " " << res.mean << " in " << sec << std::endl;
+    std::printf("Permanent: %.17e\nStdError: %.6e samples %llu zeros %.4f\n", res.mean, res.std_error,
+                (unsigned long long)res.samples, res.zero_fraction);
+    std::fflush(stdout);
+  }
+  sup_free(mat);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   Cli c;
-  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rvou:";
+  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rvou:S:";
   const struct option long_options[] = {{"binary", 0, NULL, 'b'},       {"sparse", 0, NULL, 's'},
                                         {"preprocessing", 1, NULL, 'r'}, {"threads", 1, NULL, 't'},
                                         {"file", 1, NULL, 'f'},          {"gpu", 0, NULL, 'g'},
@@ -57,6 +128,7 @@ int main(int argc, char** argv) {
                                         {"gpu-id", 1, NULL, 'l'},        {"reps", 1, NULL, 'k'},
                                         {"rccl", 0, NULL, 'R'},          {"verbose", 0, NULL, 'v'},
                                         {"compression", 0, NULL, 'o'},   {"scaling", 1, NULL, 'u'},
+                                        {"seed", 1, NULL, 'S'},
                                         {NULL, 0, NULL, 0}};
   int opt;
   auto need_arg = [&](char o) -> bool {
@@ -78,9 +150,12 @@ int main(int argc, char** argv) {
       case 'd': if (!need_arg('d')) return 1; c.gpu_num = std::atoi(optarg); break;
       case 'c': c.cpu = true; break;
       case 'p': if (!need_arg('p')) return 1; c.perman_algo = std::atoi(optarg); break;
-      case 'x': case 'y': case 'z': case 'm': case 'n':
-        if (!need_arg((char)opt)) return 1;  // approximation / grid parameters: accepted, unused
-        break;
+      case 'x': if (!need_arg('x')) return 1; c.number_of_times = std::atol(optarg); break;
+      case 'y': if (!need_arg('y')) return 1; c.scale_intervals = std::atoi(optarg); break;
+      case 'z': if (!need_arg('z')) return 1; c.scale_times = std::atoi(optarg); break;
+      case 'm': if (!need_arg('m')) return 1; c.gridm = std::atoi(optarg); break;
+      case 'n': if (!need_arg('n')) return 1; c.gridn = std::atoi(optarg); break;
+      case 'S': if (!need_arg('S')) return 1; c.seed = std::strtoull(optarg, nullptr, 10); break;
       case 'i': c.grid_graph = true; break;
       case 'l': if (!need_arg('l')) return 1; c.device = std::atoi(optarg); break;
       case 'k': if (!need_arg('k')) return 1; c.reps = std::max(1, std::atoi(optarg)); break;
@@ -101,12 +176,7 @@ int main(int argc, char** argv) {
   }
   for (int i = optind; i < argc; ++i) std::printf("Non-option argument %s\n", argv[i]);
   if (!c.cpu && !c.gpu) c.gpu = true;  // main.cu:482-484
-  if (c.grid_graph || c.approximation) {
-    std::fprintf(stderr,
-                 "perman: approximation (-a) and grid-graph (-i) modes are outside this engine's scope "
-                 "(exact Ryser / Gray-code path only; see DESIGN.md)\n");
-    return 2;
-  }
+  if (c.grid_graph || c.approximation) return run_approx(c);
 
   void* mat = nullptr;
   sup_dtype t;

@@ -37,6 +37,10 @@ for step in "$@"; do
            prof_pmc pmc_sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT
            prof_pmc pmc_lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY;;
     probe) run probe 300 python3 tools/probe.py;;
+    pmc44) for k in sparse skip; do
+             run "pmc44_sq_$k" 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace -d "$OUT/pmc44_sq_$k" -o run --output-format csv -- python3 tools/run_one.py synth44_0.15_int 2 $k
+             run "pmc44_wait_$k" 300 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_WAIT_ANY --kernel-trace -d "$OUT/pmc44_wait_$k" -o run --output-format csv -- python3 tools/run_one.py synth44_0.15_int 2 $k
+           done;;
     *) run "$step" 900 bash -c "$step";;
   esac
 done
