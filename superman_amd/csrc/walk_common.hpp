@@ -187,7 +187,8 @@ __device__ __forceinline__ void for_down(F&& f) {
 // nb blocks pays ~nb uniform branches (not NB), blocks still run top-down,
 // and the control flow stays structured (x/U updated in place, no phi
 // copies).  Rows 0-15 are fetched before the first branch, rows 16-31 and
-// 32-63 inside the branch that first needs them.
+// (N <= 40, N > 48) 32-63 inside the branch that first needs them; for
+// 40 < N <= 48 each block from 4 on fetches its own rows right before use.
 template <int N, int B>
 __device__ __forceinline__ void sparse_nest(double (&x)[N], double (&U)[Blocks<N>::NB + 1], cdbl* col, int nb,
                                             double (&c)[N]) {
@@ -195,8 +196,12 @@ __device__ __forceinline__ void sparse_nest(double (&x)[N], double (&U)[Blocks<N
   if constexpr (B < NB) {
     if (nb > B) {
       if constexpr (B == 2) fetch_rows<N, 16, (N < 32 ? N : 32)>(col, c);
-      if constexpr (B == 4) fetch_rows<N, 32, N>(col, c);
+      if constexpr (B == 4 && (N <= 40 || N > 48)) fetch_rows<N, 32, N>(col, c);
       sparse_nest<N, B + 1>(x, U, col, nb, c);
+      // 40 < N <= 48: blocks 4.. fetch their own 8 rows after the deeper blocks
+      // are done, so at most rows 0-31 + one block are live in SGPRs (no spills
+      // in the walk loop; for N > 48 this form costs occupancy instead)
+      if constexpr (B >= 4 && N > 40 && N <= 48) fetch_rows<N, 8 * B, (8 * B + 8 < N ? 8 * B + 8 : N)>(col, c);
       blk_add<N, B>(x, c);
       blk_prod<N, B>(x, U);
     }

@@ -45,7 +45,11 @@ __global__ __launch_bounds__(kBlock) void walk_sparse(WalkParams p) {
       double acc = U[0];
       uint32_t t = 1;
       for (; t + 1 < T; t += 2) {
-        sparse_step<N>(x, U, opaque_c(p.cols, offL + ((t >> 1) & 1u) * NP * 8u), nb0);
+        // re-materialise nb0 in an SGPR every iteration: hoisted "nb0 > B"
+        // masks would be spilled to VGPR lanes and cost v_readlane (VALU) per step
+        int nbo = nb0;
+        asm volatile("" : "+s"(nbo));
+        sparse_step<N>(x, U, opaque_c(p.cols, offL + ((t >> 1) & 1u) * NP * 8u), nbo);
         acc -= U[0];
         const uint32_t u = t + 1;
         const uint32_t k = (uint32_t)__builtin_ctz(u);
