@@ -10,6 +10,12 @@ power-of-two-aligned shards; each rank walks its shard through the C ABI
 sums the fp64 partials — the only data-path collective.  Total work per
 step is fixed (one permanent), so scaling is "strong".
 
+The walk kernel is the segmented walk specialised for the matrix's pattern
+(superman_amd/csrc/jit.cpp; --jit 1, the default here): it is compiled once
+with hiprtc before the warmup (compile time reported as config.jit_compile_ms,
+outside the timed region, like the plan), then every timed step walks all
+2^39 Gray steps.  --jit -1 runs the ahead-of-time prefix-blocked kernel.
+
 Prints ONE JSON line on rank 0 (driver contract), including the roofline of
 the walk kernel (hipEvents on its own stream, measured inside the library)
 and a CPU baseline (oracle/ port of the reference's parallel_perman64 chunk
@@ -38,8 +44,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--matrix", default=os.path.join(ROOT, "tests", "fixtures", "double__40_0.50_0"))
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
-    ap.add_argument("--kernel", default="dense", choices=["dense", "dense_plain", "sparse", "skip"],
-                    help="dense = -p4/-p6 (engine picks plain or prefix-blocked walk); sparse/skip = -s paths")
+    ap.add_argument("--kernel", default="dense", choices=["dense", "dense_plain", "sparse", "skip", "seg"],
+                    help="dense = -p4/-p6 (engine picks the cheapest walk); sparse/skip = -s paths")
+    ap.add_argument("--jit", type=int, default=1, choices=[-1, 0, 1],
+                    help="segmented walk specialised for the pattern: 1 when cheaper, 0 auto, -1 never")
     ap.add_argument("--rehearse", action="store_true",
                     help="all ranks on device 0 over gloo: rehearse the N-rank path on a one-GPU box")
     ap.add_argument("--prep", type=int, default=0, choices=[0, 1, 2], help="-r: 1 SortOrder, 2 SkipOrder")
@@ -56,22 +64,24 @@ def shard_chunks(n: int, rank: int, world: int) -> tuple[int, int]:
     return C * rank // world, C * (rank + 1) // world
 
 
-def pmc_traffic(n: int):
-    """HBM bytes per walk launch from the committed rocprofv3 PMC summary, if any."""
+def pmc_traffic(n: int, kernel: str):
+    """HBM bytes per walk launch from the committed rocprofv3 PMC summary of
+    this kernel, if any."""
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc*.json"), recursive=True), reverse=True):
         try:
             d = json.load(open(p))
-            if d.get("n") == n and "hbm_bytes_per_launch" in d:
+            if d.get("n") == n and "hbm_bytes_per_launch" in d and kernel in d.get("kernel", ""):
                 return d["hbm_bytes_per_launch"]
         except Exception:
             pass
     return None
 
 
-def cpu_baseline(a, n: int, budget_s: float, gpu_sup):
+def cpu_baseline(a, n: int, budget_s: float, gpu_sup, kernel: str):
     """Reference algorithm (oracle port of cpu_perman64, gpu_exact_dense.cu:6-69)
     on an aligned sample [2^(n-2), 2^(n-2)+S) of the same workload, all host
-    threads; also the GPU on the same sample for the relative error."""
+    threads; also the GPU (same walk family as the bench) on the same sample
+    for the relative error."""
     import oracle
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     s0 = 1 << (n - 2)
@@ -85,7 +95,7 @@ def cpu_baseline(a, n: int, budget_s: float, gpu_sup):
     t = time.perf_counter()
     cpu = oracle.ref_dense_partial(a, s0, s0 + size, threads)
     dt = time.perf_counter() - t
-    gpu = gpu_sup.partial(a, s0, s0 + size)
+    gpu = gpu_sup.partial(a, s0, s0 + size, kernel=kernel)
     err = abs(gpu - cpu) / max(abs(cpu), 1e-300)
     return {"value": size / dt, "unit": "gray-steps/s", "cores": threads, "kind": "port",
             "sample": f"reference Gray indices [2^{n-2}, 2^{n-2}+2^{k}) of {os.path.basename(args.matrix)} "
@@ -121,9 +131,13 @@ def main():
     L, m, _ = S.layout(n)
     c0, c1 = shard_chunks(n, rank, world)
     my_steps = (c1 - c0) << (L + m)
+    # plan + (segmented walk) hiprtc compile, once, before the timed region;
+    # gpu_num = world so that --jit 0 decides as the N-rank plan would
+    prep = S.prepare(a, args.kernel, jit=args.jit, gpu_num=world)
 
     def step():
-        part, st = S.perman_shard(a, rank, world, kernel=args.kernel, device_id=dev, return_stats=True)
+        part, st = S.perman_shard(a, rank, world, kernel=args.kernel, device_id=dev, return_stats=True,
+                                  jit=args.jit)
         if world > 1:
             t = torch.tensor([part], dtype=torch.float64, device=tdev)
             dist.all_reduce(t)  # RCCL over xGMI: the single data-path collective
@@ -155,8 +169,9 @@ def main():
     k_ms = sum(kms) / len(kms)
     flops = 2.0 * n * my_steps  # n fp64 adds + n fp64 muls per Gray step
     achieved = flops / (k_ms * 1e-3) / 1e12
-    traffic = pmc_traffic(n)
-    walk = {0: "walk_dense", 1: "walk_sparse", 2: "walk_skip"}[st["walk_kind"]]
+    walk = {0: f"sup::walk_dense<{n}>", 1: f"sup::walk_sparse<{n}>", 2: f"sup::walk_skip<{n}>",
+            3: "sup_walk_seg"}[st["walk_kind"]]
+    traffic = pmc_traffic(n, walk)
     fname = os.path.basename(args.matrix).replace("__", "/")
     density = float((a != 0).sum()) / (n * n)
     rec = {
@@ -175,20 +190,29 @@ def main():
         "config": {"workload": f"{args.kernel} Ryser/Gray-code exact permanent (-p4/-p6 path), n={n} "
                                f"d={density:.2f} ({fname}), 2^{n - 1} Gray steps per step",
                    "n": n, "density": round(density, 4), "gray_steps_per_step": 1 << (n - 1),
-                   "kernel_request": args.kernel, "preprocessing": args.prep,
+                   "kernel_request": args.kernel, "preprocessing": args.prep, "jit": args.jit,
+                   "walk": {0: "dense", 1: "prefix-blocked", 2: "skipper", 3: "segmented (pattern-specialised)"}[
+                       st["walk_kind"]],
+                   "jit_compile_ms": prep["compile_ms"],
                    "parallelism": f"dp{world}: contiguous wave-chunk shards + one RCCL all-reduce"},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": f"sup::{walk}<{n}>", "kernel_ms_avg": k_ms,
+                     "kernel": walk, "kernel_ms_avg": k_ms,
                      "algorithmic_flops_per_launch": flops,
                      "flops_definition": "2n fp64 flops per Gray step (n adds + n muls, SURVEY 8(d)); the "
-                                         "prefix-blocked walk skips structural zeros, so it executes "
-                                         f"~{st['est_ops_per_step']:.1f} fp64 VALU ops per step instead of "
-                                         f"{2 * n + 1}; fp64 issue ceiling without FMA = 0.5 of peak"},
+                                         f"{walk} walk skips the operations structural zeros make redundant, "
+                                         f"so it executes ~{st['est_ops_per_step']:.1f} fp64 VALU ops per step "
+                                         f"(cost model) instead of {2 * n + 1}; fp64 issue ceiling without FMA "
+                                         "= 0.5 of peak",
+                     # executed (cost-model) fp64 VALU ops / s and their share of the
+                     # non-FMA issue rate (peak / 2): the kernel's issue efficiency
+                     "executed_fp64_ops_per_s": st["est_ops_per_step"] * my_steps / (k_ms * 1e-3),
+                     "issue_frac": st["est_ops_per_step"] * my_steps / (k_ms * 1e-3) / (FP64_PEAK_TFLOPS * 1e12 / 2)},
         "permanent": perm,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cb_rec, err = cpu_baseline(a, n, args.cpu_seconds, S)
+        cb_rec, err = cpu_baseline(a, n, args.cpu_seconds, S,
+                                   "seg" if st["walk_kind"] == 3 else args.kernel)
         rec["cpu_baseline"] = cb_rec
         rec["rel_err_vs_cpu"] = err
     else:

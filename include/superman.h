@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SUP_ABI_VERSION 1
+#define SUP_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------ */
 #define SUP_OK            0
@@ -66,7 +66,10 @@ typedef enum {
                                  its cost model says the matrix's zeros make that cheaper (same sum) */
   SUP_KERNEL_SPARYSER = 1,    /* kernel_xshared_coalescing_mshared_sparse   gpu_exact_sparse.cu:455-552 */
   SUP_KERNEL_SKIPPER = 2,     /* kernel_xshared_coalescing_mshared_skipper  gpu_exact_sparse.cu:555-670 */
-  SUP_KERNEL_DENSE_PLAIN = 3  /* always the plain dense walk (2n fp64 ops per Gray step)                */
+  SUP_KERNEL_DENSE_PLAIN = 3, /* always the plain dense walk (2n fp64 ops per Gray step)                */
+  SUP_KERNEL_SEGMENTED = 4    /* always the segmented walk specialised for the matrix pattern (n >= 10;
+                                 the GPU entry points compile it with hiprtc, sup_perman_cpu runs the
+                                 same operations on host threads)                                       */
 } sup_kernel;
 
 /* ---- multi-device scheduling policy -------------------------------------- */
@@ -89,6 +92,10 @@ typedef struct {
   int use_rccl;       /* 1: multi-device partials combined by one RCCL all-reduce (bit-     */
                       /*    identical to the host combine); 2: also with a single device    */
   int verbose;        /* print per-device / per-chunk timing lines like the reference        */
+  int jit;            /* segmented walk specialised for the matrix pattern (hiprtc, gfx950):  */
+                      /*  -1 never; 0 auto: when its cost model wins and the predicted walk  */
+                      /*  time saved exceeds ~1 s (compile ~0.4 s, then cached in memory and */
+                      /*  on disk); 1 whenever its cost model wins                           */
 } sup_opts;
 
 typedef struct {
@@ -102,9 +109,11 @@ typedef struct {
   int      grid;            /* blocks per launch (256 threads each) on each device             */
   int      chunks_done_cpu; /* queue items taken by the CPU worker                              */
   double   partials[16];    /* per-device partial sums (before the final combine)              */
-  int      walk_kind;       /* walk actually run: 0 dense, 1 prefix-blocked (SpaRyser), 2 SkipPer */
+  int      walk_kind;       /* walk actually run: 0 dense, 1 prefix-blocked (SpaRyser), 2 SkipPer,
+                               3 segmented (pattern-specialised, sup_opts.jit)                   */
   int      leaves;          /* permanents computed: 1, or the leaf count of sup_perman_reduced   */
   double   est_ops_per_step;/* cost model: fp64 VALU ops per Gray step and lane                 */
+  double   jit_ms;          /* hiprtc compile time spent by this call (0 when cached / unused)   */
 } sup_stats;
 
 /* Fill `o` with defaults. */
@@ -144,12 +153,19 @@ int sup_partial(const void* mat, sup_dtype t, int n, sup_kernel kernel,
 int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int shard, int nshards,
                      const sup_opts* o, double* out_partial, sup_stats* st);
 
-/* The plan sup_perman would run: walk kind (0 dense, 1 prefix/SpaRyser,
- * 2 SkipPer), engine-bit -> column map (n-1 entries), lane and walk bits.
+/* The plan sup_perman would run with options `o` (NULL = defaults; o->jit and
+ * o->gpu_num matter): walk kind (0 dense, 1 prefix/SpaRyser, 2 SkipPer,
+ * 3 segmented), engine-bit -> column map (n-1 entries), lane and walk bits.
  * For the test harness's bit-exact mirror of the enumeration. */
-int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, int* walk_kind, int* colmap,
-                  int* lane_bits, int* walk_bits);
+int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o, int* walk_kind,
+                  int* colmap, int* lane_bits, int* walk_bits);
 
+/* Build the plan sup_perman would run and, if it is the segmented walk,
+ * compile its kernel now (hiprtc; no device needed) into the in-memory and
+ * disk caches, so a later sup_perman does not pay the compile.  *walk_kind =
+ * the plan's walk kind; *compile_ms = hiprtc time spent (0 when cached). */
+int sup_prepare(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o, int* walk_kind,
+                double* compile_ms);
 /* Explicit CPU algorithm for the CLI's `-c` mode (reference RunAlgo cpu
  * branch, main.cu:186-238): the same wave-chunk walk on `threads` host
  * threads, bit-identical to the GPU kernels.  Never used as a fallback by the

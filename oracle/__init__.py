@@ -100,7 +100,7 @@ def engine_layout(n: int) -> tuple[int, int, int]:
     return L.value, m.value, h.value
 
 
-KINDS = {"dense": 0, "sparse": 1, "skip": 2, 0: 0, 1: 1, 2: 2}
+KINDS = {"dense": 0, "sparse": 1, "skip": 2, "seg": 3, 0: 0, 1: 1, 2: 2, 3: 3}
 
 
 def _colmap(colmap):
@@ -128,10 +128,10 @@ def engine_perman(a, kind="dense", colmap=None, threads: int = 8) -> float:
     return load().orc_engine_perman(a.ctypes.data, a.shape[0], KINDS[kind], ptr, threads)
 
 
-def engine_perman_as(sup_module, a, kernel="dense", threads: int = 8) -> float:
+def engine_perman_as(sup_module, a, kernel="dense", threads: int = 8, jit: int = 0) -> float:
     """Mirror of exactly the plan the product runs for `kernel` (walk kind and
     column map queried through the C ABI's sup_plan_info)."""
-    info = sup_module.plan_info(a, kernel)
+    info = sup_module.plan_info(a, kernel, jit=jit)
     return engine_perman(a, info["kind"], info["colmap"], threads)
 
 

@@ -386,6 +386,10 @@ typedef struct {
   unsigned long long rowmask[ORC_MAXN], umask;
   double x0[ORC_MAXN];
   double col[2 * ORC_MAXN][ORC_MAXN]; /* [2e+neg][j] */
+  /* segmented walk (kind 3): segment i = rows [seg[i], seg[i+1]), rest = [seg[nseg], n) */
+  int nseg, seg[ORC_MAXN + 1], smax[ORC_MAXN], segb;
+  char dirty[ORC_MAXN][ORC_MAXN]; /* [walk bit][segment] */
+  char dyn[ORC_MAXN];             /* rows some walk bit >= segb touches */
 } eplan;
 
 /* Layout: L = min(6, n-1); m = max(min(rest, 10), rest - 20); h = rest - m. */
@@ -449,6 +453,34 @@ static void engine_plan(const double* a, int n, int kind, const int* colmap, int
       if (a[i * n + P->colmap[L + k]] != 0.0) rm |= 1ULL << k;
     P->rowmask[j] = rm;
   }
+  if (kind == 3) {
+    /* segments: the rows each walk bit touches first (rows are in first-touch order) */
+    int R = 0;
+    char seen[ORC_MAXN] = {0};
+    P->nseg = 0;
+    P->seg[0] = 0;
+    for (int k = 0; k < m; ++k) {
+      for (int j = 0; j < n; ++j)
+        if (P->col[2 * (L + k)][j] != 0.0 && !seen[j]) seen[j] = 1, ++R;
+      if (R > P->seg[P->nseg]) P->seg[++P->nseg] = R;
+    }
+    /* walk bits < segb = min(m, 5) get their own step (touched rows); bits
+     * >= segb share one step over the union of their rows (jit.cpp) */
+    P->segb = m < 5 ? m : 5;
+    for (int k = P->segb; k < m; ++k)
+      for (int j = 0; j < n; ++j)
+        if (P->col[2 * (L + k)][j] != 0.0) P->dyn[j] = 1;
+    for (int k = 0; k < m; ++k) {
+      P->smax[k] = -1;
+      for (int j = 0; j < n; ++j)
+        if (k < P->segb ? P->col[2 * (L + k)][j] != 0.0 : P->dyn[j]) {
+          int i = 0;
+          while (P->seg[i + 1] <= j) ++i;
+          P->dirty[k][i] = 1;
+          if (i > P->smax[k]) P->smax[k] = i;
+        }
+    }
+  }
 }
 
 static double e_prod4(const double* x, int n) {
@@ -495,6 +527,30 @@ static void e_start(const eplan* P, unsigned long long ga, unsigned lane, double
   }
 }
 
+/* segmented walk: segment product = recursive halving tree (jit.cpp tree()) */
+static double e_tree(const double* x, int lo, int hi) {
+  if (hi - lo == 1) return x[lo];
+  int mid = lo + (hi - lo + 1) / 2;
+  return e_tree(x, lo, mid) * e_tree(x, mid, hi);
+}
+
+static void e_seg_chain(const eplan* P, const double* S, double R, double* U, int i) {
+  int rest = P->seg[P->nseg] < P->n;
+  U[i] = i + 1 < P->nseg ? S[i] * U[i + 1] : (rest ? S[i] * R : S[i]);
+}
+
+/* one step of walk bit k: touched rows only, then dirty segments and the chain */
+static void e_seg_step(const eplan* P, double* x, double* S, double R, double* U, int k, int neg) {
+  const double* c = P->col[2 * (P->L + k) + neg];
+  if (P->smax[k] < 0) return;
+  for (int j = 0; j < P->n; ++j)
+    if (k < P->segb ? c[j] != 0.0 : P->dyn[j]) x[j] += c[j];
+  for (int i = P->smax[k]; i >= 0; --i) {
+    if (P->dirty[k][i]) S[i] = e_tree(x, P->seg[i], P->seg[i + 1]);
+    e_seg_chain(P, S, R, U, i);
+  }
+}
+
 static double pair64(double* v) {
   for (int w = 64; w > 1; w >>= 1)
     for (int i = 0; i < w / 2; ++i) v[i] = v[2 * i] + v[2 * i + 1];
@@ -519,7 +575,20 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
       }
       double x[ORC_MAXN], U[ORC_MAXN / 8 + 2], acc;
       e_start(P, ga, l, x);
-      if (P->kind == 0) {
+      if (P->kind == 3) {
+        double S[ORC_MAXN], SU[ORC_MAXN + 1];
+        double R = P->seg[P->nseg] < n ? e_tree(x, P->seg[P->nseg], n) : 1.0;
+        for (int i = P->nseg - 1; i >= 0; --i) {
+          S[i] = e_tree(x, P->seg[i], P->seg[i + 1]);
+          e_seg_chain(P, S, R, SU, i);
+        }
+        acc = SU[0];
+        for (unsigned t = 1; t < T; ++t) {
+          unsigned k = __builtin_ctz(t), neg = (t >> (k + 1)) & 1u;
+          e_seg_step(P, x, S, R, SU, (int)k, (int)neg);
+          acc = (t & 1u) ? acc - SU[0] : acc + SU[0];
+        }
+      } else if (P->kind == 0) {
         acc = e_prod4(x, n);
         for (unsigned t = 1; t < T; ++t) {
           unsigned k = __builtin_ctz(t), neg = (t >> (k + 1)) & 1u;
@@ -605,7 +674,8 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
 }
 
 /* Engine-mirror partial over wave-chunks [c0, c1) with layout (L, m).
- * kind: 0 dense, 1 SpaRyser (prefix blocks), 2 SkipPer.  colmap: engine bit e
+ * kind: 0 dense, 1 SpaRyser (prefix blocks), 2 SkipPer, 3 segmented walk
+ * (jit.cpp's generated kernel).  colmap: engine bit e
  * -> matrix column (n-1 entries; NULL = identity). */
 double orc_engine_range(const double* a, int n, int kind, const int* colmap, int L, int m, unsigned long long c0,
                         unsigned long long c1, int threads, unsigned long long* visited) {

@@ -19,7 +19,7 @@ from ._lib import (KERNEL_DENSE, KERNEL_SKIPPER, KERNEL_SPARYSER, LEAF_FN, SCHED
                    SCHED_STATIC, SupApproxResult, SupError, SupOpts, SupReduceOpts, SupStats)
 
 __all__ = [
-    "perman", "perman_cpu", "partial", "perman_shard", "plan_info", "read_matrix", "read_mtx", "sort_order",
+    "perman", "perman_cpu", "partial", "perman_shard", "plan_info", "prepare", "read_matrix", "read_mtx", "sort_order",
     "skip_order", "compress", "decompose", "perman_reduced", "approx", "grid_graph", "ALGOS_APPROX",
     "nw_start", "device_count", "layout", "SupError", "ALGOS_DENSE", "ALGOS_SPARSE",
     "gpu_perman64_xshared_coalescing_mshared",
@@ -61,8 +61,9 @@ ALGOS_SPARSE = {
          SCHED_STATIC),
 }
 _KERNELS = {"dense": KERNEL_DENSE, "sparse": KERNEL_SPARYSER, "spa": KERNEL_SPARYSER,
-            "skipper": KERNEL_SKIPPER, "skip": KERNEL_SKIPPER, "dense_plain": _lib.KERNEL_DENSE_PLAIN}
-WALK_NAMES = {0: "dense", 1: "sparse", 2: "skip"}
+            "skipper": KERNEL_SKIPPER, "skip": KERNEL_SKIPPER, "dense_plain": _lib.KERNEL_DENSE_PLAIN,
+            "seg": _lib.KERNEL_SEGMENTED, "segmented": _lib.KERNEL_SEGMENTED}
+WALK_NAMES = {0: "dense", 1: "sparse", 2: "skip", 3: "seg"}
 
 
 def _mat(a, max_n: int = 64) -> tuple[np.ndarray, int, int]:
@@ -79,13 +80,14 @@ def _mat(a, max_n: int = 64) -> tuple[np.ndarray, int, int]:
 
 
 def _opts(gpu_num=1, device_id=0, threads=16, cpu=False, walk_log2=0, chunk_log2=0, use_rccl=False,
-          verbose=False) -> SupOpts:
+          verbose=False, jit=0) -> SupOpts:
     lib = _lib.load()
     o = SupOpts()
     lib.sup_opts_init(C.byref(o))
     o.gpu_num, o.device_id, o.threads = int(gpu_num), int(device_id), int(threads)
     o.cpu_worker, o.walk_log2, o.chunk_log2 = int(bool(cpu)), int(walk_log2), int(chunk_log2)
     o.use_rccl, o.verbose = int(use_rccl), int(bool(verbose))  # use_rccl=2: RCCL even on one device
+    o.jit = int(jit)  # segmented walk: -1 never, 0 auto, 1 whenever its cost model wins
     return o
 
 
@@ -107,25 +109,30 @@ def layout(n: int) -> tuple[int, int, int]:
 
 def perman(mat, algo: int = 4, sparse: bool = False, gpu_num: int = 1, cpu: bool = False,
            threads: int = 16, device_id: int = 0, use_rccl: bool = False, walk_log2: int = 0,
-           chunk_log2: int = 0, return_stats: bool = False):
+           chunk_log2: int = 0, return_stats: bool = False, jit: int = 0, kernel: str | None = None):
     """GPU exact permanent, dispatched by the reference algorithm id (main.cu:30-143).
 
     ``sparse`` selects the sparse table (SpaRyser ids 1-6, SkipPer 7/8).  Apply
-    ``sort_order``/``skip_order`` first to mirror ``-r1``/``-r2``.
+    ``sort_order``/``skip_order`` first to mirror ``-r1``/``-r2``.  ``jit``:
+    pattern-specialised segmented walk (-1 never, 0 auto, 1 when it is cheaper).
+    ``kernel`` overrides the algorithm id's walk family ("dense", "sparse",
+    "skip", "dense_plain", "seg") and keeps its device schedule.
     """
     table = ALGOS_SPARSE if sparse else ALGOS_DENSE
     if algo not in table:
         raise SupError(-7, "perman", f"unknown algorithm id {algo}")
-    _, kernel, sched = table[algo]
+    _, kern, sched = table[algo]
+    if kernel is not None:
+        kern = _KERNELS[kernel]
     if algo == 66:
         gpu_num = 4
     if sched == SCHED_SINGLE:
         gpu_num = 1
     a, dt, n = _mat(mat)
     lib = _lib.load()
-    o = _opts(gpu_num, device_id, threads, cpu, walk_log2, chunk_log2, use_rccl)
+    o = _opts(gpu_num, device_id, threads, cpu, walk_log2, chunk_log2, use_rccl, jit=jit)
     out, st = C.c_double(0.0), SupStats()
-    _lib.check(lib.sup_perman(a.ctypes.data, dt, n, kernel, sched, C.byref(o), C.byref(out), C.byref(st)),
+    _lib.check(lib.sup_perman(a.ctypes.data, dt, n, kern, sched, C.byref(o), C.byref(out), C.byref(st)),
                table[algo][0])
     return (out.value, st.as_dict()) if return_stats else out.value
 
@@ -153,27 +160,42 @@ def partial(mat, start: int, end: int, kernel: str = "dense", gpu_num: int = 1, 
 
 
 def perman_shard(mat, shard: int, nshards: int, kernel: str = "dense", device_id: int = 0,
-                 return_stats: bool = False):
+                 return_stats: bool = False, jit: int = 0):
     """Partial sum of shard `shard` of `nshards` of the engine's enumeration
     (one process per GPU): the shards add up to perm / (4(n&1)-2)."""
     a, dt, n = _mat(mat)
     lib = _lib.load()
-    o = _opts(device_id=device_id)
+    o = _opts(device_id=device_id, jit=jit)
     out, st = C.c_double(0.0), SupStats()
     _lib.check(lib.sup_perman_shard(a.ctypes.data, dt, n, _KERNELS[kernel], int(shard), int(nshards), C.byref(o),
                                     C.byref(out), C.byref(st)), "perman_shard")
     return (out.value, st.as_dict()) if return_stats else out.value
 
 
-def plan_info(mat, kernel: str = "dense") -> dict:
-    """The plan the engine runs for `kernel`: walk kind, column map, layout."""
+def plan_info(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1) -> dict:
+    """The plan the engine runs for `kernel` (and options jit / gpu_num): walk
+    kind, column map, layout."""
     a, dt, n = _mat(mat)
     lib = _lib.load()
     kind, L, m = C.c_int(), C.c_int(), C.c_int()
     cm = np.zeros(max(n - 1, 1), np.int32)
-    _lib.check(lib.sup_plan_info(a.ctypes.data, dt, n, _KERNELS[kernel], C.byref(kind), cm.ctypes.data,
+    o = _opts(gpu_num=gpu_num, jit=jit)
+    _lib.check(lib.sup_plan_info(a.ctypes.data, dt, n, _KERNELS[kernel], C.byref(o), C.byref(kind), cm.ctypes.data,
                                  C.byref(L), C.byref(m)), "plan_info")
     return {"kind": WALK_NAMES[kind.value], "colmap": cm[: n - 1].copy(), "L": L.value, "m": m.value}
+
+
+def prepare(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1) -> dict:
+    """Plan `mat` as perman / perman_shard would and compile the segmented
+    walk's specialised kernel now if the plan uses it (hiprtc, no device
+    needed): {"kind": walk name, "compile_ms": hiprtc time (0 when cached)}."""
+    a, dt, n = _mat(mat)
+    lib = _lib.load()
+    kind, ms = C.c_int(), C.c_double(0.0)
+    o = _opts(gpu_num=gpu_num, jit=jit)
+    _lib.check(lib.sup_prepare(a.ctypes.data, dt, n, _KERNELS[kernel], C.byref(o), C.byref(kind), C.byref(ms)),
+               "prepare")
+    return {"kind": WALK_NAMES[kind.value], "compile_ms": ms.value}
 
 
 def nw_start(mat) -> tuple[np.ndarray, float]:

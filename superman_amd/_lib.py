@@ -27,13 +27,14 @@ ERRORS = {
     -7: "SUP_EUNSUPPORTED",
 }
 SUP_INT32, SUP_FLOAT32, SUP_FLOAT64 = 0, 1, 2
-KERNEL_DENSE, KERNEL_SPARYSER, KERNEL_SKIPPER, KERNEL_DENSE_PLAIN = 0, 1, 2, 3
+KERNEL_DENSE, KERNEL_SPARYSER, KERNEL_SKIPPER, KERNEL_DENSE_PLAIN, KERNEL_SEGMENTED = 0, 1, 2, 3, 4
 SCHED_SINGLE, SCHED_STATIC, SCHED_CHUNKS = 0, 1, 2
 
 # Every symbol include/superman.h declares (checked by tests/test_capi.py).
 EXPORTS = [
     "sup_opts_init", "sup_abi_version", "sup_last_error", "sup_device_count",
     "sup_perman", "sup_partial", "sup_perman_cpu", "sup_nw_start", "sup_perman_shard", "sup_plan_info",
+    "sup_prepare",
     "sup_gpu_perman64_xshared_coalescing_mshared",
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpu",
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks",
@@ -53,7 +54,7 @@ class SupOpts(C.Structure):
         ("gpu_num", C.c_int), ("device_id", C.c_int), ("threads", C.c_int),
         ("cpu_worker", C.c_int), ("grid_dim", C.c_int), ("block_dim", C.c_int),
         ("walk_log2", C.c_int), ("chunk_log2", C.c_int), ("use_rccl", C.c_int),
-        ("verbose", C.c_int),
+        ("verbose", C.c_int), ("jit", C.c_int),
     ]
 
 
@@ -86,6 +87,7 @@ class SupStats(C.Structure):
         ("devices_used", C.c_int), ("lane_bits", C.c_int), ("walk_bits", C.c_int),
         ("grid", C.c_int), ("chunks_done_cpu", C.c_int), ("partials", C.c_double * 16),
         ("walk_kind", C.c_int), ("leaves", C.c_int), ("est_ops_per_step", C.c_double),
+        ("jit_ms", C.c_double),
     ]
 
     def as_dict(self) -> dict:
@@ -124,7 +126,7 @@ def load() -> C.CDLL:
             build()
         lib = C.CDLL(LIB_PATH)
         _declare(lib)
-        if lib.sup_abi_version() != 1:
+        if lib.sup_abi_version() != 2:
             raise RuntimeError("libsuperman_hip.so ABI version mismatch")
         _lib = lib
         return lib
@@ -142,7 +144,8 @@ def _declare(lib: C.CDLL) -> None:
                                 C.POINTER(SupStats)]
     lib.sup_perman_cpu.argtypes = [P, I, I, I, I, C.POINTER(D), C.POINTER(SupStats)]
     lib.sup_perman_shard.argtypes = [P, I, I, I, I, I, C.POINTER(SupOpts), C.POINTER(D), C.POINTER(SupStats)]
-    lib.sup_plan_info.argtypes = [P, I, I, I, C.POINTER(I), P, C.POINTER(I), C.POINTER(I)]
+    lib.sup_plan_info.argtypes = [P, I, I, I, C.POINTER(SupOpts), C.POINTER(I), P, C.POINTER(I), C.POINTER(I)]
+    lib.sup_prepare.argtypes = [P, I, I, I, C.POINTER(SupOpts), C.POINTER(I), C.POINTER(C.c_double)]
     lib.sup_nw_start.argtypes = [P, I, I, C.POINTER(D), C.POINTER(D)]
     lib.sup_read_matrix.argtypes = [C.c_char_p, I, C.POINTER(P), C.POINTER(I), C.POINTER(I), C.POINTER(I)]
     lib.sup_free.argtypes = [P]

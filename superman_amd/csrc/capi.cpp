@@ -24,6 +24,7 @@ WalkKind kind_of(sup_kernel k) {
   switch (k) {
     case SUP_KERNEL_SPARYSER: return kWalkSparse;
     case SUP_KERNEL_SKIPPER: return kWalkSkip;
+    case SUP_KERNEL_SEGMENTED: return kWalkSeg;
     default: return kWalkDense;
   }
 }
@@ -44,6 +45,7 @@ void fill_stats(sup_stats* st, const Plan& P, const SchedResult& r, double wall_
   st->walk_kind = (int)P.kind;
   st->leaves = 1;
   st->est_ops_per_step = walk_cost(P);
+  st->jit_ms = r.compile_ms;
 }
 
 }  // namespace
@@ -95,7 +97,7 @@ int sup_perman(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched
     lay.m = std::min(o.walk_log2, rest);
     lay.h = rest - lay.m;
   }
-  if ((rc = plan_for(A.data(), n, kernel, lay, P))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, lay, P, o.jit, sched == SUP_SCHED_SINGLE ? 1 : o.gpu_num))) return rc;
   SchedResult r;
   if ((rc = schedule(P, sched, o, 0, P.lay.chunks(), r))) return rc;
   *out = (double)(4 * (n & 1) - 2) * r.total;  // gpu_exact_dense.cu:698
@@ -181,7 +183,7 @@ int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int
   std::vector<double> A;
   if ((rc = to_double(mat, t, n, A))) return rc;
   Plan P;
-  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, nshards))) return rc;
   const uint64_t C = P.lay.chunks();
   const uint64_t c0 = C * (uint64_t)shard / (uint64_t)nshards, c1 = C * (uint64_t)(shard + 1) / (uint64_t)nshards;
   SchedResult r;
@@ -192,18 +194,37 @@ int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int
   return SUP_OK;
 }
 
-int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, int* walk_kind, int* colmap, int* L,
-                  int* m) {
+int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o_in, int* walk_kind,
+                  int* colmap, int* L, int* m) {
   std::vector<double> A;
   int rc = to_double(mat, t, n, A);
   if (rc) return rc;
+  sup_opts o;
+  if (o_in) o = *o_in;
+  else sup_opts_init(&o);
   Plan P;
-  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num))) return rc;
   if (walk_kind) *walk_kind = (int)P.kind;
   if (colmap)
     for (int e = 0; e < n - 1; ++e) colmap[e] = P.colmap[e];
   if (L) *L = P.lay.L;
   if (m) *m = P.lay.m;
+  return SUP_OK;
+}
+
+int sup_prepare(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o_in, int* walk_kind,
+                double* compile_ms) {
+  std::vector<double> A;
+  int rc = to_double(mat, t, n, A);
+  if (rc) return rc;
+  sup_opts o;
+  if (o_in) o = *o_in;
+  else sup_opts_init(&o);
+  Plan P;
+  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num))) return rc;
+  if (walk_kind) *walk_kind = (int)P.kind;
+  if (compile_ms) *compile_ms = 0.0;
+  if (P.kind == kWalkSeg) return jit_compile_only(P, compile_ms);
   return SUP_OK;
 }
 

@@ -141,6 +141,7 @@ std::vector<int> greedy_walk_order(const double* A, int n, int count) {
 
 double walk_cost(const Plan& P) {
   if (P.kind == kWalkDense) return 2.0 * P.n + 1.0;
+  if (P.kind == kWalkSeg) return seg_walk_cost(P);
   double cost = 0.0, w = 0.5;
   for (int k = 0; k < P.lay.m; ++k, w *= 0.5) cost += w * (16.0 * P.nblk[P.lay.L + k] + 1.0);
   return cost + w * 16.0 * ((P.n + 7) / 8);  // tail: the rest of the walk bits, bounded
@@ -162,10 +163,11 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
   // ---- engine bit -> matrix column
   P.colmap.resize(nb);
   for (int e = 0; e < nb; ++e) P.colmap[e] = e;
-  if (!identity_map && kind == kWalkSparse && m > 0) {
-    // walk bits get the greedy prefix order (greedy_walk_order), lane bits
-    // the next L columns of that order, high bits the rest in matrix order.
-    std::vector<int> order = greedy_walk_order(A, n, m + L);
+  if (!identity_map && (kind == kWalkSparse || kind == kWalkSeg) && m > 0) {
+    // walk bits get the greedy prefix order (greedy_walk_order; the segmented
+    // walk: seg_walk_order), lane bits the next L columns of that order, high
+    // bits the rest in matrix order.
+    std::vector<int> order = kind == kWalkSeg ? seg_walk_order(A, n, m, m + L) : greedy_walk_order(A, n, m + L);
     std::vector<char> used(n, 0);
     for (int k = 0; k < m; ++k) P.colmap[L + k] = order[k], used[order[k]] = 1;
     for (int e = 0; e < L; ++e) P.colmap[e] = order[m + e], used[order[m + e]] = 1;
@@ -231,28 +233,50 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
       if (A[(size_t)i * n + P.colmap[L + k]] != 0.0) rm |= 1ull << k;
     P.rowmask[j] = rm;
   }
+  if (kind == kWalkSeg) return build_seg(P);
   return SUP_OK;
 }
 
-int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P) {
+// fp64 VALU lane-ops per second of one MI355X on the walk kernels (measured:
+// 46.6 ops/step at 7.98e11 steps/s on the n=40 bench), for jit's auto mode.
+static constexpr double kLaneOpsPerSec = 3.7e13;
+// Compile + load of a specialised kernel is ~0.4 s; auto mode specialises only
+// when the predicted walk time saved is clearly larger.
+static constexpr double kJitMinSavingSec = 1.0;
+
+int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit, int ndev) {
+  // candidates in preference order; the cheapest by walk_cost wins
+  std::vector<WalkKind> kinds;
   switch (kernel) {
     case SUP_KERNEL_SKIPPER: return make_plan(A, n, kWalkSkip, false, lay, P);
-    case SUP_KERNEL_SPARYSER: return make_plan(A, n, kWalkSparse, false, lay, P);
     case SUP_KERNEL_DENSE_PLAIN: return make_plan(A, n, kWalkDense, false, lay, P);
-    case SUP_KERNEL_DENSE: {
-      Plan d, s;
-      int rc = make_plan(A, n, kWalkDense, false, lay, d);
-      if (rc) return rc;
-      if (n >= 8 && (rc = make_plan(A, n, kWalkSparse, false, lay, s)) == SUP_OK && walk_cost(s) < walk_cost(d)) {
-        P = std::move(s);
-        return SUP_OK;
+    case SUP_KERNEL_SEGMENTED:
+      if (n < 10 || lay.m < 3) {
+        set_error("the segmented walk needs n >= 10 (>= 3 walk bits)");
+        return SUP_EUNSUPPORTED;
       }
-      P = std::move(d);
-      return SUP_OK;
+      return make_plan(A, n, kWalkSeg, false, lay, P);
+    case SUP_KERNEL_SPARYSER: kinds = {kWalkSparse}; break;
+    case SUP_KERNEL_DENSE: kinds = {kWalkDense}; if (n >= 8) kinds.push_back(kWalkSparse); break;
+    default: set_error("unknown sup_kernel"); return SUP_EINVAL;
+  }
+  Plan best;
+  int rc = make_plan(A, n, kinds[0], false, lay, best);
+  if (rc) return rc;
+  for (size_t i = 1; i < kinds.size(); ++i) {
+    Plan c;
+    if (make_plan(A, n, kinds[i], false, lay, c) == SUP_OK && walk_cost(c) < walk_cost(best)) best = std::move(c);
+  }
+  if (jit >= 0 && n >= 8 && lay.m >= 3) {
+    Plan s;
+    if (make_plan(A, n, kWalkSeg, false, lay, s) == SUP_OK && walk_cost(s) < walk_cost(best)) {
+      const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
+      const double saved = steps * (walk_cost(best) - walk_cost(s)) / kLaneOpsPerSec;
+      if (jit >= 1 || saved >= kJitMinSavingSec) best = std::move(s);
     }
   }
-  set_error("unknown sup_kernel");
-  return SUP_EINVAL;
+  P = std::move(best);
+  return SUP_OK;
 }
 
 double pairwise_host(const std::vector<double>& v) {
@@ -276,6 +300,8 @@ struct DeviceCtx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double* d_cols = nullptr;
   size_t cols_cap = 0;
+  double* d_jtab = nullptr;
+  size_t jtab_cap = 0;
   double* d_x0 = nullptr;
   int* d_nblk = nullptr;
   uint64_t* d_rowmask = nullptr;
@@ -288,7 +314,7 @@ struct DeviceCtx {
   unsigned* d_counter = nullptr;
   double* d_result = nullptr;
   std::mutex mu;
-  int occ[3][SUP_MAX_N + 1] = {};
+  int occ[3][SUP_MAX_N + 1] = {};  // AOT kernels; segmented walk: jit_occupancy
 };
 
 static std::mutex g_ctx_mu;
@@ -373,7 +399,12 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   const bool visited = want_visited && P.kind == kWalkSkip;
   if (visited && (rc = ensure(c->d_visited, c->visited_cap, (size_t)count))) return rc;
 
+  const bool seg = P.kind == kWalkSeg;
+  if (seg && (rc = ensure(c->d_jtab, c->jtab_cap, P.jtab.size()))) return rc;
+
   hipStream_t s = c->stream;
+  if (seg)
+    SUP_HIP(hipMemcpyAsync(c->d_jtab, P.jtab.data(), P.jtab.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemcpyAsync(c->d_cols, P.cols.data(), P.cols.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemcpyAsync(c->d_x0, P.x0.data(), P.x0.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemcpyAsync(c->d_nblk, P.nblk.data(), P.nblk.size() * sizeof(int), hipMemcpyHostToDevice, s));
@@ -381,7 +412,9 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
                          hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
 
-  int& occ = c->occ[P.kind][P.n];
+  int occ_seg = 0;
+  if (seg && (rc = jit_occupancy(dev, P, &occ_seg, &r.compile_ms))) return rc;
+  int& occ = seg ? occ_seg : c->occ[P.kind][P.n];
   if (occ == 0) {
     int b = 0;
     SUP_HIP(walk_occupancy(P.kind, P.n, &b));
@@ -411,6 +444,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   p.counter = c->d_counter;
   p.visited = visited ? c->d_visited : nullptr;
   p.group = group;
+  p.jtab = seg ? c->d_jtab : nullptr;
   p.nb_lo = p.nb_hi = 0;
   for (int k = 0; k < P.lay.m && k < 32; ++k) {
     const uint64_t v = (uint64_t)(P.nblk[P.lay.L + k] & 15);
@@ -419,7 +453,11 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   }
 
   SUP_HIP(hipEventRecord(c->ev0, s));
-  SUP_HIP(launch_walk(P.kind, P.n, p, (int)grid, s));
+  if (seg) {
+    if ((rc = jit_launch(dev, P, p, (int)grid, s))) return rc;
+  } else {
+    SUP_HIP(launch_walk(P.kind, P.n, p, (int)grid, s));
+  }
   SUP_HIP(hipEventRecord(c->ev1, s));
   SUP_HIP(launch_pairwise_reduce(c->d_chunk, count, c->d_scratch, c->d_result, s));
   double result = 0.0;
@@ -507,6 +545,11 @@ int rccl_allreduce_partials(const std::vector<int>& devs, const std::vector<std:
 int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uint64_t c1,
              SchedResult& out) {
   out = SchedResult();
+  struct JitClock {  // hiprtc time spent while this schedule ran
+    SchedResult& o;
+    double t0 = jit_compile_ms_total();
+    ~JitClock() { o.compile_ms = jit_compile_ms_total() - t0; }
+  } jit_clock{out};
   int ndev = 0;
   int rc = device_count(&ndev);
   if (rc) return rc;

@@ -47,6 +47,19 @@ struct Plan {
   std::vector<int> nblk;           // n-1: prefix row-block count per engine bit
   std::vector<uint64_t> rowmask;   // n: walk-bit mask of each engine row
   uint64_t umask = 0;              // lane-uniform engine rows
+  // ---- segmented walk (kind kWalkSeg, jit.cpp) ----
+  // Engine rows [0, R) are the rows some walk column touches, in first-touch
+  // order; segment i = rows [seg_start[i], seg_start[i+1]) are the rows walk
+  // bit k_i touched first; rows [seg_start.back(), n) ("rest") no walk column
+  // touches.  touched[k] = engine rows with a nonzero in walk bit k.
+  std::vector<int> seg_start;
+  std::vector<std::vector<int>> touched;
+  int seg_b = 0;                   // walk bits [0, seg_b) have specialised steps (seg_static_bits)
+  std::vector<int> dyn_rows;       // rows touched by walk bits >= seg_b (their shared step)
+  std::vector<int> jofs;           // [m] offset (doubles) of walk bit k's + block in jtab
+  std::vector<double> jtab;        // packed touched values: + block, - block (each padded to 8)
+  std::string jit_src;             // generated HIP source of the specialised kernel
+  uint64_t jit_key = 0;            // hash of jit_src + compile options
 };
 
 // Build a plan.  identity_map keeps engine bit e = column e (needed when a
@@ -57,6 +70,27 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
 // Walk-column order minimising the prefix-block cost (first `count` columns).
 std::vector<int> greedy_walk_order(const double* A, int n, int count);
 
+// ---- segmented walk (jit.cpp) ----
+// Walk-column order for the segmented walk: greedy starts from every column,
+// then pairwise-swap descent on seg_cost (first `count` columns returned).
+std::vector<int> seg_walk_order(const double* A, int n, int m, int count);
+// Fill the segment structure, packed table and generated source of a plan
+// whose rows are already in first-touch order (make_plan, kind kWalkSeg).
+int build_seg(Plan& P);
+// Walk bits with a specialised step: min(m, 5) (the walk loop is unrolled by
+// 2^b Gray steps; bits >= b share one straight-line step).
+int seg_static_bits(int m);
+// fp64 VALU ops per Gray step and lane of the segmented walk.
+double seg_walk_cost(const Plan& P);
+// Resolve (compile or fetch from cache) the specialised kernel of P for the
+// current device `dev`, then launch it / query its occupancy.
+int jit_occupancy(int dev, const Plan& P, int* blocks_per_cu, double* compile_ms);
+int jit_launch(int dev, const Plan& P, const WalkParams& p, int grid, hipStream_t s);
+// Compile (or find in the caches) the specialised kernel of P without loading it.
+int jit_compile_only(const Plan& P, double* compile_ms);
+// Milliseconds spent compiling specialised kernels in this process (hiprtc).
+double jit_compile_ms_total();
+
 // Estimated fp64 VALU ops per Gray step of a plan (dense: 2n+1; prefix kernels:
 // sum_k 2^-(k+1) (16 nblk_k + 1)).
 double walk_cost(const Plan& P);
@@ -65,13 +99,16 @@ double walk_cost(const Plan& P);
 // SUP_KERNEL_DENSE the engine takes the prefix-blocked walk whenever its cost
 // model is lower (same sum, structural zeros skipped); SUP_KERNEL_DENSE_PLAIN
 // forces the plain dense walk.
-int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P);
+// jit: sup_opts.jit (-1 never, 0 auto, 1 whenever the segmented walk's cost
+// model wins); ndev: devices the walk is spread over (auto mode's estimate).
+int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit = -1, int ndev = 1);
 
 struct RangeResult {
   double partial = 0.0;     // pairwise sum over the range's wave-chunks
   double kernel_ms = 0.0;   // walk kernel device time (hipEvents on the launch stream)
   uint64_t visited = 0;     // evaluated products (lanes * steps), skipper only
   int grid = 0;
+  double compile_ms = 0.0;  // segmented walk: hiprtc compile time spent by this call
 };
 
 // Walk wave-chunks [c0, c1) of plan P on device `dev` (synchronous).
@@ -90,6 +127,7 @@ struct SchedResult {
   int devices = 0;
   int grid = 0;
   int cpu_items = 0;
+  double compile_ms = 0.0;  // summed over devices
   std::vector<double> dev_partials;
 };
 int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uint64_t c1,

@@ -7,6 +7,7 @@
 // device is present.  It simulates the 64 lanes of a wave and performs the
 // same fp64 operations in the same order as walk_{dense,sparse,skip}.hip, so
 // a chunk range gives bit-identical partials on CPU and GPU.
+#include <algorithm>
 #include <cmath>
 #include <thread>
 
@@ -19,6 +20,7 @@ namespace {
 struct Lane {
   double x[SUP_MAX_N];
   double U[SUP_MAX_N / 8 + 2];
+  double S[SUP_MAX_N], SU[SUP_MAX_N + 1], R;  // segmented walk
 };
 
 inline double prod4(const double* x, int n) {
@@ -90,11 +92,92 @@ inline uint32_t next_toggle(uint32_t t, uint32_t k) {
   return c;
 }
 
+// ---- segmented walk (jit.cpp's generated kernel, same operations) --------
+double seg_tree(const double* x, int lo, int hi) {
+  if (hi - lo == 1) return x[lo];
+  const int mid = lo + (hi - lo + 1) / 2;
+  return seg_tree(x, lo, mid) * seg_tree(x, mid, hi);
+}
+
+// Walk bits k < seg_b: their own touched rows; bits >= seg_b: one shared step
+// over dyn_rows (the generated kernel's straight-line step for those bits).
+struct SegSteps {
+  std::vector<int> smax;                  // deepest touched segment per walk bit (-1: none)
+  std::vector<std::vector<char>> dirty;   // [k][segment]
+  explicit SegSteps(const Plan& P) : smax(P.lay.m, -1), dirty(P.lay.m) {
+    const int nseg = (int)P.seg_start.size() - 1;
+    for (int k = 0; k < P.lay.m; ++k) {
+      dirty[k].assign(nseg, 0);
+      for (int r : (k < P.seg_b ? P.touched[k] : P.dyn_rows)) {
+        int i = 0;
+        while (P.seg_start[i + 1] <= r) ++i;
+        dirty[k][i] = 1;
+        smax[k] = std::max(smax[k], i);
+      }
+    }
+  }
+};
+
+inline void seg_chain(Lane& s, const Plan& P, int i) {
+  const int nseg = (int)P.seg_start.size() - 1;
+  const bool rest = P.seg_start.back() < P.n;
+  s.SU[i] = i + 1 < nseg ? s.S[i] * s.SU[i + 1] : (rest ? s.S[i] * s.R : s.S[i]);
+}
+
+void seg_init(Lane& s, const Plan& P) {
+  const int nseg = (int)P.seg_start.size() - 1;
+  s.R = P.seg_start.back() < P.n ? seg_tree(s.x, P.seg_start.back(), P.n) : 1.0;
+  for (int i = nseg - 1; i >= 0; --i) {
+    s.S[i] = seg_tree(s.x, P.seg_start[i], P.seg_start[i + 1]);
+    seg_chain(s, P, i);
+  }
+}
+
+void seg_step(Lane& s, const Plan& P, const SegSteps& st, int k, int neg) {
+  if (k >= P.seg_b) {  // shared step: full signed column over dyn_rows (zeros included)
+    if (P.dyn_rows.empty()) return;
+    const double* c = col_of(P, P.lay.L + k, neg);
+    for (int r : P.dyn_rows) s.x[r] += c[r];
+  } else {
+    const std::vector<int>& t = P.touched[k];
+    if (t.empty()) return;
+    const size_t blk = (t.size() + 7) & ~(size_t)7;
+    const double* v = P.jtab.data() + P.jofs[k] + (neg ? blk : 0);
+    for (size_t i = 0; i < t.size(); ++i) s.x[t[i]] += v[i];
+  }
+  for (int i = st.smax[k]; i >= 0; --i) {
+    if (st.dirty[k][i]) s.S[i] = seg_tree(s.x, P.seg_start[i], P.seg_start[i + 1]);
+    seg_chain(s, P, i);
+  }
+}
+
 // One wave-chunk: returns the wave's pairwise lane sum.
 double chunk_partial(const Plan& P, uint64_t ga) {
   const int n = P.n, L = P.lay.L, m = P.lay.m;
   const uint32_t T = 1u << m;
   double lane_val[64];
+  if (P.kind == kWalkSeg) {
+    const SegSteps st(P);
+    for (unsigned l = 0; l < 64; ++l) {
+      if (l >= (1u << L)) {
+        lane_val[l] = 0.0;
+        continue;
+      }
+      Lane s;
+      chunk_start(P, ga, l, s);
+      seg_init(s, P);
+      double acc = s.SU[0];
+      for (uint32_t t = 1; t < T; ++t) {
+        const uint32_t k = __builtin_ctz(t);
+        seg_step(s, P, st, (int)k, (t >> (k + 1)) & 1u);
+        acc = (t & 1u) ? acc - s.SU[0] : acc + s.SU[0];
+      }
+      const unsigned par = (unsigned)__builtin_popcount(l) & 1u;
+      if ((((unsigned)ga) ^ par) & 1u) acc = -acc;
+      lane_val[l] = acc;
+    }
+    return pairwise64(lane_val);
+  }
   if (P.kind != kWalkSkip) {
     for (unsigned l = 0; l < 64; ++l) {
       if (l >= (1u << L)) {

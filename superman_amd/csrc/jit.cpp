@@ -1,0 +1,605 @@
+// jit.cpp — the segmented walk: a Gray walk kernel specialised at run time for
+// one matrix pattern, compiled for gfx950 with hiprtc.
+//
+// Why.  The reference SpaRyser step touches only the CSC rows of the flipped
+// column but keeps the product incrementally with an fp64 divide
+// (gpu_exact_sparse.cu:503-549).  The ahead-of-time prefix-blocked walk
+// (walk_sparse.hip) avoids the divide by keeping suffix products of 8-row
+// blocks, but it must add the whole block (zeros included) and re-multiply
+// every block of the prefix.  When the kernel is generated for the pattern at
+// hand, every walk step is straight-line code that
+//   * adds the flipped column only to the rows it touches (values packed
+//     contiguously, one s_load_dwordx16 per 8 of them, SGPR operands of
+//     v_add_f64), and
+//   * re-multiplies only the segments that contain a touched row, then the
+//     suffix chain U_i = S_i * U_{i+1} down to U_0, the term.
+// Segments are the first-touch groups of the walk columns (rows walk bit k
+// touched first), so a step of walk bit k never goes deeper than segment k.
+// The cost model (seg_walk_cost) is ~37.5 fp64 ops per Gray step on the n=40
+// d=0.5 bench matrix against 45.5 for the 8-row blocks and 81 for the plain
+// dense walk; 10.1 against 21.5 on the n=36 d=0.2 SpaRyser config.
+//
+// The walk loop is unrolled by 8 Gray steps: steps t = 8q+1..8q+7 flip walk
+// bits 0,1,0,2,0,1,0 — bits 0 and 1 with compile-time signs (their table
+// address is a constant), bit 2 with sign q&1 — and t = 8q+8 flips bit
+// 3+ctz(q+1) through a switch.  Everything else (chunk start, lane layout,
+// wave-chunk queue, reduction order) is walk_common.hpp's, shared with the
+// ahead-of-time kernels, and the arithmetic is mirrored bit for bit by
+// engine_cpu.cpp (seg_*) and oracle/oracle.c (kind 3).
+//
+// Compiled code objects are cached in memory (per process, per device) and on
+// disk: $SUP_JIT_CACHE_DIR, else $XDG_CACHE_HOME/superman_amd, else
+// ~/.cache/superman_amd (SUP_JIT_CACHE_DIR="" disables the disk cache).
+#include <hip/hiprtc.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <sstream>
+
+#include "engine.hpp"
+
+namespace sup {
+
+namespace {
+#include "jit_headers.inc"  // kWalkCommonSrc, kWalkParamsSrc (generated from the headers by the Makefile)
+
+// ---------------------------------------------------------------- planning --
+
+struct SegShape {
+  std::vector<int> seg_start;               // boundaries, rows in first-touch order
+  std::vector<std::vector<int>> touched;    // per walk bit, engine rows
+};
+
+// Segment structure of walk columns `walk` (matrix columns, in walk-bit order):
+// rows are numbered in first-touch order.
+SegShape seg_shape(const double* A, int n, const std::vector<int>& walk) {
+  SegShape s;
+  std::vector<int> pos(n, -1);
+  int R = 0;
+  s.seg_start.push_back(0);
+  for (int c : walk) {
+    for (int i = 0; i < n; ++i)
+      if (pos[i] < 0 && A[(size_t)i * n + c] != 0.0) pos[i] = R++;
+    if (R > s.seg_start.back()) s.seg_start.push_back(R);
+  }
+  for (int c : walk) {
+    std::vector<int> t;
+    for (int i = 0; i < n; ++i)
+      if (A[(size_t)i * n + c] != 0.0) t.push_back(pos[i]);
+    std::sort(t.begin(), t.end());
+    s.touched.push_back(std::move(t));
+  }
+  return s;
+}
+
+int seg_index(const std::vector<int>& seg_start, int row) {
+  return (int)(std::upper_bound(seg_start.begin(), seg_start.end(), row) - seg_start.begin()) - 1;
+}
+
+// VALU ops of one step of walk bit k (the generated code, exactly): |touched|
+// adds; per segment i <= smax: (len_i - 1) muls when it holds a touched row,
+// one chain mul (none for the last segment when no rest rows exist); one
+// accumulate.
+double step_ops(const std::vector<int>& seg_start, int n, const std::vector<int>& t) {
+  if (t.empty()) return 1.0;
+  const int nseg = (int)seg_start.size() - 1;
+  const bool rest = seg_start.back() < n;
+  std::vector<char> dirty(nseg, 0);
+  int smax = 0;
+  for (int r : t) {
+    const int i = seg_index(seg_start, r);
+    dirty[i] = 1;
+    smax = std::max(smax, i);
+  }
+  double ops = (double)t.size() + 1.0;
+  for (int i = 0; i <= smax; ++i) {
+    if (dirty[i]) ops += seg_start[i + 1] - seg_start[i] - 1;
+    if (i < nseg - 1 || rest) ops += 1.0;
+  }
+  return ops;
+}
+
+// Walk bits k < b get a specialised step each; bits k >= b (1/2^b of the
+// steps) share one step over the union of their rows.
+double cost_of(const std::vector<int>& seg_start, int n, const std::vector<std::vector<int>>& touched) {
+  const int m = (int)touched.size(), b = seg_static_bits(m);
+  std::vector<char> in(n, 0);
+  for (int k = b; k < m; ++k)
+    for (int r : touched[k]) in[r] = 1;
+  std::vector<int> dyn;
+  for (int j = 0; j < n; ++j)
+    if (in[j]) dyn.push_back(j);
+  const double dyn_ops = step_ops(seg_start, n, dyn);
+  double c = 0.0, w = 0.5;
+  for (int k = 0; k < m; ++k, w *= 0.5) c += w * (k < b ? step_ops(seg_start, n, touched[k]) : dyn_ops);
+  return c;
+}
+
+double shape_cost(const SegShape& s, int n) { return cost_of(s.seg_start, n, s.touched); }
+
+}  // namespace
+
+int seg_static_bits(int m) { return std::min(m, 5); }
+
+double seg_walk_cost(const Plan& P) { return cost_of(P.seg_start, P.n, P.touched); }
+
+std::vector<int> seg_walk_order(const double* A, int n, int m, int count) {
+  const int nb = n - 1;
+  m = std::min(m, nb);
+  count = std::min(std::max(count, m), nb);
+  std::vector<int> nnz(n, 0);
+  for (int c = 0; c < nb; ++c)
+    for (int i = 0; i < n; ++i) nnz[c] += A[(size_t)i * n + c] != 0.0;
+  // greedy continuation: fewest newly touched rows, then fewest nonzeros, then lowest index
+  auto extend = [&](std::vector<int> order, int upto) {
+    std::vector<char> used(n, 0), placed(n, 0);
+    for (int c : order) {
+      used[c] = 1;
+      for (int i = 0; i < n; ++i) placed[i] |= A[(size_t)i * n + c] != 0.0;
+    }
+    while ((int)order.size() < upto) {
+      int best = -1, bnew = 1 << 30;
+      for (int c = 0; c < nb; ++c) {
+        if (used[c]) continue;
+        int nw = 0;
+        for (int i = 0; i < n; ++i) nw += !placed[i] && A[(size_t)i * n + c] != 0.0;
+        if (nw < bnew || (nw == bnew && nnz[c] < nnz[best])) best = c, bnew = nw;
+      }
+      used[best] = 1;
+      order.push_back(best);
+      for (int i = 0; i < n; ++i) placed[i] |= A[(size_t)i * n + best] != 0.0;
+    }
+    return order;
+  };
+  auto cost = [&](const std::vector<int>& o) {
+    return shape_cost(seg_shape(A, n, std::vector<int>(o.begin(), o.begin() + m)), n);
+  };
+  std::vector<int> best;
+  double bcost = 1e300;
+  for (int f = 0; f < nb && m > 0; ++f) {
+    std::vector<int> o = extend({f}, m);
+    const double c = cost(o);
+    if (c < bcost) bcost = c, best = o;
+  }
+  if (m == 0) return extend({}, count);
+  // descent: swap a walk position with another walk position or an unused
+  // column while the cost drops (positions whose weight 2^-(k+1) is visible)
+  const int hot = std::min(m, 12);
+  for (int pass = 0; pass < 8; ++pass) {
+    bool improved = false;
+    for (int a = 0; a < hot; ++a) {
+      for (int c = 0; c < nb; ++c) {
+        if (c == best[a]) continue;
+        std::vector<int> o = best;
+        auto it = std::find(o.begin(), o.end(), c);
+        if (it != o.end()) std::swap(o[a], *it);
+        else o[a] = c;
+        const double v = cost(o);
+        if (v < bcost - 1e-12) bcost = v, best = o, improved = true;
+      }
+    }
+    if (!improved) break;
+  }
+  return extend(best, count);
+}
+
+// ----------------------------------------------------------------- codegen --
+namespace {
+
+std::string tree(int lo, int hi) {
+  if (hi - lo == 1) return "x[" + std::to_string(lo) + "]";
+  const int mid = lo + (hi - lo + 1) / 2;
+  return "(" + tree(lo, mid) + " * " + tree(mid, hi) + ")";
+}
+
+struct Gen {
+  const Plan& P;
+  int nseg;
+  bool rest;
+  std::ostringstream o;
+  explicit Gen(const Plan& p) : P(p), nseg((int)p.seg_start.size() - 1), rest(p.seg_start.back() < p.n) {}
+
+  int len(int i) const { return P.seg_start[i + 1] - P.seg_start[i]; }
+  std::string S(int i) const { return len(i) == 1 ? "x[" + std::to_string(P.seg_start[i]) + "]" : "S" + std::to_string(i); }
+  std::string unext(int i) const { return i + 1 < nseg ? "U" + std::to_string(i + 1) : "R"; }
+  std::string chain(int i) const {
+    return (i + 1 < nseg || rest) ? S(i) + " * " + unext(i) : S(i);
+  }
+
+  // Add the values at table pointer `cv` (dbl8 pieces) to rows `rows`:
+  // value i of the block belongs to row rows[i] (packed table), or value
+  // rows[i] of the block (full column, `full`).  At most 2 pieces (32 SGPRs)
+  // are pinned at a time.
+  void adds(const std::vector<int>& rows, bool full, const char* ind) {
+    std::vector<std::pair<int, int>> vr;  // (value index, row)
+    for (size_t i = 0; i < rows.size(); ++i) vr.push_back({full ? rows[i] : (int)i, rows[i]});
+    std::vector<int> pieces;
+    for (auto& e : vr)
+      if (pieces.empty() || pieces.back() != e.first / 8) pieces.push_back(e.first / 8);
+    for (size_t g = 0; g < pieces.size(); g += 2) {
+      const size_t ge = std::min(pieces.size(), g + 2);
+      for (size_t q = g; q < ge; ++q) o << ind << "  jdbl8 v" << pieces[q] << " = cv[" << pieces[q] << "];\n";
+      o << ind << "  asm volatile(\"\" :";
+      for (size_t q = g; q < ge; ++q) o << (q > g ? ", " : " ") << "\"+s\"(v" << pieces[q] << ")";
+      o << ");\n";
+      for (auto& e : vr)
+        if (e.first / 8 >= pieces[g] && e.first / 8 <= pieces[ge - 1])
+          o << ind << "  x[" << e.second << "] += v" << e.first / 8 << "[" << e.first % 8 << "];\n";
+      if (ge < pieces.size()) o << ind << "  __builtin_amdgcn_sched_barrier(0);\n";
+    }
+  }
+
+  void products(const std::vector<int>& rows, const char* ind) {
+    std::vector<char> dirty(nseg, 0);
+    int smax = 0;
+    for (int r : rows) {
+      const int i = seg_index(P.seg_start, r);
+      dirty[i] = 1;
+      smax = std::max(smax, i);
+    }
+    for (int i = smax; i >= 0; --i) {
+      if (dirty[i] && len(i) > 1)
+        o << ind << "  S" << i << " = " << tree(P.seg_start[i], P.seg_start[i + 1]) << ";\n";
+      o << ind << "  U" << i << " = " << chain(i) << ";\n";
+    }
+  }
+
+  // step of walk bit k < seg_b: packed touched values; `off` = byte offset expression
+  void step(int k, const std::string& off, const char* ind) {
+    const std::vector<int>& t = P.touched[k];
+    if (t.empty()) return;
+    o << ind << "{\n";
+    o << ind << "  cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off << ");\n";
+    adds(t, false, ind);
+    products(t, ind);
+    o << ind << "}\n";
+  }
+
+  std::string off_const(int k, int neg) const {
+    const int blk = (((int)P.touched[k].size() + 7) & ~7);
+    return std::to_string((P.jofs[k] + neg * blk) * 8) + "u";
+  }
+  std::string off_dyn(int k, const char* negv) const {
+    const int blk = (((int)P.touched[k].size() + 7) & ~7);
+    return std::to_string(P.jofs[k] * 8) + "u + " + negv + " * " + std::to_string(blk * 8) + "u";
+  }
+
+  std::string source() {
+    const int n = P.n, L = P.lay.L, m = P.lay.m, b = P.seg_b;
+    const int R0 = P.seg_start.back();
+    const unsigned B = 1u << b, Q = 1u << (m - b);
+    o << "// generated by superman_amd jit.cpp: segmented Gray walk, n=" << n << " L=" << L << " m=" << m
+      << " segments=" << nseg << " static bits=" << b << "\n";
+    o << "#include \"walk_common.hpp\"\n";
+    o << "namespace sup {\n";
+    o << "typedef double jdbl8 __attribute__((ext_vector_type(8)));\n";
+    o << "typedef const __attribute__((address_space(4))) jdbl8 cjdbl8;\n";
+    o << "extern \"C\" __global__ __launch_bounds__(kBlock) void sup_walk_seg(WalkParams p) {\n";
+    o << "  constexpr int N = " << n << ";\n";
+    o << "  const uint32_t lane = threadIdx.x & 63u;\n";
+    o << "  const bool lane_valid = lane < " << (1u << L) << "u;\n";
+    o << "  const uint32_t lane_par = __builtin_popcount(lane) & 1u;\n";
+    o << "  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {\n";
+    o << "    double keep = 0.0;\n";
+    o << "    for (uint32_t j = 0; j < (uint32_t)p.group; ++j) {\n";
+    o << "      const uint64_t a = (uint64_t)g * p.group + j;\n";
+    o << "      if (a >= p.chunk_count) break;\n";
+    o << "      const uint64_t ga = p.chunk_begin + a;\n";
+    o << "      double x[N];\n";
+    o << "      chunk_start<N>(x, p, ga, lane);\n";
+    if (rest) o << "      const double R = " << tree(R0, n) << ";\n";
+    for (int i = 0; i < nseg; ++i)
+      if (len(i) > 1) o << "      double S" << i << " = " << tree(P.seg_start[i], P.seg_start[i + 1]) << ";\n";
+    for (int i = nseg - 1; i >= 0; --i) o << "      double U" << i << " = " << chain(i) << ";\n";
+    o << "      double acc = U0;\n";
+    o << "      for (uint32_t q = 0; q < " << Q << "u; ++q) {\n";
+    const char* ind = "        ";
+    // t = B*q + s, s = 1 .. B-1: bit k = ctz(s); neg = (t >> (k+1)) & 1, which
+    // is bit k+1 of s for k < b-1 and bit 0 of q for k = b-1
+    for (unsigned st = 1; st < B; ++st) {
+      const int k = __builtin_ctz(st);
+      if (k < b - 1) {
+        step(k, off_const(k, (st >> (k + 1)) & 1u), ind);
+      } else {
+        o << ind << "{\n" << ind << "  const uint32_t ng = q & 1u;\n";
+        step(k, off_dyn(k, "ng"), "          ");
+        o << ind << "}\n";
+      }
+      o << ind << (st & 1u ? "acc -= U0;\n" : "acc += U0;\n");
+    }
+    if (m > b) {
+      // t = B(q+1): bit k = b + ctz(q+1) >= b, neg = ((q+1) >> (ctz(q+1)+1)) & 1.
+      // One straight-line step for all of them (no per-bit branches): the full
+      // signed column is added to every row some bit >= b touches (zeros
+      // elsewhere) and every segment such a row lies in is re-multiplied.
+      o << ind << "if (q + 1u < " << Q << "u) {\n";
+      o << ind << "  const uint32_t kk = (uint32_t)__builtin_ctz(q + 1u);\n";
+      o << ind << "  const uint32_t ng = ((q + 1u) >> (kk + 1u)) & 1u;\n";
+      o << ind << "  cjdbl8* cv = (cjdbl8*)opaque_c(p.cols, (2u * (" << (L + b) << "u + kk) + ng) * "
+        << P.NP * 8 << "u);\n";
+      adds(P.dyn_rows, true, ind);
+      products(P.dyn_rows, ind);
+      o << ind << "  acc += U0;\n";
+      o << ind << "}\n";
+    }
+    o << "      }\n";
+    o << "      if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;\n";
+    o << "      const double part = wave_sum(lane_valid ? acc : 0.0);\n";
+    o << "      keep = (lane == j) ? part : keep;\n";
+    o << "    }\n";
+    o << "    const uint64_t a = (uint64_t)g * p.group + lane;\n";
+    o << "    if (lane < (uint32_t)p.group && a < p.chunk_count) p.chunk_out[a] = keep;\n";
+    o << "  }\n";
+    o << "}\n";
+    o << "}  // namespace sup\n";
+    return o.str();
+  }
+};
+
+const char* const kJitOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
+constexpr int kJitNopts = 4;
+
+uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+
+}  // namespace
+
+int build_seg(Plan& P) {
+  const int n = P.n, L = P.lay.L, m = P.lay.m;
+  if (m < 3) {
+    set_error("segmented walk needs >= 3 walk bits");
+    return SUP_EINVAL;
+  }
+  // rows are in first-touch order already: rebuild the shape in engine rows
+  P.touched.assign(m, {});
+  P.seg_start.assign(1, 0);
+  std::vector<char> seen(n, 0);
+  int R = 0;
+  for (int k = 0; k < m; ++k) {
+    const double* col = P.cols.data() + (size_t)(2 * (L + k)) * P.NP;
+    for (int j = 0; j < n; ++j)
+      if (col[j] != 0.0) {
+        P.touched[k].push_back(j);
+        if (!seen[j]) seen[j] = 1, ++R;
+      }
+    if (R > P.seg_start.back()) P.seg_start.push_back(R);
+  }
+  for (int j = 0; j < R; ++j)
+    if (!seen[j]) {
+      set_error("segmented walk: rows are not in first-touch order");
+      return SUP_EINVAL;
+    }
+  if (P.seg_start.size() < 2) {
+    set_error("segmented walk: no walk column has a nonzero");
+    return SUP_EINVAL;
+  }
+  P.seg_b = seg_static_bits(m);
+  P.dyn_rows.clear();
+  {
+    std::vector<char> in(n, 0);
+    for (int k = P.seg_b; k < m; ++k)
+      for (int r : P.touched[k]) in[r] = 1;
+    for (int j = 0; j < n; ++j)
+      if (in[j]) P.dyn_rows.push_back(j);
+  }
+  P.jofs.assign(m, 0);
+  P.jtab.clear();
+  for (int k = 0; k < m; ++k) {
+    const std::vector<int>& t = P.touched[k];
+    const size_t blk = (t.size() + 7) & ~(size_t)7;
+    P.jofs[k] = (int)P.jtab.size();
+    P.jtab.resize(P.jtab.size() + 2 * std::max<size_t>(blk, 8), 0.0);
+    for (size_t i = 0; i < t.size(); ++i) {
+      P.jtab[P.jofs[k] + i] = P.cols[(size_t)(2 * (L + k)) * P.NP + t[i]];
+      P.jtab[P.jofs[k] + blk + i] = P.cols[(size_t)(2 * (L + k) + 1) * P.NP + t[i]];
+    }
+  }
+  Gen g(P);
+  P.jit_src = g.source();
+  std::string key = P.jit_src;
+  for (int i = 0; i < kJitNopts; ++i) key += std::string("\n//") + kJitOpts[i];
+  key += std::string("\n//") + kWalkCommonSrc + kWalkParamsSrc;
+  P.jit_key = fnv1a(key);
+  return SUP_OK;
+}
+
+// ------------------------------------------------------ compile and cache --
+namespace {
+
+std::mutex g_jit_mu;
+std::map<uint64_t, std::shared_ptr<std::vector<char>>> g_code;        // key -> code object
+std::map<std::pair<int, uint64_t>, hipFunction_t> g_fn;               // (device, key) -> kernel
+std::map<std::pair<int, uint64_t>, int> g_occ;
+double g_compile_ms = 0.0;
+
+std::string cache_dir() {
+  const char* e = std::getenv("SUP_JIT_CACHE_DIR");
+  if (e) return e;  // "" disables
+  if (const char* x = std::getenv("XDG_CACHE_HOME")) return std::string(x) + "/superman_amd";
+  if (const char* h = std::getenv("HOME")) return std::string(h) + "/.cache/superman_amd";
+  return "";
+}
+
+std::string key_hex(uint64_t k) {
+  char b[32];
+  std::snprintf(b, sizeof b, "%016llx", (unsigned long long)k);
+  return b;
+}
+
+bool read_file(const std::string& path, std::vector<char>& out) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  const long sz = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  out.resize(sz > 0 ? (size_t)sz : 0);
+  const bool ok = sz > 0 && std::fread(out.data(), 1, out.size(), f) == out.size();
+  std::fclose(f);
+  return ok;
+}
+
+void write_file_atomic(const std::string& dir, const std::string& name, const std::vector<char>& data) {
+  std::string cur;
+  for (size_t i = 1; i <= dir.size(); ++i)  // mkdir -p
+    if (i == dir.size() || dir[i] == '/') {
+      cur = dir.substr(0, i);
+      ::mkdir(cur.c_str(), 0755);
+    }
+  const std::string tmp = dir + "/." + name + "." + std::to_string(::getpid());
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return;  // cache is best effort
+  const bool ok = std::fwrite(data.data(), 1, data.size(), f) == data.size();
+  std::fclose(f);
+  if (ok) std::rename(tmp.c_str(), (dir + "/" + name).c_str());
+  else std::remove(tmp.c_str());
+}
+
+int compile(const Plan& P, std::shared_ptr<std::vector<char>>& code) {
+  auto it = g_code.find(P.jit_key);
+  if (it != g_code.end()) {
+    code = it->second;
+    return SUP_OK;
+  }
+  const std::string dir = cache_dir();
+  const std::string name = "seg_" + key_hex(P.jit_key) + ".co";
+  auto co = std::make_shared<std::vector<char>>();
+  if (!dir.empty() && read_file(dir + "/" + name, *co)) {
+    g_code[P.jit_key] = co;
+    code = co;
+    return SUP_OK;
+  }
+  if (const char* d = std::getenv("SUP_JIT_DUMP")) {  // debugging: keep the generated source
+    FILE* f = std::fopen((std::string(d) + "/seg_" + key_hex(P.jit_key) + ".hip").c_str(), "w");
+    if (f) std::fputs(P.jit_src.c_str(), f), std::fclose(f);
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  hiprtcProgram prog;
+  const char* hdr[] = {kWalkCommonSrc, kWalkParamsSrc};
+  const char* names[] = {"walk_common.hpp", "walk_params.hpp"};
+  if (hiprtcCreateProgram(&prog, P.jit_src.c_str(), "sup_walk_seg.hip", 2, hdr, names) != HIPRTC_SUCCESS) {
+    set_error("hiprtcCreateProgram failed");
+    return SUP_EHIP;
+  }
+  const hiprtcResult cr = hiprtcCompileProgram(prog, kJitNopts, kJitOpts);
+  if (cr != HIPRTC_SUCCESS) {
+    size_t ls = 0;
+    hiprtcGetProgramLogSize(prog, &ls);
+    std::string log(ls, '\0');
+    if (ls) hiprtcGetProgramLog(prog, &log[0]);
+    hiprtcDestroyProgram(&prog);
+    set_error(std::string("hiprtc compile of the segmented walk failed: ") + hiprtcGetErrorString(cr) + "\n" +
+              log.substr(0, 2000));
+    return SUP_EHIP;
+  }
+  size_t cs = 0;
+  hiprtcGetCodeSize(prog, &cs);
+  co->resize(cs);
+  hiprtcGetCode(prog, co->data());
+  hiprtcDestroyProgram(&prog);
+  g_compile_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (!dir.empty()) write_file_atomic(dir, name, *co);
+  g_code[P.jit_key] = co;
+  code = co;
+  return SUP_OK;
+}
+
+int resolve(int dev, const Plan& P, hipFunction_t* fn) {
+  if (P.kind != kWalkSeg || P.jit_src.empty()) {
+    set_error("plan has no segmented-walk kernel");
+    return SUP_EINVAL;
+  }
+  std::lock_guard<std::mutex> g(g_jit_mu);
+  auto k = std::make_pair(dev, P.jit_key);
+  auto it = g_fn.find(k);
+  if (it != g_fn.end()) {
+    *fn = it->second;
+    return SUP_OK;
+  }
+  std::shared_ptr<std::vector<char>> code;
+  int rc = compile(P, code);
+  if (rc) return rc;
+  hipModule_t mod;
+  hipError_t e = hipModuleLoadData(&mod, code->data());
+  if (e != hipSuccess) {
+    set_error(std::string("hipModuleLoadData (segmented walk): ") + hipGetErrorString(e));
+    return SUP_EHIP;
+  }
+  if ((e = hipModuleGetFunction(fn, mod, "sup_walk_seg")) != hipSuccess) {
+    set_error(std::string("hipModuleGetFunction (segmented walk): ") + hipGetErrorString(e));
+    return SUP_EHIP;
+  }
+  g_fn[k] = *fn;  // modules live for the process (one per pattern and device)
+  return SUP_OK;
+}
+
+}  // namespace
+
+int jit_compile_only(const Plan& P, double* compile_ms) {
+  if (P.kind != kWalkSeg || P.jit_src.empty()) {
+    set_error("plan has no segmented-walk kernel");
+    return SUP_EINVAL;
+  }
+  const double before = jit_compile_ms_total();
+  std::shared_ptr<std::vector<char>> code;
+  int rc;
+  {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    rc = compile(P, code);
+  }
+  if (compile_ms) *compile_ms = jit_compile_ms_total() - before;
+  return rc;
+}
+
+int jit_occupancy(int dev, const Plan& P, int* blocks_per_cu, double* compile_ms) {
+  const double before = jit_compile_ms_total();
+  hipFunction_t fn;
+  int rc = resolve(dev, P, &fn);
+  if (rc) return rc;
+  if (compile_ms) *compile_ms = jit_compile_ms_total() - before;
+  std::lock_guard<std::mutex> g(g_jit_mu);
+  auto k = std::make_pair(dev, P.jit_key);
+  auto it = g_occ.find(k);
+  if (it != g_occ.end()) {
+    *blocks_per_cu = it->second;
+    return SUP_OK;
+  }
+  int b = 0;
+  hipError_t e = hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kBlock, 0);
+  if (e != hipSuccess) {
+    set_error(std::string("occupancy query (segmented walk): ") + hipGetErrorString(e));
+    return SUP_EHIP;
+  }
+  g_occ[k] = b > 0 ? b : 1;
+  *blocks_per_cu = g_occ[k];
+  return SUP_OK;
+}
+
+int jit_launch(int dev, const Plan& P, const WalkParams& p, int grid, hipStream_t s) {
+  hipFunction_t fn;
+  int rc = resolve(dev, P, &fn);
+  if (rc) return rc;
+  WalkParams arg = p;
+  void* args[] = {&arg};
+  hipError_t e = hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, kBlock, 1, 1, 0, s, args, nullptr);
+  if (e != hipSuccess) {
+    set_error(std::string("hipModuleLaunchKernel (segmented walk): ") + hipGetErrorString(e));
+    return SUP_EHIP;
+  }
+  return SUP_OK;
+}
+
+double jit_compile_ms_total() {
+  std::lock_guard<std::mutex> g(g_jit_mu);
+  return g_compile_ms;
+}
+
+}  // namespace sup

@@ -24,7 +24,9 @@ SUP_DECL_RANGE(skip, 33)
 SUP_DECL_RANGE(skip, 49)
 #undef SUP_DECL_RANGE
 
-enum WalkKind { kWalkDense = 0, kWalkSparse = 1, kWalkSkip = 2 };
+// kWalkSeg: the pattern-specialised segmented walk (jit.cpp), compiled at run
+// time with hiprtc for one matrix pattern; launched through hipModule APIs.
+enum WalkKind { kWalkDense = 0, kWalkSparse = 1, kWalkSkip = 2, kWalkSeg = 3 };
 
 // Launch the walk kernel of `kind` for matrix order n (1..64).
 hipError_t launch_walk(WalkKind kind, int n, const WalkParams& p, int grid, hipStream_t s);

@@ -63,6 +63,7 @@ hipError_t launch_walk(WalkKind kind, int n, const WalkParams& p, int grid, hipS
     case kWalkDense: { SUP_DISPATCH(dense, launch, n, p, grid, s) }
     case kWalkSparse: { SUP_DISPATCH(sparse, launch, n, p, grid, s) }
     case kWalkSkip: { SUP_DISPATCH(skip, launch, n, p, grid, s) }
+    case kWalkSeg: break;  // run-time specialised: jit_launch (jit.cpp)
   }
   return hipErrorInvalidValue;
 }
@@ -73,6 +74,7 @@ hipError_t walk_occupancy(WalkKind kind, int n, int* blocks_per_cu) {
     case kWalkDense: { SUP_DISPATCH(dense, occupancy, n, blocks_per_cu) }
     case kWalkSparse: { SUP_DISPATCH(sparse, occupancy, n, blocks_per_cu) }
     case kWalkSkip: { SUP_DISPATCH(skip, occupancy, n, blocks_per_cu) }
+    case kWalkSeg: break;  // jit_occupancy (jit.cpp)
   }
   return hipErrorInvalidValue;
 }

@@ -17,12 +17,21 @@
 // v_add_f64: no LDS traffic and no VALU address work on the hot loop.  X lives
 // in VGPRs (n fp64 values per lane).
 #pragma once
+// Also compiled by hiprtc for the pattern-specialised walk (jit.cpp), where
+// the HIP runtime header is implicit and <stdint.h> is not available.
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "walk_params.hpp"
 
 namespace sup {
+
+template <int V>
+struct Int {
+  static constexpr int value = V;
+};
 
 // Constant address space pointer: uniform loads through it become s_load.
 typedef const __attribute__((address_space(4))) double cdbl;
@@ -178,7 +187,7 @@ __device__ __forceinline__ void suffix_all(const double (&x)[N], double (&U)[Blo
 template <int B, int LO, class F>
 __device__ __forceinline__ void for_down(F&& f) {
   if constexpr (B >= LO) {
-    f(std::integral_constant<int, B>{});
+    f(Int<B>{});
     for_down<B - 1, LO>(f);
   }
 }

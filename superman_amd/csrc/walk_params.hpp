@@ -1,6 +1,11 @@
 // walk_params.hpp — launch parameters shared by host and the gfx950 walk kernels.
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <stdint.h>
+#else
+using __hip_internal::uint32_t;
+using __hip_internal::uint64_t;
+#endif
 
 namespace sup {
 
@@ -35,6 +40,9 @@ struct WalkParams {
   // resident wave (tail balance beats write coalescing).
   unsigned int group;
   unsigned int pad2_;
+  // segmented walk (jit.cpp): per walk bit, the values of the rows its column
+  // touches, packed (+ block, then - block, each padded to 8 doubles)
+  const double* jtab;
 };
 
 }  // namespace sup

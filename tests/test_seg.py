@@ -1,0 +1,78 @@
+"""Segmented walk on the CPU (no GPU needed): the host-thread walk of the
+pattern-specialised enumeration is bit-exact against the oracle's independent
+mirror (oracle/oracle.c kind 3); the planner picks it only where its cost model
+wins; and the generated HIP source compiles for gfx950 with hiprtc for shapes
+at the edges (n = 10 and 64, a zero walk column, no rest rows)."""
+import numpy as np
+import pytest
+
+from conftest import fixture_path, rel
+
+
+def _rand(n, d, seed, ints=True):
+    rng = np.random.default_rng(seed)
+    mask = rng.random((n, n)) < d
+    mask[np.arange(n), rng.permutation(n)] = True
+    vals = rng.integers(1, 6, (n, n)) if ints else rng.random((n, n)) * 5
+    return np.where(mask, vals, 0).astype(np.float64)
+
+
+@pytest.mark.parametrize("n,d,seed", [(10, 0.5, 1), (12, 0.3, 2), (14, 0.6, 3), (16, 0.2, 4), (17, 1.0, 5)])
+def test_cpu_seg_vs_mirror_and_exact(sup, orc, n, d, seed):
+    a = _rand(n, d, seed)
+    got = sup.perman_cpu(a, "seg", threads=4)
+    assert got == orc.engine_perman_as(sup, a, "seg", threads=4)
+    exact = float(orc.exact_perman(a))
+    assert abs(got - exact) <= 1e-12 * max(abs(exact), 1.0)
+
+
+def test_cpu_seg_corpus_vs_sparse(sup, orc):
+    a, _, _ = sup.read_matrix(fixture_path("synth/22_0.20_int"))
+    b = sup.skip_order(a)[0]
+    got = sup.perman_cpu(b, "seg", threads=8)
+    assert got == orc.engine_perman_as(sup, b, "seg", threads=8)
+    assert rel(got, sup.perman_cpu(b, "sparse", threads=8)) < 1e-12
+
+
+def test_planner_choice(sup):
+    a, _, _ = sup.read_matrix(fixture_path("double__40_0.50_0"))
+    assert sup.plan_info(a, "dense", jit=-1)["kind"] == "sparse"
+    assert sup.plan_info(a, "dense", jit=1)["kind"] == "seg"
+    # auto: the n = 40 walk saves ~0.1 s on one GPU, below the compile threshold
+    assert sup.plan_info(a, "dense", jit=0)["kind"] == "sparse"
+    b, _, _ = sup.read_matrix(fixture_path("synth44_0.15_int"))
+    b = sup.skip_order(b)[0]
+    assert sup.plan_info(b, "sparse", jit=0)["kind"] == "seg"  # 2^43 steps: worth compiling
+    assert sup.plan_info(b, "skip", jit=1)["kind"] == "skip"   # SkipPer is never replaced
+    # all-nonzero matrix: one segment holds every row; the segmented step is the
+    # plain step without its final multiply (2n ops instead of 2n + 1)
+    _, st = sup.perman_cpu(np.ones((12, 12)), "seg", threads=2, return_stats=True)
+    assert 23 <= st["est_ops_per_step"] <= 24  # 2n per step (truncated at the 2^-m walk tail)
+
+
+def test_seg_cost_model_reported(sup):
+    a, _, _ = sup.read_matrix(fixture_path("synth/22_0.20_int"))
+    _, st_seg = sup.perman_cpu(a, "seg", threads=4, return_stats=True)
+    _, st_blk = sup.perman_cpu(a, "sparse", threads=4, return_stats=True)
+    assert st_seg["walk_kind"] == 3 and st_blk["walk_kind"] == 1
+    assert 0 < st_seg["est_ops_per_step"] < st_blk["est_ops_per_step"]
+
+
+@pytest.mark.parametrize("case", ["n10", "n64", "zero_walk_col", "no_rest"])
+def test_generated_kernel_compiles(sup, case, tmp_path, monkeypatch):
+    monkeypatch.setenv("SUP_JIT_CACHE_DIR", str(tmp_path))
+    if case == "n10":
+        a = _rand(10, 0.5, 7)
+    elif case == "n64":
+        a = _rand(64, 0.1, 8, ints=False)
+    elif case == "zero_walk_col":
+        a = _rand(24, 0.3, 9)
+        a[:, 3] = 0.0  # a column with no nonzero: its steps only accumulate
+    else:
+        a = _rand(24, 0.9, 10)  # every row touched by the walk columns: no rest segment
+    info = sup.prepare(a, "seg")
+    assert info["kind"] == "seg"
+    assert info["compile_ms"] > 0.0
+    assert len(list(tmp_path.glob("seg_*.co"))) == 1  # disk cache written
+    again = sup.prepare(a, "seg")
+    assert again["compile_ms"] == 0.0  # in-memory cache

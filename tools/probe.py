@@ -18,7 +18,9 @@ print("n16 ok", flush=True)
 
 def run(label, m, kernel, reps=2):
     n = m.shape[0]
-    kind = {"dense": "dense", "dense_plain": "dense_plain", "sparse": "sparse", "skip": "skip"}[kernel]
+    kind = kernel
+    if kind == "seg":
+        print(f"  prepare: {S.prepare(m, 'seg')}", flush=True)
     S.perman_shard(m, 0, 1, kernel=kind)
     best = None
     for _ in range(reps):
@@ -44,20 +46,20 @@ for path, prep in (("double__32_0.50_0", 0), ("double__36_0.20_0", 1), ("double_
         m = S.sort_order(m)[0]
     if prep == 2:
         m = S.skip_order(m)[0]
-    for kernel in (("sparse", "skip") if m.shape[0] > 40 else
-                   ("dense_plain", "dense", "sparse") + (("skip",) if prep == 2 else ())):
+    for kernel in (("sparse", "seg", "skip") if m.shape[0] > 40 else
+                   ("dense_plain", "dense", "sparse", "seg") + (("skip",) if prep == 2 else ())):
         run(f"{path} r{prep}", m, kernel, reps=1 if m.shape[0] > 40 else 2)
 
 if only:
     sys.exit(0)
 # strong-scaling rehearsal on one GPU: the 8 shards of the n=40 bench, one by one
 m, _, _ = S.read_matrix("tests/fixtures/double__40_0.50_0")
-full = S.perman_shard(m, 0, 1)
+full = S.perman_shard(m, 0, 1, jit=1)
 parts, times = [], []
 for world in (2, 4, 8):
     parts, times = [], []
     for r in range(world):
-        v, st = S.perman_shard(m, r, world, return_stats=True)
+        v, st = S.perman_shard(m, r, world, return_stats=True, jit=1)
         parts.append(v)
         times.append(st["kernel_ms"])
     import math
