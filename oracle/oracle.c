@@ -464,16 +464,17 @@ static void engine_plan(const double* a, int n, int kind, const int* colmap, int
         if (P->col[2 * (L + k)][j] != 0.0 && !seen[j]) seen[j] = 1, ++R;
       if (R > P->seg[P->nseg]) P->seg[++P->nseg] = R;
     }
-    /* walk bits < segb = min(m, 5) get their own step (touched rows); bits
-     * >= segb share one step over the union of their rows (jit.cpp) */
-    P->segb = m < 5 ? m : 5;
-    for (int k = P->segb; k < m; ++k)
+    /* paired walk: pair steps flip walk bits k >= 1; bits k <= segb =
+     * min(m-1, 5) get their own step (touched rows), bits > segb share one
+     * step over the union of their rows (jit.cpp) */
+    P->segb = m - 1 < 5 ? m - 1 : 5;
+    for (int k = P->segb + 1; k < m; ++k)
       for (int j = 0; j < n; ++j)
         if (P->col[2 * (L + k)][j] != 0.0) P->dyn[j] = 1;
-    for (int k = 0; k < m; ++k) {
+    for (int k = 1; k < m; ++k) {
       P->smax[k] = -1;
       for (int j = 0; j < n; ++j)
-        if (k < P->segb ? P->col[2 * (L + k)][j] != 0.0 : P->dyn[j]) {
+        if (k <= P->segb ? P->col[2 * (L + k)][j] != 0.0 : P->dyn[j]) {
           int i = 0;
           while (P->seg[i + 1] <= j) ++i;
           P->dirty[k][i] = 1;
@@ -539,16 +540,33 @@ static void e_seg_chain(const eplan* P, const double* S, double R, double* U, in
   U[i] = i + 1 < P->nseg ? S[i] * U[i + 1] : (rest ? S[i] * R : S[i]);
 }
 
-/* one step of walk bit k: touched rows only, then dirty segments and the chain */
-static void e_seg_step(const eplan* P, double* x, double* S, double R, double* U, int k, int neg) {
+/* paired form: segment 0 (rows walk bit 0 touches) is held as x (bit 0
+ * clear) and y = x + a_0 (bit 0 set); D = prod_seg0 x - prod_seg0 y */
+static double e_seg_d(const eplan* P, const double* x, const double* y) {
+  return e_tree(x, 0, P->seg[1]) - e_tree(y, 0, P->seg[1]);
+}
+
+/* factor multiplying D: U1, else the rest product R, else 1 */
+static double e_seg_u1(const eplan* P, const double* U, double R) {
+  return P->nseg >= 2 ? U[1] : (P->seg[P->nseg] < P->n ? R : 1.0);
+}
+
+/* one pair step flipping walk bit k >= 1: its rows (both copies in segment
+ * 0), then dirty segments >= 1 and the chain, then D if segment 0 is dirty */
+static void e_seg_step(const eplan* P, double* x, double* y, double* S, double R, double* U, double* D, int k,
+                       int neg) {
   const double* c = P->col[2 * (P->L + k) + neg];
   if (P->smax[k] < 0) return;
   for (int j = 0; j < P->n; ++j)
-    if (k < P->segb ? c[j] != 0.0 : P->dyn[j]) x[j] += c[j];
-  for (int i = P->smax[k]; i >= 0; --i) {
+    if (k <= P->segb ? c[j] != 0.0 : P->dyn[j]) {
+      x[j] += c[j];
+      if (j < P->seg[1]) y[j] += c[j];
+    }
+  for (int i = P->smax[k]; i >= 1; --i) {
     if (P->dirty[k][i]) S[i] = e_tree(x, P->seg[i], P->seg[i + 1]);
     e_seg_chain(P, S, R, U, i);
   }
+  if (P->dirty[k][0]) *D = e_seg_d(P, x, y);
 }
 
 static double pair64(double* v) {
@@ -576,17 +594,20 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
       double x[ORC_MAXN], U[ORC_MAXN / 8 + 2], acc;
       e_start(P, ga, l, x);
       if (P->kind == 3) {
-        double S[ORC_MAXN], SU[ORC_MAXN + 1];
+        double S[ORC_MAXN], SU[ORC_MAXN + 1], y[ORC_MAXN], D;
+        for (int r = 0; r < P->seg[1]; ++r) y[r] = x[r] + P->col[2 * L][r];
         double R = P->seg[P->nseg] < n ? e_tree(x, P->seg[P->nseg], n) : 1.0;
-        for (int i = P->nseg - 1; i >= 0; --i) {
+        for (int i = P->nseg - 1; i >= 1; --i) {
           S[i] = e_tree(x, P->seg[i], P->seg[i + 1]);
           e_seg_chain(P, S, R, SU, i);
         }
-        acc = SU[0];
-        for (unsigned t = 1; t < T; ++t) {
-          unsigned k = __builtin_ctz(t), neg = (t >> (k + 1)) & 1u;
-          e_seg_step(P, x, S, R, SU, (int)k, (int)neg);
-          acc = (t & 1u) ? acc - SU[0] : acc + SU[0];
+        D = e_seg_d(P, x, y);
+        acc = D * e_seg_u1(P, SU, R);
+        /* pair j = Gray steps 2j, 2j+1: contributes (-1)^j D U1 */
+        for (unsigned j = 1; j < T / 2; ++j) {
+          unsigned pb = __builtin_ctz(j), neg = (j >> (pb + 1)) & 1u;
+          e_seg_step(P, x, y, S, R, SU, &D, (int)pb + 1, (int)neg);
+          acc = fma((j & 1u) ? -D : D, e_seg_u1(P, SU, R), acc);
         }
       } else if (P->kind == 0) {
         acc = e_prod4(x, n);

@@ -20,7 +20,7 @@ namespace {
 struct Lane {
   double x[SUP_MAX_N];
   double U[SUP_MAX_N / 8 + 2];
-  double S[SUP_MAX_N], SU[SUP_MAX_N + 1], R;  // segmented walk
+  double S[SUP_MAX_N], SU[SUP_MAX_N + 1], R, D, y[SUP_MAX_N];  // segmented walk
 };
 
 inline double prod4(const double* x, int n) {
@@ -99,16 +99,20 @@ double seg_tree(const double* x, int lo, int hi) {
   return seg_tree(x, lo, mid) * seg_tree(x, mid, hi);
 }
 
-// Walk bits k < seg_b: their own touched rows; bits >= seg_b: one shared step
-// over dyn_rows (the generated kernel's straight-line step for those bits).
+// Paired form: Gray steps 2j, 2j+1 differ in walk bit 0 only; segment 0 (the
+// rows walk bit 0 touches) is kept as x (bit 0 clear) and y = x + a_0, and the
+// pair adds (-1)^j (prod_seg0 x - prod_seg0 y) * U1.  Pair step j flips walk
+// bit k = ctz(j) + 1; walk bits k <= seg_b use their own touched rows, bits
+// > seg_b one shared step over dyn_rows (the generated kernel's straight-line
+// step for those bits).
 struct SegSteps {
   std::vector<int> smax;                  // deepest touched segment per walk bit (-1: none)
   std::vector<std::vector<char>> dirty;   // [k][segment]
   explicit SegSteps(const Plan& P) : smax(P.lay.m, -1), dirty(P.lay.m) {
     const int nseg = (int)P.seg_start.size() - 1;
-    for (int k = 0; k < P.lay.m; ++k) {
+    for (int k = 1; k < P.lay.m; ++k) {
       dirty[k].assign(nseg, 0);
-      for (int r : (k < P.seg_b ? P.touched[k] : P.dyn_rows)) {
+      for (int r : (k <= P.seg_b ? P.touched[k] : P.dyn_rows)) {
         int i = 0;
         while (P.seg_start[i + 1] <= r) ++i;
         dirty[k][i] = 1;
@@ -124,31 +128,51 @@ inline void seg_chain(Lane& s, const Plan& P, int i) {
   s.SU[i] = i + 1 < nseg ? s.S[i] * s.SU[i + 1] : (rest ? s.S[i] * s.R : s.S[i]);
 }
 
-void seg_init(Lane& s, const Plan& P) {
+// the factor multiplying D: U1, else R, else 1 (fma(D, 1, acc) == acc + D)
+inline double seg_u1(const Lane& s, const Plan& P) {
   const int nseg = (int)P.seg_start.size() - 1;
+  return nseg >= 2 ? s.SU[1] : (P.seg_start.back() < P.n ? s.R : 1.0);
+}
+
+inline double seg_d(const Lane& s, const Plan& P) {
+  return seg_tree(s.x, 0, P.seg_start[1]) - seg_tree(s.y, 0, P.seg_start[1]);
+}
+
+void seg_init(Lane& s, const Plan& P) {
+  const int nseg = (int)P.seg_start.size() - 1, len0 = P.seg_start[1];
+  for (int r = 0; r < len0; ++r) s.y[r] = s.x[r] + P.jtab[P.jofs[0] + r];
   s.R = P.seg_start.back() < P.n ? seg_tree(s.x, P.seg_start.back(), P.n) : 1.0;
-  for (int i = nseg - 1; i >= 0; --i) {
+  for (int i = nseg - 1; i >= 1; --i) {
     s.S[i] = seg_tree(s.x, P.seg_start[i], P.seg_start[i + 1]);
     seg_chain(s, P, i);
   }
+  s.D = seg_d(s, P);
 }
 
 void seg_step(Lane& s, const Plan& P, const SegSteps& st, int k, int neg) {
-  if (k >= P.seg_b) {  // shared step: full signed column over dyn_rows (zeros included)
+  const int len0 = P.seg_start[1];
+  if (k > P.seg_b) {  // shared step: full signed column over dyn_rows (zeros included)
     if (P.dyn_rows.empty()) return;
     const double* c = col_of(P, P.lay.L + k, neg);
-    for (int r : P.dyn_rows) s.x[r] += c[r];
+    for (int r : P.dyn_rows) {
+      s.x[r] += c[r];
+      if (r < len0) s.y[r] += c[r];
+    }
   } else {
     const std::vector<int>& t = P.touched[k];
     if (t.empty()) return;
     const size_t blk = (t.size() + 7) & ~(size_t)7;
     const double* v = P.jtab.data() + P.jofs[k] + (neg ? blk : 0);
-    for (size_t i = 0; i < t.size(); ++i) s.x[t[i]] += v[i];
+    for (size_t i = 0; i < t.size(); ++i) {
+      s.x[t[i]] += v[i];
+      if (t[i] < len0) s.y[t[i]] += v[i];
+    }
   }
-  for (int i = st.smax[k]; i >= 0; --i) {
+  for (int i = st.smax[k]; i >= 1; --i) {
     if (st.dirty[k][i]) s.S[i] = seg_tree(s.x, P.seg_start[i], P.seg_start[i + 1]);
     seg_chain(s, P, i);
   }
+  if (st.dirty[k][0]) s.D = seg_d(s, P);
 }
 
 // One wave-chunk: returns the wave's pairwise lane sum.
@@ -166,11 +190,11 @@ double chunk_partial(const Plan& P, uint64_t ga) {
       Lane s;
       chunk_start(P, ga, l, s);
       seg_init(s, P);
-      double acc = s.SU[0];
-      for (uint32_t t = 1; t < T; ++t) {
-        const uint32_t k = __builtin_ctz(t);
-        seg_step(s, P, st, (int)k, (t >> (k + 1)) & 1u);
-        acc = (t & 1u) ? acc - s.SU[0] : acc + s.SU[0];
+      double acc = s.D * seg_u1(s, P);
+      for (uint32_t j = 1; j < T / 2; ++j) {  // pair steps: walk bit ctz(j) + 1
+        const uint32_t pb = __builtin_ctz(j);
+        seg_step(s, P, st, (int)pb + 1, (j >> (pb + 1)) & 1u);
+        acc = std::fma((j & 1u) ? -s.D : s.D, seg_u1(s, P), acc);
       }
       const unsigned par = (unsigned)__builtin_popcount(l) & 1u;
       if ((((unsigned)ga) ^ par) & 1u) acc = -acc;

@@ -83,50 +83,57 @@ int seg_index(const std::vector<int>& seg_start, int row) {
   return (int)(std::upper_bound(seg_start.begin(), seg_start.end(), row) - seg_start.begin()) - 1;
 }
 
-// VALU ops of one step of walk bit k (the generated code, exactly): |touched|
-// adds; per segment i <= smax: (len_i - 1) muls when it holds a touched row,
-// one chain mul (none for the last segment when no rest rows exist); one
-// accumulate.
+// VALU ops of one pair step flipping a walk bit k >= 1 that touches rows t
+// (the generated code, exactly): |t| adds, plus one more per touched row of
+// segment 0 (its bit-0-set copy y); per segment i >= 1 up to the deepest
+// touched one: (len_i - 1) muls when it holds a touched row and one chain mul
+// (none for the last segment when no rest rows exist); segment 0, when
+// touched: both products and their difference, 2 (len_0 - 1) + 1; one fma
+// into the accumulator.
 double step_ops(const std::vector<int>& seg_start, int n, const std::vector<int>& t) {
   if (t.empty()) return 1.0;
   const int nseg = (int)seg_start.size() - 1;
   const bool rest = seg_start.back() < n;
   std::vector<char> dirty(nseg, 0);
   int smax = 0;
+  double ops = (double)t.size() + 1.0;
   for (int r : t) {
     const int i = seg_index(seg_start, r);
     dirty[i] = 1;
     smax = std::max(smax, i);
+    if (i == 0) ops += 1.0;
   }
-  double ops = (double)t.size() + 1.0;
-  for (int i = 0; i <= smax; ++i) {
+  if (dirty[0]) ops += 2.0 * (seg_start[1] - 1) + 1.0;
+  for (int i = 1; i <= smax; ++i) {
     if (dirty[i]) ops += seg_start[i + 1] - seg_start[i] - 1;
     if (i < nseg - 1 || rest) ops += 1.0;
   }
   return ops;
 }
 
-// Walk bits k < b get a specialised step each; bits k >= b (1/2^b of the
-// steps) share one step over the union of their rows.
+// Gray steps come in pairs that differ in walk bit 0 only, so a pair step
+// flips walk bit k >= 1 (pair bit k-1); pair bits p < b get a specialised
+// step each, bits p >= b (1/2^b of the pair steps) share one step over the
+// union of their rows.  Ops per Gray step = ops per pair step / 2.
 double cost_of(const std::vector<int>& seg_start, int n, const std::vector<std::vector<int>>& touched) {
   const int m = (int)touched.size(), b = seg_static_bits(m);
   std::vector<char> in(n, 0);
-  for (int k = b; k < m; ++k)
+  for (int k = b + 1; k < m; ++k)
     for (int r : touched[k]) in[r] = 1;
   std::vector<int> dyn;
   for (int j = 0; j < n; ++j)
     if (in[j]) dyn.push_back(j);
   const double dyn_ops = step_ops(seg_start, n, dyn);
   double c = 0.0, w = 0.5;
-  for (int k = 0; k < m; ++k, w *= 0.5) c += w * (k < b ? step_ops(seg_start, n, touched[k]) : dyn_ops);
-  return c;
+  for (int p = 0; p + 1 < m; ++p, w *= 0.5) c += w * (p < b ? step_ops(seg_start, n, touched[p + 1]) : dyn_ops);
+  return c / 2.0;
 }
 
 double shape_cost(const SegShape& s, int n) { return cost_of(s.seg_start, n, s.touched); }
 
 }  // namespace
 
-int seg_static_bits(int m) { return std::min(m, 5); }
+int seg_static_bits(int m) { return std::min(m - 1, 5); }
 
 double seg_walk_cost(const Plan& P) { return cost_of(P.seg_start, P.n, P.touched); }
 
@@ -158,7 +165,9 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count) {
     }
     return order;
   };
+  // walk bit 0 defines segment 0 (the paired rows): it must touch a row
   auto cost = [&](const std::vector<int>& o) {
+    if (nnz[o[0]] == 0) return 1e300;
     return shape_cost(seg_shape(A, n, std::vector<int>(o.begin(), o.begin() + m)), n);
   };
   std::vector<int> best;
@@ -193,18 +202,25 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count) {
 // ----------------------------------------------------------------- codegen --
 namespace {
 
-std::string tree(int lo, int hi) {
-  if (hi - lo == 1) return "x[" + std::to_string(lo) + "]";
+std::string tree(int lo, int hi, const char* v = "x") {
+  if (hi - lo == 1) return std::string(v) + "[" + std::to_string(lo) + "]";
   const int mid = lo + (hi - lo + 1) / 2;
-  return "(" + tree(lo, mid) + " * " + tree(mid, hi) + ")";
+  return "(" + tree(lo, mid, v) + " * " + tree(mid, hi, v) + ")";
 }
 
+// Generated kernel (paired segmented walk).  Gray steps 2j and 2j+1 differ in
+// walk bit 0 only, so they are evaluated together: segment 0 (the rows walk
+// bit 0 touches) is held twice, x (bit 0 clear) and y = x + a_0 (bit 0 set),
+// and the pair contributes (-1)^j (prod_seg0 x - prod_seg0 y) * U1, U1 being
+// the product of every other row.  The pair walk is a Gray walk over walk
+// bits 1..m-1 (pair bit p = walk bit p+1).
 struct Gen {
   const Plan& P;
-  int nseg;
+  int nseg, len0;
   bool rest;
   std::ostringstream o;
-  explicit Gen(const Plan& p) : P(p), nseg((int)p.seg_start.size() - 1), rest(p.seg_start.back() < p.n) {}
+  explicit Gen(const Plan& p)
+      : P(p), nseg((int)p.seg_start.size() - 1), len0(p.seg_start[1]), rest(p.seg_start.back() < p.n) {}
 
   int len(int i) const { return P.seg_start[i + 1] - P.seg_start[i]; }
   std::string S(int i) const { return len(i) == 1 ? "x[" + std::to_string(P.seg_start[i]) + "]" : "S" + std::to_string(i); }
@@ -212,11 +228,18 @@ struct Gen {
   std::string chain(int i) const {
     return (i + 1 < nseg || rest) ? S(i) + " * " + unext(i) : S(i);
   }
+  // the factor that multiplies D: U1, or R, or nothing
+  std::string ux() const { return nseg >= 2 ? "U1" : (rest ? "R" : ""); }
+  std::string dexpr() const { return tree(0, len0, "x") + " - " + tree(0, len0, "y"); }
+  void accumulate(bool neg, const char* ind) {
+    if (ux().empty()) o << ind << (neg ? "acc -= D;\n" : "acc += D;\n");
+    else o << ind << "acc = __builtin_fma(" << (neg ? "-D" : "D") << ", " << ux() << ", acc);\n";
+  }
 
-  // Add the values at table pointer `cv` (dbl8 pieces) to rows `rows`:
-  // value i of the block belongs to row rows[i] (packed table), or value
-  // rows[i] of the block (full column, `full`).  At most 2 pieces (32 SGPRs)
-  // are pinned at a time.
+  // Add the values at table pointer `cv` (dbl8 pieces) to rows `rows` (and
+  // to their y copies in segment 0): value i of the block belongs to row
+  // rows[i] (packed table), or value rows[i] of the block (full column,
+  // `full`).  At most 2 pieces (32 SGPRs) are pinned at a time.
   void adds(const std::vector<int>& rows, bool full, const char* ind) {
     std::vector<std::pair<int, int>> vr;  // (value index, row)
     for (size_t i = 0; i < rows.size(); ++i) vr.push_back({full ? rows[i] : (int)i, rows[i]});
@@ -230,8 +253,11 @@ struct Gen {
       for (size_t q = g; q < ge; ++q) o << (q > g ? ", " : " ") << "\"+s\"(v" << pieces[q] << ")";
       o << ");\n";
       for (auto& e : vr)
-        if (e.first / 8 >= pieces[g] && e.first / 8 <= pieces[ge - 1])
-          o << ind << "  x[" << e.second << "] += v" << e.first / 8 << "[" << e.first % 8 << "];\n";
+        if (e.first / 8 >= pieces[g] && e.first / 8 <= pieces[ge - 1]) {
+          const std::string v = "v" + std::to_string(e.first / 8) + "[" + std::to_string(e.first % 8) + "]";
+          o << ind << "  x[" << e.second << "] += " << v << ";\n";
+          if (e.second < len0) o << ind << "  y[" << e.second << "] += " << v << ";\n";
+        }
       if (ge < pieces.size()) o << ind << "  __builtin_amdgcn_sched_barrier(0);\n";
     }
   }
@@ -244,14 +270,15 @@ struct Gen {
       dirty[i] = 1;
       smax = std::max(smax, i);
     }
-    for (int i = smax; i >= 0; --i) {
+    for (int i = smax; i >= 1; --i) {
       if (dirty[i] && len(i) > 1)
         o << ind << "  S" << i << " = " << tree(P.seg_start[i], P.seg_start[i + 1]) << ";\n";
       o << ind << "  U" << i << " = " << chain(i) << ";\n";
     }
+    if (dirty[0]) o << ind << "  D = " << dexpr() << ";\n";
   }
 
-  // step of walk bit k < seg_b: packed touched values; `off` = byte offset expression
+  // pair step flipping walk bit k <= seg_b: packed touched values; `off` = byte offset expression
   void step(int k, const std::string& off, const char* ind) {
     const std::vector<int>& t = P.touched[k];
     if (t.empty()) return;
@@ -274,14 +301,24 @@ struct Gen {
   std::string source() {
     const int n = P.n, L = P.lay.L, m = P.lay.m, b = P.seg_b;
     const int R0 = P.seg_start.back();
-    const unsigned B = 1u << b, Q = 1u << (m - b);
-    o << "// generated by superman_amd jit.cpp: segmented Gray walk, n=" << n << " L=" << L << " m=" << m
-      << " segments=" << nseg << " static bits=" << b << "\n";
+    const unsigned B = 1u << b, Q = 1u << (m - 1 - b);
+    o << "// generated by superman_amd jit.cpp: paired segmented Gray walk, n=" << n << " L=" << L << " m=" << m
+      << " segments=" << nseg << " pair bits specialised=" << b << "\n";
     o << "#include \"walk_common.hpp\"\n";
     o << "namespace sup {\n";
     o << "typedef double jdbl8 __attribute__((ext_vector_type(8)));\n";
     o << "typedef const __attribute__((address_space(4))) jdbl8 cjdbl8;\n";
-    o << "extern \"C\" __global__ __launch_bounds__(kBlock) void sup_walk_seg(WalkParams p) {\n";
+    // occupancy target from the values live across the walk loop (x, y, S_i,
+    // U_i, D, acc, R, loop state; 2 VGPRs each): the default heuristic of the
+    // compiler trades occupancy 2 for scheduling freedom, which costs more
+    // latency hiding than it buys.  SUP_JIT_WAVES overrides (experiments).
+    int nS = 0;
+    for (int i = 1; i < nseg; ++i) nS += len(i) > 1;
+    const int live = 2 * (n + len0 + nS + nseg + 6);
+    int waves = live <= 116 ? 4 : (live <= 156 ? 3 : 2);
+    if (const char* e = std::getenv("SUP_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
+    o << "extern \"C\" __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(" << waves
+      << "))) void sup_walk_seg(WalkParams p) {\n";
     o << "  constexpr int N = " << n << ";\n";
     o << "  const uint32_t lane = threadIdx.x & 63u;\n";
     o << "  const bool lane_valid = lane < " << (1u << L) << "u;\n";
@@ -292,41 +329,47 @@ struct Gen {
     o << "      const uint64_t a = (uint64_t)g * p.group + j;\n";
     o << "      if (a >= p.chunk_count) break;\n";
     o << "      const uint64_t ga = p.chunk_begin + a;\n";
-    o << "      double x[N];\n";
+    o << "      double x[N], y[" << len0 << "];\n";
     o << "      chunk_start<N>(x, p, ga, lane);\n";
+    o << "      {\n";  // y = x + a_0 on segment 0 (the + block of walk bit 0)
+    o << "        cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off_const(0, 0) << ");\n";
+    for (int r = 0; r < len0; ++r) o << "        y[" << r << "] = x[" << r << "] + cv[" << r / 8 << "][" << r % 8 << "];\n";
+    o << "      }\n";
     if (rest) o << "      const double R = " << tree(R0, n) << ";\n";
-    for (int i = 0; i < nseg; ++i)
+    for (int i = 1; i < nseg; ++i)
       if (len(i) > 1) o << "      double S" << i << " = " << tree(P.seg_start[i], P.seg_start[i + 1]) << ";\n";
-    for (int i = nseg - 1; i >= 0; --i) o << "      double U" << i << " = " << chain(i) << ";\n";
-    o << "      double acc = U0;\n";
+    for (int i = nseg - 1; i >= 1; --i) o << "      double U" << i << " = " << chain(i) << ";\n";
+    o << "      double D = " << dexpr() << ";\n";
+    o << "      double acc = " << (ux().empty() ? std::string("D") : "D * " + ux()) << ";\n";
     o << "      for (uint32_t q = 0; q < " << Q << "u; ++q) {\n";
     const char* ind = "        ";
-    // t = B*q + s, s = 1 .. B-1: bit k = ctz(s); neg = (t >> (k+1)) & 1, which
-    // is bit k+1 of s for k < b-1 and bit 0 of q for k = b-1
+    // pair index j = B*q + s, s = 1 .. B-1: pair bit p = ctz(s) (walk bit p+1);
+    // neg = (j >> (p+1)) & 1 = bit p+1 of s for p < b-1, bit 0 of q for p = b-1
     for (unsigned st = 1; st < B; ++st) {
-      const int k = __builtin_ctz(st);
-      if (k < b - 1) {
-        step(k, off_const(k, (st >> (k + 1)) & 1u), ind);
+      const int pb = __builtin_ctz(st);
+      if (pb < b - 1) {
+        step(pb + 1, off_const(pb + 1, (st >> (pb + 1)) & 1u), ind);
       } else {
         o << ind << "{\n" << ind << "  const uint32_t ng = q & 1u;\n";
-        step(k, off_dyn(k, "ng"), "          ");
+        step(pb + 1, off_dyn(pb + 1, "ng"), "          ");
         o << ind << "}\n";
       }
-      o << ind << (st & 1u ? "acc -= U0;\n" : "acc += U0;\n");
+      accumulate(st & 1u, ind);
     }
-    if (m > b) {
-      // t = B(q+1): bit k = b + ctz(q+1) >= b, neg = ((q+1) >> (ctz(q+1)+1)) & 1.
-      // One straight-line step for all of them (no per-bit branches): the full
-      // signed column is added to every row some bit >= b touches (zeros
-      // elsewhere) and every segment such a row lies in is re-multiplied.
+    if (Q > 1) {
+      // j = B(q+1): pair bit b + ctz(q+1) (walk bit b+1+ctz(q+1)), neg =
+      // ((q+1) >> (ctz(q+1)+1)) & 1.  One straight-line step for all of them
+      // (no per-bit branches): the full signed column is added to every row
+      // some walk bit > b touches (zeros elsewhere) and every segment such a
+      // row lies in is re-multiplied.
       o << ind << "if (q + 1u < " << Q << "u) {\n";
       o << ind << "  const uint32_t kk = (uint32_t)__builtin_ctz(q + 1u);\n";
       o << ind << "  const uint32_t ng = ((q + 1u) >> (kk + 1u)) & 1u;\n";
-      o << ind << "  cjdbl8* cv = (cjdbl8*)opaque_c(p.cols, (2u * (" << (L + b) << "u + kk) + ng) * "
+      o << ind << "  cjdbl8* cv = (cjdbl8*)opaque_c(p.cols, (2u * (" << (L + b + 1) << "u + kk) + ng) * "
         << P.NP * 8 << "u);\n";
       adds(P.dyn_rows, true, ind);
       products(P.dyn_rows, ind);
-      o << ind << "  acc += U0;\n";
+      accumulate(false, "          ");
       o << ind << "}\n";
     }
     o << "      }\n";
@@ -359,6 +402,7 @@ int build_seg(Plan& P) {
     set_error("segmented walk needs >= 3 walk bits");
     return SUP_EINVAL;
   }
+  if (P.cols.empty()) return SUP_EINVAL;
   // rows are in first-touch order already: rebuild the shape in engine rows
   P.touched.assign(m, {});
   P.seg_start.assign(1, 0);
@@ -378,15 +422,15 @@ int build_seg(Plan& P) {
       set_error("segmented walk: rows are not in first-touch order");
       return SUP_EINVAL;
     }
-  if (P.seg_start.size() < 2) {
-    set_error("segmented walk: no walk column has a nonzero");
+  if (P.touched[0].empty()) {
+    set_error("segmented walk: walk column 0 has no nonzero");
     return SUP_EINVAL;
   }
   P.seg_b = seg_static_bits(m);
   P.dyn_rows.clear();
   {
     std::vector<char> in(n, 0);
-    for (int k = P.seg_b; k < m; ++k)
+    for (int k = P.seg_b + 1; k < m; ++k)
       for (int r : P.touched[k]) in[r] = 1;
     for (int j = 0; j < n; ++j)
       if (in[j]) P.dyn_rows.push_back(j);
