@@ -15,17 +15,27 @@
 //     suffix chain U_i = S_i * U_{i+1} down to U_0, the term.
 // Segments are the first-touch groups of the walk columns (rows walk bit k
 // touched first), so a step of walk bit k never goes deeper than segment k.
-// The cost model (seg_walk_cost) is ~37.5 fp64 ops per Gray step on the n=40
-// d=0.5 bench matrix against 45.5 for the 8-row blocks and 81 for the plain
-// dense walk; 10.1 against 21.5 on the n=36 d=0.2 SpaRyser config.
 //
-// The walk loop is unrolled by 8 Gray steps: steps t = 8q+1..8q+7 flip walk
-// bits 0,1,0,2,0,1,0 — bits 0 and 1 with compile-time signs (their table
-// address is a constant), bit 2 with sign q&1 — and t = 8q+8 flips bit
-// 3+ctz(q+1) through a switch.  Everything else (chunk start, lane layout,
-// wave-chunk queue, reduction order) is walk_common.hpp's, shared with the
-// ahead-of-time kernels, and the arithmetic is mirrored bit for bit by
-// engine_cpu.cpp (seg_*) and oracle/oracle.c (kind 3).
+// Paired form.  Gray steps 2j and 2j+1 differ in walk bit 0 only.  Segment 0
+// (the rows walk bit 0 touches) is held twice, x (bit 0 clear) and
+// y = x + a_0 (bit 0 set), and the pair contributes
+//   (-1)^j (prod_seg0 x - prod_seg0 y) * U1,    U1 = product of all other rows,
+// accumulated with one fma.  The walk is then a Gray walk over walk bits
+// 1..m-1 at half the step count; a step touching segment 0 updates both copies
+// and re-forms both products.  The loop is unrolled by 2^b pair steps
+// (b = seg_static_bits): pair bits below b get straight-line steps with
+// compile-time table offsets (the top one with sign q&1), and every higher
+// bit shares one straight-line step over the union of their rows (full signed
+// column, zeros included) — a switch over per-bit steps would make LLVM
+// carry copies of x across its arms (measured: 120 -> 242 VGPRs).
+//
+// Measured on MI355X (profiles/r1): n=40 d=0.5 bench matrix 29.4 VALU
+// instructions per Gray step (cost model 32.7; the prefix-blocked AOT walk
+// executes 46.6, the plain dense walk 81), VALU 99% busy, 1.26e12 steps/s.
+// Everything else (chunk start, lane layout, wave-chunk queue, reduction
+// order) is walk_common.hpp's, shared with the ahead-of-time kernels, and
+// the arithmetic is mirrored bit for bit by engine_cpu.cpp (seg_*) and
+// oracle/oracle.c (kind 3).
 //
 // Compiled code objects are cached in memory (per process, per device) and on
 // disk: $SUP_JIT_CACHE_DIR, else $XDG_CACHE_HOME/superman_amd, else
