@@ -387,9 +387,9 @@ typedef struct {
   double x0[ORC_MAXN];
   double col[2 * ORC_MAXN][ORC_MAXN]; /* [2e+neg][j] */
   /* segmented walk (kind 3): segment i = rows [seg[i], seg[i+1]), rest = [seg[nseg], n) */
-  int nseg, seg[ORC_MAXN + 1], smax[ORC_MAXN], segb;
-  char dirty[ORC_MAXN][ORC_MAXN]; /* [walk bit][segment] */
-  char dyn[ORC_MAXN];             /* rows some walk bit >= segb touches */
+  int nseg, seg[ORC_MAXN + 1], segb, len0;
+  int nsub, sub[ORC_MAXN + 1];    /* sub-segments of segment 0 */
+  char dyn[ORC_MAXN];             /* rows some walk bit > segb touches */
 } eplan;
 
 /* Layout: L = min(6, n-1); m = max(min(rest, 10), rest - 20); h = rest - m. */
@@ -430,6 +430,25 @@ static void engine_plan(const double* a, int n, int kind, const int* colmap, int
     }
     for (int i = 0; i < n; ++i)
       if (!placed[i]) P->rowperm[cnt++] = i;
+    if (kind == 3) {
+      /* segmented walk: the rows of walk column 0 first, ordered by first
+       * touch among walk columns 1.., the ones no other walk column touches
+       * last; then the other rows in first-touch order (jit.cpp seg_row_order) */
+      char pl[ORC_MAXN] = {0}, in0[ORC_MAXN] = {0};
+      int c0 = P->colmap[L];
+      cnt = 0;
+      for (int i = 0; i < n; ++i) in0[i] = a[i * n + c0] != 0.0;
+      for (int k = 1; k < m; ++k)
+        for (int i = 0; i < n; ++i)
+          if (in0[i] && !pl[i] && a[i * n + P->colmap[L + k]] != 0.0) pl[i] = 1, P->rowperm[cnt++] = i;
+      for (int i = 0; i < n; ++i)
+        if (in0[i] && !pl[i]) pl[i] = 1, P->rowperm[cnt++] = i;
+      for (int k = 1; k < m; ++k)
+        for (int i = 0; i < n; ++i)
+          if (!pl[i] && a[i * n + P->colmap[L + k]] != 0.0) pl[i] = 1, P->rowperm[cnt++] = i;
+      for (int i = 0; i < n; ++i)
+        if (!pl[i]) P->rowperm[cnt++] = i;
+    }
   }
   for (int e = 0; e < nb; ++e)
     if (e < L || e >= L + m) P->nblk[e] = (n + 7) / 8;
@@ -464,23 +483,24 @@ static void engine_plan(const double* a, int n, int kind, const int* colmap, int
         if (P->col[2 * (L + k)][j] != 0.0 && !seen[j]) seen[j] = 1, ++R;
       if (R > P->seg[P->nseg]) P->seg[++P->nseg] = R;
     }
-    /* paired walk: pair steps flip walk bits k >= 1; bits k <= segb =
-     * min(m-1, 5) get their own step (touched rows), bits > segb share one
-     * step over the union of their rows (jit.cpp) */
+    P->len0 = P->seg[1];
+    /* sub-segments of segment 0: first touch by walk bits 1.. */
+    char got[ORC_MAXN] = {0};
+    int c = 0;
+    P->nsub = 0;
+    P->sub[0] = 0;
+    for (int k = 1; k < m; ++k) {
+      for (int j = 0; j < P->len0; ++j)
+        if (P->col[2 * (L + k)][j] != 0.0 && !got[j]) got[j] = 1, ++c;
+      if (c > P->sub[P->nsub]) P->sub[++P->nsub] = c;
+    }
+    /* pair steps flip walk bits k >= 1; bits k <= segb = min(m-1, 5) get
+     * their own step (touched rows), bits > segb share one step over the
+     * union of their rows (jit.cpp) */
     P->segb = m - 1 < 5 ? m - 1 : 5;
     for (int k = P->segb + 1; k < m; ++k)
       for (int j = 0; j < n; ++j)
         if (P->col[2 * (L + k)][j] != 0.0) P->dyn[j] = 1;
-    for (int k = 1; k < m; ++k) {
-      P->smax[k] = -1;
-      for (int j = 0; j < n; ++j)
-        if (k <= P->segb ? P->col[2 * (L + k)][j] != 0.0 : P->dyn[j]) {
-          int i = 0;
-          while (P->seg[i + 1] <= j) ++i;
-          P->dirty[k][i] = 1;
-          if (i > P->smax[k]) P->smax[k] = i;
-        }
-    }
   }
 }
 
@@ -535,38 +555,73 @@ static double e_tree(const double* x, int lo, int hi) {
   return e_tree(x, lo, mid) * e_tree(x, mid, hi);
 }
 
-static void e_seg_chain(const eplan* P, const double* S, double R, double* U, int i) {
-  int rest = P->seg[P->nseg] < P->n;
-  U[i] = i + 1 < P->nseg ? S[i] * U[i + 1] : (rest ? S[i] * R : S[i]);
+/* a product chain over row ranges [lo_i, hi_i): segment products S_i (trees),
+ * U_i = S_i * U_{i+1}, the last closed by the constant tail product T (rows
+ * [tlo, thi)) when the tail is not empty */
+typedef struct {
+  int K, lo[ORC_MAXN], hi[ORC_MAXN], tlo, thi;
+} echain;
+typedef struct {
+  double S[ORC_MAXN], U[ORC_MAXN], T;
+} echv;
+
+static void e_link(const echain* c, echv* v, int i) {
+  if (i + 1 < c->K) v->U[i] = v->S[i] * v->U[i + 1];
+  else v->U[i] = c->thi > c->tlo ? v->S[i] * v->T : v->S[i];
+}
+static void e_chain_init(const echain* c, const double* a, echv* v) {
+  v->T = c->thi > c->tlo ? e_tree(a, c->tlo, c->thi) : 1.0;
+  for (int i = c->K - 1; i >= 0; --i) {
+    v->S[i] = e_tree(a, c->lo[i], c->hi[i]);
+    e_link(c, v, i);
+  }
+}
+static double e_chain_top(const echain* c, const echv* v) {
+  return c->K ? v->U[0] : (c->thi > c->tlo ? v->T : 1.0);
+}
+/* rows flagged in `rows` changed: re-form their segments, then the chain from
+ * the deepest one up; returns whether any segment of the chain changed */
+static int e_chain_update(const echain* c, const double* a, echv* v, const char* rows) {
+  int smax = -1;
+  char dirty[ORC_MAXN] = {0};
+  for (int i = 0; i < c->K; ++i)
+    for (int r = c->lo[i]; r < c->hi[i]; ++r)
+      if (rows[r]) dirty[i] = 1, smax = i;
+  for (int i = smax; i >= 0; --i) {
+    if (dirty[i]) v->S[i] = e_tree(a, c->lo[i], c->hi[i]);
+    e_link(c, v, i);
+  }
+  return smax >= 0;
 }
 
-/* paired form: segment 0 (rows walk bit 0 touches) is held as x (bit 0
- * clear) and y = x + a_0 (bit 0 set); D = prod_seg0 x - prod_seg0 y */
-static double e_seg_d(const eplan* P, const double* x, const double* y) {
-  return e_tree(x, 0, P->seg[1]) - e_tree(y, 0, P->seg[1]);
+static void e_seg_chains(const eplan* P, echain* outer, echain* inner) {
+  outer->K = 0;
+  for (int i = 1; i < P->nseg; ++i) outer->lo[outer->K] = P->seg[i], outer->hi[outer->K++] = P->seg[i + 1];
+  outer->tlo = P->seg[P->nseg], outer->thi = P->n;
+  inner->K = 0;
+  for (int i = 0; i < P->nsub; ++i) inner->lo[inner->K] = P->sub[i], inner->hi[inner->K++] = P->sub[i + 1];
+  inner->tlo = P->sub[P->nsub], inner->thi = P->len0;
 }
 
-/* factor multiplying D: U1, else the rest product R, else 1 */
-static double e_seg_u1(const eplan* P, const double* U, double R) {
-  return P->nseg >= 2 ? U[1] : (P->seg[P->nseg] < P->n ? R : 1.0);
-}
-
-/* one pair step flipping walk bit k >= 1: its rows (both copies in segment
- * 0), then dirty segments >= 1 and the chain, then D if segment 0 is dirty */
-static void e_seg_step(const eplan* P, double* x, double* y, double* S, double R, double* U, double* D, int k,
-                       int neg) {
+/* one pair step flipping walk bit k >= 1: its rows (x, and y on segment 0),
+ * the outer chain, and segment 0's chains over x and y with D = top_x - top_y */
+static void e_seg_step(const eplan* P, const echain* outer, const echain* inner, double* x, double* y, echv* vo,
+                       echv* vx, echv* vy, double* D, int k, int neg) {
   const double* c = P->col[2 * (P->L + k) + neg];
-  if (P->smax[k] < 0) return;
+  char rows[ORC_MAXN] = {0};
+  int any = 0;
   for (int j = 0; j < P->n; ++j)
     if (k <= P->segb ? c[j] != 0.0 : P->dyn[j]) {
       x[j] += c[j];
-      if (j < P->seg[1]) y[j] += c[j];
+      if (j < P->len0) y[j] += c[j];
+      rows[j] = 1, any = 1;
     }
-  for (int i = P->smax[k]; i >= 1; --i) {
-    if (P->dirty[k][i]) S[i] = e_tree(x, P->seg[i], P->seg[i + 1]);
-    e_seg_chain(P, S, R, U, i);
+  if (!any) return;
+  e_chain_update(outer, x, vo, rows);
+  if (e_chain_update(inner, x, vx, rows)) {
+    e_chain_update(inner, y, vy, rows);
+    *D = e_chain_top(inner, vx) - e_chain_top(inner, vy);
   }
-  if (P->dirty[k][0]) *D = e_seg_d(P, x, y);
 }
 
 static double pair64(double* v) {
@@ -594,20 +649,21 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
       double x[ORC_MAXN], U[ORC_MAXN / 8 + 2], acc;
       e_start(P, ga, l, x);
       if (P->kind == 3) {
-        double S[ORC_MAXN], SU[ORC_MAXN + 1], y[ORC_MAXN], D;
-        for (int r = 0; r < P->seg[1]; ++r) y[r] = x[r] + P->col[2 * L][r];
-        double R = P->seg[P->nseg] < n ? e_tree(x, P->seg[P->nseg], n) : 1.0;
-        for (int i = P->nseg - 1; i >= 1; --i) {
-          S[i] = e_tree(x, P->seg[i], P->seg[i + 1]);
-          e_seg_chain(P, S, R, SU, i);
-        }
-        D = e_seg_d(P, x, y);
-        acc = D * e_seg_u1(P, SU, R);
+        static __thread echv vo, vx, vy;
+        echain outer, inner;
+        double y[ORC_MAXN], D;
+        e_seg_chains(P, &outer, &inner);
+        for (int r = 0; r < P->len0; ++r) y[r] = x[r] + P->col[2 * L][r];
+        e_chain_init(&outer, x, &vo);
+        e_chain_init(&inner, x, &vx);
+        e_chain_init(&inner, y, &vy);
+        D = e_chain_top(&inner, &vx) - e_chain_top(&inner, &vy);
+        acc = D * e_chain_top(&outer, &vo);
         /* pair j = Gray steps 2j, 2j+1: contributes (-1)^j D U1 */
         for (unsigned j = 1; j < T / 2; ++j) {
           unsigned pb = __builtin_ctz(j), neg = (j >> (pb + 1)) & 1u;
-          e_seg_step(P, x, y, S, R, SU, &D, (int)pb + 1, (int)neg);
-          acc = fma((j & 1u) ? -D : D, e_seg_u1(P, SU, R), acc);
+          e_seg_step(P, &outer, &inner, x, y, &vo, &vx, &vy, &D, (int)pb + 1, (int)neg);
+          acc = fma((j & 1u) ? -D : D, e_chain_top(&outer, &vo), acc);
         }
       } else if (P->kind == 0) {
         acc = e_prod4(x, n);

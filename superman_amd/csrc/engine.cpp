@@ -198,6 +198,11 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
     for (int i = 0; i < n; ++i)
       if (!placed[i]) order.push_back(i);
     P.rowperm = order;
+    if (kind == kWalkSeg) {  // segment 0 sub-ordered (jit.cpp)
+      std::vector<int> walk(m);
+      for (int k = 0; k < m; ++k) walk[k] = P.colmap[L + k];
+      P.rowperm = seg_row_order(A, n, walk);
+    }
     // a walk column may touch no new row: nblk must still cover its own rows,
     // which are all inside the prefix, so the prefix count above is correct.
   }

@@ -54,7 +54,9 @@ struct Plan {
   // touches.  touched[k] = engine rows with a nonzero in walk bit k.
   std::vector<int> seg_start;
   std::vector<std::vector<int>> touched;
-  int seg_b = 0;                   // walk bits [0, seg_b) have specialised steps (seg_static_bits)
+  std::vector<int> sub_start;      // sub-segments of segment 0 (first touch by walk bits >= 1);
+                                   // rows [sub_start.back(), seg_start[1]) are constant per chunk
+  int seg_b = 0;                   // pair bits [0, seg_b) have specialised steps (seg_static_bits)
   std::vector<int> dyn_rows;       // rows touched by walk bits >= seg_b (their shared step)
   std::vector<int> jofs;           // [m] offset (doubles) of walk bit k's + block in jtab
   std::vector<double> jtab;        // packed touched values: + block, - block (each padded to 8)
@@ -74,6 +76,10 @@ std::vector<int> greedy_walk_order(const double* A, int n, int count);
 // Walk-column order for the segmented walk: greedy starts from every column,
 // then pairwise-swap descent on seg_cost (first `count` columns returned).
 std::vector<int> seg_walk_order(const double* A, int n, int m, int count);
+// Engine row order of the segmented walk for walk columns `walk`: rows in
+// first-touch order, segment 0 (the rows of walk[0]) internally ordered by
+// first touch among walk[1..], its rows no other walk column touches last.
+std::vector<int> seg_row_order(const double* A, int n, const std::vector<int>& walk);
 // Fill the segment structure, packed table and generated source of a plan
 // whose rows are already in first-touch order (make_plan, kind kWalkSeg).
 int build_seg(Plan& P);

@@ -20,7 +20,6 @@ namespace {
 struct Lane {
   double x[SUP_MAX_N];
   double U[SUP_MAX_N / 8 + 2];
-  double S[SUP_MAX_N], SU[SUP_MAX_N + 1], R, D, y[SUP_MAX_N];  // segmented walk
 };
 
 inline double prod4(const double* x, int n) {
@@ -99,64 +98,95 @@ double seg_tree(const double* x, int lo, int hi) {
   return seg_tree(x, lo, mid) * seg_tree(x, mid, hi);
 }
 
+// Product chain over row ranges (jit.cpp Chain): segment products (trees),
+// suffix products U_i = S_i * U_{i+1}, constant tail T closing the chain.
+struct ChainDef {
+  std::vector<std::pair<int, int>> segs;
+  int tail_lo = 0, tail_hi = 0;
+  bool tail() const { return tail_hi > tail_lo; }
+  int K() const { return (int)segs.size(); }
+  int index(int r) const {
+    for (int i = 0; i < K(); ++i)
+      if (r >= segs[i].first && r < segs[i].second) return i;
+    return -1;
+  }
+};
+struct ChainVal {
+  double S[SUP_MAX_N], U[SUP_MAX_N], T;
+};
+
+inline void chain_link(const ChainDef& c, ChainVal& v, int i) {
+  v.U[i] = i + 1 < c.K() ? v.S[i] * v.U[i + 1] : (c.tail() ? v.S[i] * v.T : v.S[i]);
+}
+void chain_init(const ChainDef& c, const double* a, ChainVal& v) {
+  v.T = c.tail() ? seg_tree(a, c.tail_lo, c.tail_hi) : 1.0;
+  for (int i = c.K() - 1; i >= 0; --i) {
+    v.S[i] = seg_tree(a, c.segs[i].first, c.segs[i].second);
+    chain_link(c, v, i);
+  }
+}
+// the chain's product: U_0, else the tail, else none (1: fma(D, 1, acc) == acc + D)
+inline double chain_top(const ChainDef& c, const ChainVal& v) { return c.K() ? v.U[0] : (c.tail() ? v.T : 1.0); }
+
 // Paired form: Gray steps 2j, 2j+1 differ in walk bit 0 only; segment 0 (the
 // rows walk bit 0 touches) is kept as x (bit 0 clear) and y = x + a_0, and the
-// pair adds (-1)^j (prod_seg0 x - prod_seg0 y) * U1.  Pair step j flips walk
-// bit k = ctz(j) + 1; walk bits k <= seg_b use their own touched rows, bits
-// > seg_b one shared step over dyn_rows (the generated kernel's straight-line
-// step for those bits).
+// pair adds (-1)^j (prod_seg0 x - prod_seg0 y) * U1 (U1 = outer chain over the
+// other rows; segment 0's products are sub-segment chains over x and y).
+// Pair step j flips walk bit k = ctz(j) + 1; walk bits k <= seg_b use their
+// own touched rows, bits > seg_b one shared step over dyn_rows (the generated
+// kernel's straight-line step for those bits).
 struct SegSteps {
-  std::vector<int> smax;                  // deepest touched segment per walk bit (-1: none)
-  std::vector<std::vector<char>> dirty;   // [k][segment]
-  explicit SegSteps(const Plan& P) : smax(P.lay.m, -1), dirty(P.lay.m) {
-    const int nseg = (int)P.seg_start.size() - 1;
+  ChainDef outer, inner;
+  std::vector<std::vector<char>> odirty, idirty;  // [k][q]: segment smax-q dirty
+  std::vector<int> omax, imax;
+  explicit SegSteps(const Plan& P) : odirty(P.lay.m), idirty(P.lay.m), omax(P.lay.m, -1), imax(P.lay.m, -1) {
+    const int nseg = (int)P.seg_start.size() - 1, len0 = P.seg_start[1];
+    for (int i = 1; i < nseg; ++i) outer.segs.push_back({P.seg_start[i], P.seg_start[i + 1]});
+    outer.tail_lo = P.seg_start.back(), outer.tail_hi = P.n;
+    for (size_t i = 0; i + 1 < P.sub_start.size(); ++i) inner.segs.push_back({P.sub_start[i], P.sub_start[i + 1]});
+    inner.tail_lo = P.sub_start.back(), inner.tail_hi = len0;
     for (int k = 1; k < P.lay.m; ++k) {
-      dirty[k].assign(nseg, 0);
+      std::vector<char> od(std::max(outer.K(), 1), 0), id(std::max(inner.K(), 1), 0);
       for (int r : (k <= P.seg_b ? P.touched[k] : P.dyn_rows)) {
-        int i = 0;
-        while (P.seg_start[i + 1] <= r) ++i;
-        dirty[k][i] = 1;
-        smax[k] = std::max(smax[k], i);
+        const int io = outer.index(r), ii = inner.index(r);
+        if (io >= 0) od[io] = 1, omax[k] = std::max(omax[k], io);
+        if (ii >= 0) id[ii] = 1, imax[k] = std::max(imax[k], ii);
       }
+      for (int i = omax[k]; i >= 0; --i) odirty[k].push_back(od[i]);
+      for (int i = imax[k]; i >= 0; --i) idirty[k].push_back(id[i]);
     }
   }
 };
 
-inline void seg_chain(Lane& s, const Plan& P, int i) {
-  const int nseg = (int)P.seg_start.size() - 1;
-  const bool rest = P.seg_start.back() < P.n;
-  s.SU[i] = i + 1 < nseg ? s.S[i] * s.SU[i + 1] : (rest ? s.S[i] * s.R : s.S[i]);
-}
+struct SegLane {
+  double y[SUP_MAX_N], D;
+  ChainVal o, ix, iy;
+};
 
-// the factor multiplying D: U1, else R, else 1 (fma(D, 1, acc) == acc + D)
-inline double seg_u1(const Lane& s, const Plan& P) {
-  const int nseg = (int)P.seg_start.size() - 1;
-  return nseg >= 2 ? s.SU[1] : (P.seg_start.back() < P.n ? s.R : 1.0);
-}
-
-inline double seg_d(const Lane& s, const Plan& P) {
-  return seg_tree(s.x, 0, P.seg_start[1]) - seg_tree(s.y, 0, P.seg_start[1]);
-}
-
-void seg_init(Lane& s, const Plan& P) {
-  const int nseg = (int)P.seg_start.size() - 1, len0 = P.seg_start[1];
-  for (int r = 0; r < len0; ++r) s.y[r] = s.x[r] + P.jtab[P.jofs[0] + r];
-  s.R = P.seg_start.back() < P.n ? seg_tree(s.x, P.seg_start.back(), P.n) : 1.0;
-  for (int i = nseg - 1; i >= 1; --i) {
-    s.S[i] = seg_tree(s.x, P.seg_start[i], P.seg_start[i + 1]);
-    seg_chain(s, P, i);
+inline void chain_update(const ChainDef& c, const double* a, ChainVal& v, int smax, const std::vector<char>& dirty) {
+  for (int i = smax, q = 0; i >= 0; --i, ++q) {
+    if (dirty[q]) v.S[i] = seg_tree(a, c.segs[i].first, c.segs[i].second);
+    chain_link(c, v, i);
   }
-  s.D = seg_d(s, P);
 }
 
-void seg_step(Lane& s, const Plan& P, const SegSteps& st, int k, int neg) {
+void seg_init(Lane& s, SegLane& g, const Plan& P, const SegSteps& st) {
+  const int len0 = P.seg_start[1];
+  for (int r = 0; r < len0; ++r) g.y[r] = s.x[r] + P.jtab[P.jofs[0] + r];
+  chain_init(st.outer, s.x, g.o);
+  chain_init(st.inner, s.x, g.ix);
+  chain_init(st.inner, g.y, g.iy);
+  g.D = chain_top(st.inner, g.ix) - chain_top(st.inner, g.iy);
+}
+
+void seg_step(Lane& s, SegLane& g, const Plan& P, const SegSteps& st, int k, int neg) {
   const int len0 = P.seg_start[1];
   if (k > P.seg_b) {  // shared step: full signed column over dyn_rows (zeros included)
     if (P.dyn_rows.empty()) return;
     const double* c = col_of(P, P.lay.L + k, neg);
     for (int r : P.dyn_rows) {
       s.x[r] += c[r];
-      if (r < len0) s.y[r] += c[r];
+      if (r < len0) g.y[r] += c[r];
     }
   } else {
     const std::vector<int>& t = P.touched[k];
@@ -165,14 +195,15 @@ void seg_step(Lane& s, const Plan& P, const SegSteps& st, int k, int neg) {
     const double* v = P.jtab.data() + P.jofs[k] + (neg ? blk : 0);
     for (size_t i = 0; i < t.size(); ++i) {
       s.x[t[i]] += v[i];
-      if (t[i] < len0) s.y[t[i]] += v[i];
+      if (t[i] < len0) g.y[t[i]] += v[i];
     }
   }
-  for (int i = st.smax[k]; i >= 1; --i) {
-    if (st.dirty[k][i]) s.S[i] = seg_tree(s.x, P.seg_start[i], P.seg_start[i + 1]);
-    seg_chain(s, P, i);
+  chain_update(st.outer, s.x, g.o, st.omax[k], st.odirty[k]);
+  if (st.imax[k] >= 0) {
+    chain_update(st.inner, s.x, g.ix, st.imax[k], st.idirty[k]);
+    chain_update(st.inner, g.y, g.iy, st.imax[k], st.idirty[k]);
+    g.D = chain_top(st.inner, g.ix) - chain_top(st.inner, g.iy);
   }
-  if (st.dirty[k][0]) s.D = seg_d(s, P);
 }
 
 // One wave-chunk: returns the wave's pairwise lane sum.
@@ -189,12 +220,13 @@ double chunk_partial(const Plan& P, uint64_t ga) {
       }
       Lane s;
       chunk_start(P, ga, l, s);
-      seg_init(s, P);
-      double acc = s.D * seg_u1(s, P);
+      static thread_local SegLane g;
+      seg_init(s, g, P, st);
+      double acc = g.D * chain_top(st.outer, g.o);
       for (uint32_t j = 1; j < T / 2; ++j) {  // pair steps: walk bit ctz(j) + 1
         const uint32_t pb = __builtin_ctz(j);
-        seg_step(s, P, st, (int)pb + 1, (j >> (pb + 1)) & 1u);
-        acc = std::fma((j & 1u) ? -s.D : s.D, seg_u1(s, P), acc);
+        seg_step(s, g, P, st, (int)pb + 1, (j >> (pb + 1)) & 1u);
+        acc = std::fma((j & 1u) ? -g.D : g.D, chain_top(st.outer, g.o), acc);
       }
       const unsigned par = (unsigned)__builtin_popcount(l) & 1u;
       if ((((unsigned)ga) ^ par) & 1u) acc = -acc;

@@ -93,31 +93,70 @@ int seg_index(const std::vector<int>& seg_start, int row) {
   return (int)(std::upper_bound(seg_start.begin(), seg_start.end(), row) - seg_start.begin()) - 1;
 }
 
+// Segment 0 is split the same way as the whole matrix: its rows are ordered
+// by the first walk bit >= 1 that touches them (sub-segments), rows no such
+// bit touches last (constant within a wave-chunk).  Sub-segment of each
+// segment-0 row, -1 for the constant ones; *nsub, *srest = counts.
+std::vector<int> sub_of(const std::vector<int>& seg_start, const std::vector<std::vector<int>>& touched, int* nsub,
+                        int* srest) {
+  const int len0 = seg_start[1];
+  std::vector<int> sub(len0, -1);
+  int cnt = 0, ns = 0;
+  for (size_t k = 1; k < touched.size(); ++k) {
+    bool grew = false;
+    for (int r : touched[k])
+      if (r < len0 && sub[r] < 0) sub[r] = ns, ++cnt, grew = true;
+    if (grew) ++ns;
+  }
+  *nsub = ns;
+  *srest = len0 - cnt;
+  return sub;
+}
+
+// Ops of one chain update (segments of sizes len[], constant tail present or
+// not) for dirty segments `dirty` up to `smax`: (len - 1) muls per dirty
+// segment of the tree, one chain mul per segment (none for the last one
+// without a tail).
+double chain_ops(const std::vector<int>& len, bool tail, const std::vector<char>& dirty, int smax) {
+  double ops = 0.0;
+  const int ns = (int)len.size();
+  for (int i = 0; i <= smax; ++i) {
+    if (dirty[i]) ops += len[i] - 1;
+    if (i < ns - 1 || tail) ops += 1.0;
+  }
+  return ops;
+}
+
 // VALU ops of one pair step flipping a walk bit k >= 1 that touches rows t
 // (the generated code, exactly): |t| adds, plus one more per touched row of
-// segment 0 (its bit-0-set copy y); per segment i >= 1 up to the deepest
-// touched one: (len_i - 1) muls when it holds a touched row and one chain mul
-// (none for the last segment when no rest rows exist); segment 0, when
-// touched: both products and their difference, 2 (len_0 - 1) + 1; one fma
-// into the accumulator.
-double step_ops(const std::vector<int>& seg_start, int n, const std::vector<int>& t) {
+// segment 0 (its bit-0-set copy y); the outer chain over segments >= 1; when
+// segment 0 is touched, its sub-segment chains for x and for y and their
+// difference D; one fma into the accumulator.
+double step_ops(const std::vector<int>& seg_start, int n, const std::vector<int>& t, const std::vector<int>& sub,
+                int nsub, int srest) {
   if (t.empty()) return 1.0;
-  const int nseg = (int)seg_start.size() - 1;
-  const bool rest = seg_start.back() < n;
-  std::vector<char> dirty(nseg, 0);
-  int smax = 0;
+  const int nseg = (int)seg_start.size() - 1, len0 = seg_start[1];
+  std::vector<int> olen;
+  for (int i = 1; i < nseg; ++i) olen.push_back(seg_start[i + 1] - seg_start[i]);
+  std::vector<int> slen(nsub, 0);
+  for (int r = 0; r < len0; ++r)
+    if (sub[r] >= 0) ++slen[sub[r]];
+  std::vector<char> od(std::max(nseg - 1, 1), 0), sd(std::max(nsub, 1), 0);
+  int omax = -1, smax = -1;
   double ops = (double)t.size() + 1.0;
   for (int r : t) {
-    const int i = seg_index(seg_start, r);
-    dirty[i] = 1;
-    smax = std::max(smax, i);
-    if (i == 0) ops += 1.0;
+    if (r < len0) {
+      ops += 1.0;
+      sd[sub[r]] = 1;
+      smax = std::max(smax, sub[r]);
+    } else {
+      const int i = seg_index(seg_start, r) - 1;
+      od[i] = 1;
+      omax = std::max(omax, i);
+    }
   }
-  if (dirty[0]) ops += 2.0 * (seg_start[1] - 1) + 1.0;
-  for (int i = 1; i <= smax; ++i) {
-    if (dirty[i]) ops += seg_start[i + 1] - seg_start[i] - 1;
-    if (i < nseg - 1 || rest) ops += 1.0;
-  }
+  if (omax >= 0) ops += chain_ops(olen, seg_start.back() < n, od, omax);
+  if (smax >= 0) ops += 2.0 * chain_ops(slen, srest > 0, sd, smax) + 1.0;
   return ops;
 }
 
@@ -127,15 +166,18 @@ double step_ops(const std::vector<int>& seg_start, int n, const std::vector<int>
 // union of their rows.  Ops per Gray step = ops per pair step / 2.
 double cost_of(const std::vector<int>& seg_start, int n, const std::vector<std::vector<int>>& touched) {
   const int m = (int)touched.size(), b = seg_static_bits(m);
+  int nsub = 0, srest = 0;
+  const std::vector<int> sub = sub_of(seg_start, touched, &nsub, &srest);
   std::vector<char> in(n, 0);
   for (int k = b + 1; k < m; ++k)
     for (int r : touched[k]) in[r] = 1;
   std::vector<int> dyn;
   for (int j = 0; j < n; ++j)
     if (in[j]) dyn.push_back(j);
-  const double dyn_ops = step_ops(seg_start, n, dyn);
+  const double dyn_ops = step_ops(seg_start, n, dyn, sub, nsub, srest);
   double c = 0.0, w = 0.5;
-  for (int p = 0; p + 1 < m; ++p, w *= 0.5) c += w * (p < b ? step_ops(seg_start, n, touched[p + 1]) : dyn_ops);
+  for (int p = 0; p + 1 < m; ++p, w *= 0.5)
+    c += w * (p < b ? step_ops(seg_start, n, touched[p + 1], sub, nsub, srest) : dyn_ops);
   return c / 2.0;
 }
 
@@ -209,6 +251,23 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count) {
   return extend(best, count);
 }
 
+std::vector<int> seg_row_order(const double* A, int n, const std::vector<int>& walk) {
+  std::vector<int> order;
+  std::vector<char> placed(n, 0), in0(n, 0);
+  for (int i = 0; i < n; ++i) in0[i] = !walk.empty() && A[(size_t)i * n + walk[0]] != 0.0;
+  for (size_t k = 1; k < walk.size(); ++k)  // segment 0, by first touch among walk[1..]
+    for (int i = 0; i < n; ++i)
+      if (in0[i] && !placed[i] && A[(size_t)i * n + walk[k]] != 0.0) placed[i] = 1, order.push_back(i);
+  for (int i = 0; i < n; ++i)
+    if (in0[i] && !placed[i]) placed[i] = 1, order.push_back(i);
+  for (size_t k = 1; k < walk.size(); ++k)  // the other segments
+    for (int i = 0; i < n; ++i)
+      if (!placed[i] && A[(size_t)i * n + walk[k]] != 0.0) placed[i] = 1, order.push_back(i);
+  for (int i = 0; i < n; ++i)
+    if (!placed[i]) order.push_back(i);
+  return order;
+}
+
 // ----------------------------------------------------------------- codegen --
 namespace {
 
@@ -218,6 +277,32 @@ std::string tree(int lo, int hi, const char* v = "x") {
   return "(" + tree(lo, mid, v) + " * " + tree(mid, hi, v) + ")";
 }
 
+// A product chain over row ranges: segment products S_i (trees), suffix
+// products U_i = S_i * U_{i+1}, and a constant tail T (rows no walk bit >= 1
+// touches) closing the chain.  Used for the rows outside segment 0 (over x)
+// and for the sub-segments of segment 0 (once over x, once over y).
+struct Chain {
+  std::vector<std::pair<int, int>> segs;  // row ranges [lo, hi)
+  int tail_lo = 0, tail_hi = 0;           // constant rows [tail_lo, tail_hi)
+  std::string arr, S, U, T;               // array, name prefixes, tail name
+  bool tail() const { return tail_hi > tail_lo; }
+  int K() const { return (int)segs.size(); }
+  int len(int i) const { return segs[i].second - segs[i].first; }
+  std::string seg(int i) const {
+    return len(i) == 1 ? arr + "[" + std::to_string(segs[i].first) + "]" : S + std::to_string(i);
+  }
+  std::string chain(int i) const {
+    if (i + 1 < K()) return seg(i) + " * " + U + std::to_string(i + 1);
+    return tail() ? seg(i) + " * " + T : seg(i);
+  }
+  std::string top() const { return K() ? U + "0" : (tail() ? T : std::string()); }
+  int index(int row) const {
+    for (int i = 0; i < K(); ++i)
+      if (row >= segs[i].first && row < segs[i].second) return i;
+    return -1;
+  }
+};
+
 // Generated kernel (paired segmented walk).  Gray steps 2j and 2j+1 differ in
 // walk bit 0 only, so they are evaluated together: segment 0 (the rows walk
 // bit 0 touches) is held twice, x (bit 0 clear) and y = x + a_0 (bit 0 set),
@@ -226,24 +311,47 @@ std::string tree(int lo, int hi, const char* v = "x") {
 // bits 1..m-1 (pair bit p = walk bit p+1).
 struct Gen {
   const Plan& P;
-  int nseg, len0;
-  bool rest;
+  int len0;
+  Chain outer, inx, iny;
   std::ostringstream o;
-  explicit Gen(const Plan& p)
-      : P(p), nseg((int)p.seg_start.size() - 1), len0(p.seg_start[1]), rest(p.seg_start.back() < p.n) {}
-
-  int len(int i) const { return P.seg_start[i + 1] - P.seg_start[i]; }
-  std::string S(int i) const { return len(i) == 1 ? "x[" + std::to_string(P.seg_start[i]) + "]" : "S" + std::to_string(i); }
-  std::string unext(int i) const { return i + 1 < nseg ? "U" + std::to_string(i + 1) : "R"; }
-  std::string chain(int i) const {
-    return (i + 1 < nseg || rest) ? S(i) + " * " + unext(i) : S(i);
+  explicit Gen(const Plan& p) : P(p), len0(p.seg_start[1]) {
+    const int nseg = (int)p.seg_start.size() - 1;
+    for (int i = 1; i < nseg; ++i) outer.segs.push_back({p.seg_start[i], p.seg_start[i + 1]});
+    outer.tail_lo = p.seg_start.back(), outer.tail_hi = p.n;
+    outer.arr = "x", outer.S = "So", outer.U = "Uo", outer.T = "Ro";
+    for (size_t i = 0; i + 1 < p.sub_start.size(); ++i) inx.segs.push_back({p.sub_start[i], p.sub_start[i + 1]});
+    inx.tail_lo = p.sub_start.back(), inx.tail_hi = len0;
+    iny = inx;
+    inx.arr = "x", inx.S = "Sx", inx.U = "Vx", inx.T = "Cx";
+    iny.arr = "y", iny.S = "Sy", iny.U = "Vy", iny.T = "Cy";
   }
-  // the factor that multiplies D: U1, or R, or nothing
-  std::string ux() const { return nseg >= 2 ? "U1" : (rest ? "R" : ""); }
-  std::string dexpr() const { return tree(0, len0, "x") + " - " + tree(0, len0, "y"); }
+
+  void chain_init(const Chain& c, const char* ind) {
+    if (c.tail()) o << ind << "const double " << c.T << " = " << tree(c.tail_lo, c.tail_hi, c.arr.c_str()) << ";\n";
+    for (int i = 0; i < c.K(); ++i)
+      if (c.len(i) > 1)
+        o << ind << "double " << c.S << i << " = " << tree(c.segs[i].first, c.segs[i].second, c.arr.c_str()) << ";\n";
+    for (int i = c.K() - 1; i >= 0; --i) o << ind << "double " << c.U << i << " = " << c.chain(i) << ";\n";
+  }
+  // returns whether the chain changed
+  bool chain_update(const Chain& c, const std::vector<int>& rows, const char* ind) {
+    std::vector<char> dirty(std::max(c.K(), 1), 0);
+    int smax = -1;
+    for (int r : rows) {
+      const int i = c.index(r);
+      if (i >= 0) dirty[i] = 1, smax = std::max(smax, i);
+    }
+    for (int i = smax; i >= 0; --i) {
+      if (dirty[i] && c.len(i) > 1)
+        o << ind << "  " << c.S << i << " = " << tree(c.segs[i].first, c.segs[i].second, c.arr.c_str()) << ";\n";
+      o << ind << "  " << c.U << i << " = " << c.chain(i) << ";\n";
+    }
+    return smax >= 0;
+  }
+  std::string dexpr() const { return inx.top() + " - " + iny.top(); }
   void accumulate(bool neg, const char* ind) {
-    if (ux().empty()) o << ind << (neg ? "acc -= D;\n" : "acc += D;\n");
-    else o << ind << "acc = __builtin_fma(" << (neg ? "-D" : "D") << ", " << ux() << ", acc);\n";
+    if (outer.top().empty()) o << ind << (neg ? "acc -= D;\n" : "acc += D;\n");
+    else o << ind << "acc = __builtin_fma(" << (neg ? "-D" : "D") << ", " << outer.top() << ", acc);\n";
   }
 
   // Add the values at table pointer `cv` (dbl8 pieces) to rows `rows` (and
@@ -273,19 +381,11 @@ struct Gen {
   }
 
   void products(const std::vector<int>& rows, const char* ind) {
-    std::vector<char> dirty(nseg, 0);
-    int smax = 0;
-    for (int r : rows) {
-      const int i = seg_index(P.seg_start, r);
-      dirty[i] = 1;
-      smax = std::max(smax, i);
+    chain_update(outer, rows, ind);
+    if (chain_update(inx, rows, ind)) {
+      chain_update(iny, rows, ind);
+      o << ind << "  D = " << dexpr() << ";\n";
     }
-    for (int i = smax; i >= 1; --i) {
-      if (dirty[i] && len(i) > 1)
-        o << ind << "  S" << i << " = " << tree(P.seg_start[i], P.seg_start[i + 1]) << ";\n";
-      o << ind << "  U" << i << " = " << chain(i) << ";\n";
-    }
-    if (dirty[0]) o << ind << "  D = " << dexpr() << ";\n";
   }
 
   // pair step flipping walk bit k <= seg_b: packed touched values; `off` = byte offset expression
@@ -310,22 +410,24 @@ struct Gen {
 
   std::string source() {
     const int n = P.n, L = P.lay.L, m = P.lay.m, b = P.seg_b;
-    const int R0 = P.seg_start.back();
     const unsigned B = 1u << b, Q = 1u << (m - 1 - b);
     o << "// generated by superman_amd jit.cpp: paired segmented Gray walk, n=" << n << " L=" << L << " m=" << m
-      << " segments=" << nseg << " pair bits specialised=" << b << "\n";
+      << " segment0=" << len0 << " (" << inx.K() << " sub-segments) outer segments=" << outer.K()
+      << " pair bits specialised=" << b << "\n";
     o << "#include \"walk_common.hpp\"\n";
     o << "namespace sup {\n";
     o << "typedef double jdbl8 __attribute__((ext_vector_type(8)));\n";
     o << "typedef const __attribute__((address_space(4))) jdbl8 cjdbl8;\n";
-    // occupancy target from the values live across the walk loop (x, y, S_i,
-    // U_i, D, acc, R, loop state; 2 VGPRs each): the default heuristic of the
-    // compiler trades occupancy 2 for scheduling freedom, which costs more
+    // occupancy target from the values live across the walk loop (x, y,
+    // chain values, D, acc, loop state; 2 VGPRs each): the compiler's own
+    // choice trades occupancy 2 for scheduling freedom, which costs more
     // latency hiding than it buys.  SUP_JIT_WAVES overrides (experiments).
-    int nS = 0;
-    for (int i = 1; i < nseg; ++i) nS += len(i) > 1;
-    const int live = 2 * (n + len0 + nS + nseg + 6);
-    int waves = live <= 116 ? 4 : (live <= 156 ? 3 : 2);
+    int vals = n + len0 + 4;
+    for (const Chain* c : {&outer, &inx, &iny}) {
+      vals += c->K() + (c->tail() ? 1 : 0);
+      for (int i = 0; i < c->K(); ++i) vals += c->len(i) > 1;
+    }
+    int waves = 2 * vals <= 116 ? 4 : 3;  // (occupancy 2 is never worth it: measured)
     if (const char* e = std::getenv("SUP_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
     o << "extern \"C\" __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(" << waves
       << "))) void sup_walk_seg(WalkParams p) {\n";
@@ -345,12 +447,11 @@ struct Gen {
     o << "        cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off_const(0, 0) << ");\n";
     for (int r = 0; r < len0; ++r) o << "        y[" << r << "] = x[" << r << "] + cv[" << r / 8 << "][" << r % 8 << "];\n";
     o << "      }\n";
-    if (rest) o << "      const double R = " << tree(R0, n) << ";\n";
-    for (int i = 1; i < nseg; ++i)
-      if (len(i) > 1) o << "      double S" << i << " = " << tree(P.seg_start[i], P.seg_start[i + 1]) << ";\n";
-    for (int i = nseg - 1; i >= 1; --i) o << "      double U" << i << " = " << chain(i) << ";\n";
+    chain_init(outer, "      ");
+    chain_init(inx, "      ");
+    chain_init(iny, "      ");
     o << "      double D = " << dexpr() << ";\n";
-    o << "      double acc = " << (ux().empty() ? std::string("D") : "D * " + ux()) << ";\n";
+    o << "      double acc = " << (outer.top().empty() ? std::string("D") : "D * " + outer.top()) << ";\n";
     o << "      for (uint32_t q = 0; q < " << Q << "u; ++q) {\n";
     const char* ind = "        ";
     // pair index j = B*q + s, s = 1 .. B-1: pair bit p = ctz(s) (walk bit p+1);
@@ -435,6 +536,25 @@ int build_seg(Plan& P) {
   if (P.touched[0].empty()) {
     set_error("segmented walk: walk column 0 has no nonzero");
     return SUP_EINVAL;
+  }
+  // sub-segments of segment 0: rows in first-touch order by walk bits >= 1
+  // (make_plan orders them so, seg_row_order), constant rows last
+  {
+    const int len0 = P.seg_start[1];
+    std::vector<char> got(len0, 0);
+    int cnt = 0;
+    P.sub_start.assign(1, 0);
+    for (int k = 1; k < m; ++k) {
+      for (int r : P.touched[k])
+        if (r < len0 && !got[r]) {
+          if (r != cnt) {
+            set_error("segmented walk: segment 0 rows are not in sub-segment order");
+            return SUP_EINVAL;
+          }
+          got[r] = 1, ++cnt;
+        }
+      if (cnt > P.sub_start.back()) P.sub_start.push_back(cnt);
+    }
   }
   P.seg_b = seg_static_bits(m);
   P.dyn_rows.clear();
