@@ -9,7 +9,9 @@
 // (detected by its banner, read as main.cpp:1515-1615).  Own additions: -R
 // combine multi-GPU partials with RCCL; -v per-kernel / per-chunk timing;
 // --seed (-S) the estimators' Philox seed (-a / -i; the reference seeds with
-// time(0), so its estimates are not reproducible).
+// time(0), so its estimates are not reproducible); --jit (-J) <-1|0|1> the
+// pattern-specialised segmented walk (sup_opts.jit: never / auto / whenever
+// its cost model wins).
 #include <getopt.h>
 
 #include <chrono>
@@ -32,6 +34,7 @@ struct Cli {
   long number_of_times = 100000;  // main.cu:338-344 defaults
   int scale_intervals = 4, scale_times = 5, gridm = 36, gridn = 36;
   unsigned long long seed = 1;
+  int jit = 0;
   std::string filename;
 };
 
@@ -116,7 +119,7 @@ int run_approx(const Cli& c) {
 
 int main(int argc, char** argv) {
   Cli c;
-  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rvou:S:";
+  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rvou:S:J:";
   const struct option long_options[] = {{"binary", 0, NULL, 'b'},       {"sparse", 0, NULL, 's'},
                                         {"preprocessing", 1, NULL, 'r'}, {"threads", 1, NULL, 't'},
                                         {"file", 1, NULL, 'f'},          {"gpu", 0, NULL, 'g'},
@@ -128,7 +131,7 @@ int main(int argc, char** argv) {
                                         {"gpu-id", 1, NULL, 'l'},        {"reps", 1, NULL, 'k'},
                                         {"rccl", 0, NULL, 'R'},          {"verbose", 0, NULL, 'v'},
                                         {"compression", 0, NULL, 'o'},   {"scaling", 1, NULL, 'u'},
-                                        {"seed", 1, NULL, 'S'},
+                                        {"seed", 1, NULL, 'S'},          {"jit", 1, NULL, 'J'},
                                         {NULL, 0, NULL, 0}};
   int opt;
   auto need_arg = [&](char o) -> bool {
@@ -156,6 +159,7 @@ int main(int argc, char** argv) {
       case 'm': if (!need_arg('m')) return 1; c.gridm = std::atoi(optarg); break;
       case 'n': if (!need_arg('n')) return 1; c.gridn = std::atoi(optarg); break;
       case 'S': if (!need_arg('S')) return 1; c.seed = std::strtoull(optarg, nullptr, 10); break;
+      case 'J': c.jit = std::atoi(optarg); break;  // may be negative: no need_arg
       case 'i': c.grid_graph = true; break;
       case 'l': if (!need_arg('l')) return 1; c.device = std::atoi(optarg); break;
       case 'k': if (!need_arg('k')) return 1; c.reps = std::max(1, std::atoi(optarg)); break;
@@ -206,6 +210,7 @@ int main(int argc, char** argv) {
   o.cpu_worker = (c.gpu && c.cpu) ? 1 : 0;
   o.use_rccl = c.rccl ? 1 : 0;
   o.verbose = c.verbose ? 1 : 0;
+  o.jit = c.jit;
 
   std::string name;
   sup_kernel kern = SUP_KERNEL_DENSE;
@@ -296,9 +301,11 @@ int main(int argc, char** argv) {
     }
     report(name, perm, sec);
     if (c.verbose)
-      std::printf("Stats: kernel_ms %.3f gray_steps %llu visited %llu devices %d lanes %d walk %d grid %d leaves %d\n",
+      std::printf("Stats: kernel_ms %.3f gray_steps %llu visited %llu devices %d lanes %d walk %d grid %d leaves %d "
+                  "walk_kind %d ops_per_step %.1f jit_ms %.1f\n",
                   st.kernel_ms, (unsigned long long)st.gray_steps, (unsigned long long)st.visited_steps,
-                  st.devices_used, st.lane_bits, st.walk_bits, st.grid, st.leaves);
+                  st.devices_used, st.lane_bits, st.walk_bits, st.grid, st.leaves, st.walk_kind, st.est_ops_per_step,
+                  st.jit_ms);
   }
   sup_free(mat);
   return 0;
