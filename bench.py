@@ -16,10 +16,17 @@ with hiprtc before the warmup (compile time reported as config.jit_compile_ms,
 outside the timed region, like the plan), then every timed step walks all
 2^39 Gray steps.  --jit -1 runs the ahead-of-time prefix-blocked kernel.
 
+The north star also asks for density 0.2: the reference corpus matrix
+double/40_0.20_0 (--also) is timed the same way (same shards, all-reduce and
+clock) and reported under "densities"; `value` stays the d = 0.5 metric.
+
 Prints ONE JSON line on rank 0 (driver contract), including the roofline of
 the walk kernel (hipEvents on its own stream, measured inside the library)
 and a CPU baseline (oracle/ port of the reference's parallel_perman64 chunk
 loop, timed on a bounded sample of the same workload on this host's cores).
+The roofline object also carries the committed rocprofv3 PMC evidence for the
+walk kernel (achieved occupancy, LDS bank conflicts, VALU instructions per
+step, HBM bytes per launch; profiles/, tools/pmc_summary.py).
 """
 from __future__ import annotations
 
@@ -51,6 +58,9 @@ def parse():
     ap.add_argument("--rehearse", action="store_true",
                     help="all ranks on device 0 over gloo: rehearse the N-rank path on a one-GPU box")
     ap.add_argument("--prep", type=int, default=0, choices=[0, 1, 2], help="-r: 1 SortOrder, 2 SkipOrder")
+    ap.add_argument("--also", default=os.path.join(ROOT, "tests", "fixtures", "double__40_0.20_0"),
+                    help="comma-separated companion matrices timed the same way (north star: densities "
+                         "0.2 and 0.5 at every N); '' = none")
     return ap.parse_args()
 
 
@@ -64,14 +74,16 @@ def shard_chunks(n: int, rank: int, world: int) -> tuple[int, int]:
     return C * rank // world, C * (rank + 1) // world
 
 
-def pmc_traffic(n: int, kernel: str):
-    """HBM bytes per walk launch from the committed rocprofv3 PMC summary of
-    this kernel, if any."""
+def pmc_record(n: int, kernel: str):
+    """The committed rocprofv3 PMC summary of this walk kernel at this n
+    (tools/pmc_summary.py: HBM bytes per launch, achieved occupancy, LDS bank
+    conflicts), newest round first; None if there is none."""
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc*.json"), recursive=True), reverse=True):
         try:
             d = json.load(open(p))
             if d.get("n") == n and "hbm_bytes_per_launch" in d and kernel in d.get("kernel", ""):
-                return d["hbm_bytes_per_launch"]
+                d["_path"] = os.path.relpath(p, ROOT)
+                return d
         except Exception:
             pass
     return None
@@ -122,56 +134,81 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     import superman_amd as S
 
-    a, typ, _ = S.read_matrix(args.matrix)
-    if args.prep == 1:
-        a = S.sort_order(a)[0]
-    elif args.prep == 2:
-        a = S.skip_order(a)[0]
-    n = a.shape[0]
-    L, m, _ = S.layout(n)
-    c0, c1 = shard_chunks(n, rank, world)
-    my_steps = (c1 - c0) << (L + m)
-    # plan + (segmented walk) hiprtc compile, once, before the timed region;
-    # gpu_num = world so that --jit 0 decides as the N-rank plan would
-    prep = S.prepare(a, args.kernel, jit=args.jit, gpu_num=world)
-
-    def step():
-        part, st = S.perman_shard(a, rank, world, kernel=args.kernel, device_id=dev, return_stats=True,
-                                  jit=args.jit)
-        if world > 1:
-            t = torch.tensor([part], dtype=torch.float64, device=tdev)
-            dist.all_reduce(t)  # RCCL over xGMI: the single data-path collective
-            part = float(t.item())
-        return (4 * (n & 1) - 2) * part, st
+    def load(path):
+        a = S.read_matrix(path)[0]
+        if args.prep == 1:
+            a = S.sort_order(a)[0]
+        elif args.prep == 2:
+            a = S.skip_order(a)[0]
+        return a
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    t0 = time.perf_counter()
-    kms, perm = [], None
-    for _ in range(args.steps):
-        perm, st = step()
-        kms.append(st["kernel_ms"])
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(a):
+        """W untimed + K timed steps of one whole permanent of `a`; returns
+        (elapsed max over ranks, permanent, mean walk-kernel ms, stats, compile ms)."""
+        n = a.shape[0]
+        # plan + (segmented walk) hiprtc compile, once, before the timed region;
+        # gpu_num = world so that --jit 0 decides as the N-rank plan would
+        prep = S.prepare(a, args.kernel, jit=args.jit, gpu_num=world)
+
+        def step():
+            part, st = S.perman_shard(a, rank, world, kernel=args.kernel, device_id=dev, return_stats=True,
+                                      jit=args.jit)
+            if world > 1:
+                t = torch.tensor([part], dtype=torch.float64, device=tdev)
+                dist.all_reduce(t)  # RCCL over xGMI: the single data-path collective
+                part = float(t.item())
+            return (4 * (n & 1) - 2) * part, st
+
+        for _ in range(args.warmup):
+            step()
+        barrier()
+        t0 = time.perf_counter()
+        kms, perm, st = [], None, None
+        for _ in range(args.steps):
+            perm, st = step()
+            kms.append(st["kernel_ms"])
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, perm, sum(kms) / len(kms), st, prep["compile_ms"]
+
+    a = load(args.matrix)
+    n = a.shape[0]
+    L, m, _ = S.layout(n)
+    c0, c1 = shard_chunks(n, rank, world)
+    my_steps = (c1 - c0) << (L + m)
+    elapsed, perm, k_ms, st, compile_ms = timed(a)
+    walk_names = {0: "dense", 1: "prefix-blocked", 2: "skipper", 3: "segmented (pattern-specialised)"}
+
+    # companion densities (north star: 0.2 and 0.5), same shards / all-reduce / clock
+    also = []
+    for path in [p for p in args.also.split(",") if p and os.path.abspath(p) != os.path.abspath(args.matrix)]:
+        b = load(path)
+        nb = b.shape[0]
+        e2, perm2, kms2, st2, _ = timed(b)
+        also.append({"matrix": os.path.basename(path).replace("__", "/"), "n": nb,
+                     "density": round(float((b != 0).sum()) / (nb * nb), 4),
+                     "value": args.steps * (1 << (nb - 1)) / e2, "unit": "gray-steps/s",
+                     "ms_per_step": e2 / args.steps * 1e3, "kernel_ms_avg": kms2,
+                     "walk": walk_names[st2["walk_kind"]],
+                     "est_fp64_ops_per_step": st2["est_ops_per_step"], "permanent": perm2})
 
     total_steps = args.steps * (1 << (n - 1))
     value = total_steps / elapsed
-    k_ms = sum(kms) / len(kms)
     flops = 2.0 * n * my_steps  # n fp64 adds + n fp64 muls per Gray step (SURVEY §8(d))
     achieved = flops / (k_ms * 1e-3) / 1e12
     walk = {0: f"sup::walk_dense<{n}>", 1: f"sup::walk_sparse<{n}>", 2: f"sup::walk_skip<{n}>",
             3: "sup_walk_seg"}[st["walk_kind"]]
-    traffic = pmc_traffic(n, walk)
+    pmc = pmc_record(n, walk)
+    traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     fname = os.path.basename(args.matrix).replace("__", "/")
     density = float((a != 0).sum()) / (n * n)
     rec = {
@@ -191,9 +228,8 @@ def main():
                                f"d={density:.2f} ({fname}), 2^{n - 1} Gray steps per step",
                    "n": n, "density": round(density, 4), "gray_steps_per_step": 1 << (n - 1),
                    "kernel_request": args.kernel, "preprocessing": args.prep, "jit": args.jit,
-                   "walk": {0: "dense", 1: "prefix-blocked", 2: "skipper", 3: "segmented (pattern-specialised)"}[
-                       st["walk_kind"]],
-                   "jit_compile_ms": prep["compile_ms"],
+                   "walk": walk_names[st["walk_kind"]],
+                   "jit_compile_ms": compile_ms,
                    "parallelism": f"dp{world}: contiguous wave-chunk shards + one RCCL all-reduce"},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
@@ -209,7 +245,17 @@ def main():
                      "executed_fp64_ops_per_s": st["est_ops_per_step"] * my_steps / (k_ms * 1e-3),
                      "issue_frac": st["est_ops_per_step"] * my_steps / (k_ms * 1e-3) / (FP64_PEAK_TFLOPS * 1e12 / 2)},
         "permanent": perm,
+        "densities": also,
     }
+    if pmc:  # rocprofv3 evidence for the dominant kernel (committed profile of this kernel at this n)
+        sq = pmc.get("sq", {})
+        rec["roofline"].update({
+            "pmc_source": pmc["_path"],
+            "achieved_waves_per_simd": sq.get("achieved_waves_per_simd"),
+            "achieved_occupancy_frac": sq.get("achieved_occupancy_frac"),
+            "lds_bank_conflicts": sq.get("SQ_LDS_BANK_CONFLICT"),
+            "valu_insts_per_step": sq.get("valu_insts_per_lane_step"),
+            "valu_busy_frac": sq.get("valu_busy_frac_est")})
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cb_rec, err = cpu_baseline(a, n, args.cpu_seconds, S,
                                    "seg" if st["walk_kind"] == 3 else args.kernel)

@@ -11,7 +11,10 @@ pmc_lds; each --kernel-trace only, bench.py --steps 1) and the --stats pass
     writes 8-B partials;
   * VALU wave-instructions per lane-step = SQ_INSTS_VALU / (2^(n-1) / 64);
   * clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time; VALU busy = fp64 VALU
-    issue cycles (4 per wave-instruction) per SIMD / active cycles.
+    issue cycles (4 per wave-instruction) per SIMD / active cycles;
+  * achieved occupancy = resident waves per SIMD averaged over the kernel =
+    4 x SQ_WAVE_CYCLES (quad-cycles) / 1024 SIMDs / cycles, and its share of
+    the 8 wave slots of a gfx950 SIMD.
 """
 import csv
 import glob
@@ -66,6 +69,12 @@ def main():
             cyc = sqd["GRBM_GUI_ACTIVE"] / 8.0
             sqd["clock_ghz_est"] = round(cyc / t / 1e9, 3)
             sqd["valu_busy_frac_est"] = round(sqd["SQ_INSTS_VALU"] * 4.0 / 1024.0 / cyc, 3)
+            if sqd.get("SQ_WAVE_CYCLES"):
+                # achieved occupancy: SQ_WAVE_CYCLES counts quad-cycles of resident waves
+                # (MI355X_MICROARCH.md), over 1024 SIMDs x the kernel's cycles
+                occ = sqd["SQ_WAVE_CYCLES"] * 4.0 / 1024.0 / cyc
+                sqd["achieved_waves_per_simd"] = round(occ, 3)
+                sqd["achieved_occupancy_frac"] = round(occ / 8.0, 4)  # of the 8 wave slots per SIMD
     rec["sq"] = sqd
     rec["notes"] = ("FETCH/WRITE_SIZE in KB per dispatch, no gfx950 x2 correction (scalar-load table, 8-B partial "
                     "stores). Algorithmic bytes = wave-chunk partials x 8 B + the signed column table. The walk is "
