@@ -555,72 +555,110 @@ static double e_tree(const double* x, int lo, int hi) {
   return e_tree(x, lo, mid) * e_tree(x, mid, hi);
 }
 
-/* a product chain over row ranges [lo_i, hi_i): segment products S_i (trees),
- * U_i = S_i * U_{i+1}, the last closed by the constant tail product T (rows
- * [tlo, thi)) when the tail is not empty */
+/* segmented walk products: a binary product tree per row group.  Items are
+ * the group's rows [lo, tlo) (each with the set of step classes touching it:
+ * class k-1 for walk bit k <= segb, class segb for any walk bit > segb) and,
+ * if rows [tlo, thi) exist, one constant item = e_tree over them.  Built
+ * greedily: join the two clusters (in list order, first pair i < j on ties)
+ * whose union of classes has the least weight, weight(class c < segb) =
+ * 2^(segb-1-c), weight(class segb) = 1; the joined cluster is appended.  A
+ * step of class c re-forms the nodes whose class set holds c, in creation
+ * order (jit.cpp make_tree). */
 typedef struct {
-  int K, lo[ORC_MAXN], hi[ORC_MAXN], tlo, thi;
-} echain;
+  int ni, K, tlo, thi;
+  int row[ORC_MAXN + 1];             /* item -> row, -1 = constant item */
+  unsigned isig[ORC_MAXN + 1];
+  int a[2 * ORC_MAXN], b[2 * ORC_MAXN];
+  unsigned sig[2 * ORC_MAXN];
+} etree;
 typedef struct {
-  double S[ORC_MAXN], U[ORC_MAXN], T;
-} echv;
+  double N[2 * ORC_MAXN], T;
+} etv;
 
-static void e_link(const echain* c, echv* v, int i) {
-  if (i + 1 < c->K) v->U[i] = v->S[i] * v->U[i + 1];
-  else v->U[i] = c->thi > c->tlo ? v->S[i] * v->T : v->S[i];
-}
-static void e_chain_init(const echain* c, const double* a, echv* v) {
-  v->T = c->thi > c->tlo ? e_tree(a, c->tlo, c->thi) : 1.0;
-  for (int i = c->K - 1; i >= 0; --i) {
-    v->S[i] = e_tree(a, c->lo[i], c->hi[i]);
-    e_link(c, v, i);
-  }
-}
-static double e_chain_top(const echain* c, const echv* v) {
-  return c->K ? v->U[0] : (c->thi > c->tlo ? v->T : 1.0);
-}
-/* rows flagged in `rows` changed: re-form their segments, then the chain from
- * the deepest one up; returns whether any segment of the chain changed */
-static int e_chain_update(const echain* c, const double* a, echv* v, const char* rows) {
-  int smax = -1;
-  char dirty[ORC_MAXN] = {0};
-  for (int i = 0; i < c->K; ++i)
-    for (int r = c->lo[i]; r < c->hi[i]; ++r)
-      if (rows[r]) dirty[i] = 1, smax = i;
-  for (int i = smax; i >= 0; --i) {
-    if (dirty[i]) v->S[i] = e_tree(a, c->lo[i], c->hi[i]);
-    e_link(c, v, i);
-  }
-  return smax >= 0;
+static unsigned long long e_weight(unsigned s, int segb) {
+  unsigned long long w = 0;
+  for (int c = 0; c <= segb; ++c)
+    if ((s >> c) & 1u) w += c < segb ? (1ULL << (segb - 1 - c)) : 1ULL;
+  return w;
 }
 
-static void e_seg_chains(const eplan* P, echain* outer, echain* inner) {
-  outer->K = 0;
-  for (int i = 1; i < P->nseg; ++i) outer->lo[outer->K] = P->seg[i], outer->hi[outer->K++] = P->seg[i + 1];
-  outer->tlo = P->seg[P->nseg], outer->thi = P->n;
-  inner->K = 0;
-  for (int i = 0; i < P->nsub; ++i) inner->lo[inner->K] = P->sub[i], inner->hi[inner->K++] = P->sub[i + 1];
-  inner->tlo = P->sub[P->nsub], inner->thi = P->len0;
+static void e_tree_build(etree* t, const unsigned* rsig, int lo, int tlo, int thi, int segb) {
+  int id[ORC_MAXN + 1], cnt = 0;
+  unsigned sg[ORC_MAXN + 1];
+  t->ni = 0, t->K = 0, t->tlo = tlo, t->thi = thi;
+  for (int r = lo; r < tlo; ++r) t->row[t->ni] = r, t->isig[t->ni++] = rsig[r];
+  if (thi > tlo) t->row[t->ni] = -1, t->isig[t->ni++] = 0;
+  for (int i = 0; i < t->ni; ++i) id[cnt] = i, sg[cnt++] = t->isig[i];
+  while (cnt > 1) {
+    int bi = 0, bj = 1;
+    unsigned long long bw = ~0ULL;
+    for (int i = 0; i < cnt; ++i)
+      for (int j = i + 1; j < cnt; ++j) {
+        unsigned long long w = e_weight(sg[i] | sg[j], segb);
+        if (w < bw) bw = w, bi = i, bj = j;
+      }
+    unsigned ns = sg[bi] | sg[bj];
+    t->a[t->K] = id[bi], t->b[t->K] = id[bj], t->sig[t->K] = ns;
+    ++t->K;
+    /* drop positions bi < bj, keep the order of the rest, append the join */
+    int w = 0;
+    for (int i = 0; i < cnt; ++i)
+      if (i != bi && i != bj) id[w] = id[i], sg[w++] = sg[i];
+    id[w] = t->ni + t->K - 1, sg[w++] = ns;
+    cnt = w;
+  }
+}
+
+static double e_tv_id(const etree* t, const double* a, const etv* v, int id) {
+  if (id < t->ni) return t->row[id] < 0 ? v->T : a[t->row[id]];
+  return v->N[id - t->ni];
+}
+static void e_tree_init(const etree* t, const double* a, etv* v) {
+  v->T = t->thi > t->tlo ? e_tree(a, t->tlo, t->thi) : 1.0;
+  for (int i = 0; i < t->K; ++i) v->N[i] = e_tv_id(t, a, v, t->a[i]) * e_tv_id(t, a, v, t->b[i]);
+}
+static int e_root(const etree* t) { return t->K ? t->ni + t->K - 1 : (t->ni ? 0 : -1); }
+static unsigned e_root_sig(const etree* t) { return t->K ? t->sig[t->K - 1] : (t->ni ? t->isig[0] : 0u); }
+static double e_tree_top(const etree* t, const double* a, const etv* v) {
+  int r = e_root(t);
+  return r < 0 ? 1.0 : e_tv_id(t, a, v, r);
+}
+static void e_tree_update(const etree* t, const double* a, etv* v, int c) {
+  for (int i = 0; i < t->K; ++i)
+    if ((t->sig[i] >> c) & 1u) v->N[i] = e_tv_id(t, a, v, t->a[i]) * e_tv_id(t, a, v, t->b[i]);
+}
+
+/* the outer tree (rows outside segment 0) and segment 0's tree */
+static void e_seg_trees(const eplan* P, etree* outer, etree* inner) {
+  unsigned rsig[ORC_MAXN] = {0};
+  for (int k = 1; k < P->m; ++k) {
+    int c = k <= P->segb ? k - 1 : P->segb;
+    for (int j = 0; j < P->n; ++j)
+      if (P->col[2 * (P->L + k)][j] != 0.0) rsig[j] |= 1u << c;
+  }
+  e_tree_build(outer, rsig, P->len0, P->seg[P->nseg], P->n, P->segb);
+  e_tree_build(inner, rsig, 0, P->sub[P->nsub], P->len0, P->segb);
 }
 
 /* one pair step flipping walk bit k >= 1: its rows (x, and y on segment 0),
- * the outer chain, and segment 0's chains over x and y with D = top_x - top_y */
-static void e_seg_step(const eplan* P, const echain* outer, const echain* inner, double* x, double* y, echv* vo,
-                       echv* vx, echv* vy, double* D, int k, int neg) {
+ * the outer tree, and segment 0's trees over x and y with D = top_x - top_y */
+static void e_seg_step(const eplan* P, const etree* outer, const etree* inner, double* x, double* y, etv* vo,
+                       etv* vx, etv* vy, double* D, int k, int neg) {
   const double* c = P->col[2 * (P->L + k) + neg];
-  char rows[ORC_MAXN] = {0};
   int any = 0;
   for (int j = 0; j < P->n; ++j)
     if (k <= P->segb ? c[j] != 0.0 : P->dyn[j]) {
       x[j] += c[j];
       if (j < P->len0) y[j] += c[j];
-      rows[j] = 1, any = 1;
+      any = 1;
     }
   if (!any) return;
-  e_chain_update(outer, x, vo, rows);
-  if (e_chain_update(inner, x, vx, rows)) {
-    e_chain_update(inner, y, vy, rows);
-    *D = e_chain_top(inner, vx) - e_chain_top(inner, vy);
+  int cl = k <= P->segb ? k - 1 : P->segb;
+  e_tree_update(outer, x, vo, cl);
+  if ((e_root_sig(inner) >> cl) & 1u) {
+    e_tree_update(inner, x, vx, cl);
+    e_tree_update(inner, y, vy, cl);
+    *D = e_tree_top(inner, x, vx) - e_tree_top(inner, y, vy);
   }
 }
 
@@ -649,21 +687,21 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
       double x[ORC_MAXN], U[ORC_MAXN / 8 + 2], acc;
       e_start(P, ga, l, x);
       if (P->kind == 3) {
-        static __thread echv vo, vx, vy;
-        echain outer, inner;
+        static __thread etv vo, vx, vy;
+        static __thread etree outer, inner;
         double y[ORC_MAXN], D;
-        e_seg_chains(P, &outer, &inner);
+        e_seg_trees(P, &outer, &inner);
         for (int r = 0; r < P->len0; ++r) y[r] = x[r] + P->col[2 * L][r];
-        e_chain_init(&outer, x, &vo);
-        e_chain_init(&inner, x, &vx);
-        e_chain_init(&inner, y, &vy);
-        D = e_chain_top(&inner, &vx) - e_chain_top(&inner, &vy);
-        acc = D * e_chain_top(&outer, &vo);
+        e_tree_init(&outer, x, &vo);
+        e_tree_init(&inner, x, &vx);
+        e_tree_init(&inner, y, &vy);
+        D = e_tree_top(&inner, x, &vx) - e_tree_top(&inner, y, &vy);
+        acc = D * e_tree_top(&outer, x, &vo);
         /* pair j = Gray steps 2j, 2j+1: contributes (-1)^j D U1 */
         for (unsigned j = 1; j < T / 2; ++j) {
           unsigned pb = __builtin_ctz(j), neg = (j >> (pb + 1)) & 1u;
           e_seg_step(P, &outer, &inner, x, y, &vo, &vx, &vy, &D, (int)pb + 1, (int)neg);
-          acc = fma((j & 1u) ? -D : D, e_chain_top(&outer, &vo), acc);
+          acc = fma((j & 1u) ? -D : D, e_tree_top(&outer, x, &vo), acc);
         }
       } else if (P->kind == 0) {
         acc = e_prod4(x, n);

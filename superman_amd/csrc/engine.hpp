@@ -35,6 +35,26 @@ struct Layout {
 };
 Layout default_layout(int n);
 
+// Product tree of the segmented walk (jit.cpp make_tree).  Items are engine
+// rows (item_row[t] = row) and, when tail_hi > tail_lo, one constant item
+// (item_row = -1): the halving-tree product of rows [tail_lo, tail_hi), which
+// no walk bit >= 1 touches.  Node i = value(a[i]) * value(b[i]), where id <
+// items() names item id and id = items() + i' names node i' < i.  sig = the
+// step classes that make a node dirty: bit c < seg_b for walk bit c + 1, bit
+// seg_b for the shared step of walk bits > seg_b.  A step of class c re-forms
+// exactly the nodes with bit c, in index order.
+struct ProdTree {
+  std::vector<int> item_row;
+  std::vector<uint32_t> item_sig;
+  int tail_lo = 0, tail_hi = 0;
+  std::vector<int> a, b;
+  std::vector<uint32_t> sig;
+  int items() const { return (int)item_row.size(); }
+  int K() const { return (int)a.size(); }
+  int root() const { return K() ? items() + K() - 1 : (items() ? 0 : -1); }
+  uint32_t root_sig() const { return K() ? sig.back() : (items() ? item_sig[0] : 0u); }
+};
+
 struct Plan {
   int n = 0;
   int NP = 0;
@@ -57,7 +77,9 @@ struct Plan {
   std::vector<int> sub_start;      // sub-segments of segment 0 (first touch by walk bits >= 1);
                                    // rows [sub_start.back(), seg_start[1]) are constant per chunk
   int seg_b = 0;                   // pair bits [0, seg_b) have specialised steps (seg_static_bits)
-  std::vector<int> dyn_rows;       // rows touched by walk bits >= seg_b (their shared step)
+  std::vector<int> dyn_rows;       // rows touched by walk bits > seg_b (their shared step)
+  ProdTree outer_tree;             // rows outside segment 0 (over x)
+  ProdTree inner_tree;             // segment 0's rows (once over x, once over y)
   std::vector<int> jofs;           // [m] offset (doubles) of walk bit k's + block in jtab
   std::vector<double> jtab;        // packed touched values: + block, - block (each padded to 8)
   std::string jit_src;             // generated HIP source of the specialised kernel

@@ -98,88 +98,52 @@ double seg_tree(const double* x, int lo, int hi) {
   return seg_tree(x, lo, mid) * seg_tree(x, mid, hi);
 }
 
-// Product chain over row ranges (jit.cpp Chain): segment products (trees),
-// suffix products U_i = S_i * U_{i+1}, constant tail T closing the chain.
-struct ChainDef {
-  std::vector<std::pair<int, int>> segs;
-  int tail_lo = 0, tail_hi = 0;
-  bool tail() const { return tail_hi > tail_lo; }
-  int K() const { return (int)segs.size(); }
-  int index(int r) const {
-    for (int i = 0; i < K(); ++i)
-      if (r >= segs[i].first && r < segs[i].second) return i;
-    return -1;
-  }
+// Product tree values (Plan::outer_tree / inner_tree, jit.cpp make_tree):
+// constant item T = halving tree over the tail rows, node i = value(a[i]) *
+// value(b[i]).
+struct TreeVal {
+  double N[2 * SUP_MAX_N], T;
 };
-struct ChainVal {
-  double S[SUP_MAX_N], U[SUP_MAX_N], T;
-};
-
-inline void chain_link(const ChainDef& c, ChainVal& v, int i) {
-  v.U[i] = i + 1 < c.K() ? v.S[i] * v.U[i + 1] : (c.tail() ? v.S[i] * v.T : v.S[i]);
+inline double tree_id(const ProdTree& t, const double* a, const TreeVal& v, int id) {
+  if (id < t.items()) return t.item_row[id] < 0 ? v.T : a[t.item_row[id]];
+  return v.N[id - t.items()];
 }
-void chain_init(const ChainDef& c, const double* a, ChainVal& v) {
-  v.T = c.tail() ? seg_tree(a, c.tail_lo, c.tail_hi) : 1.0;
-  for (int i = c.K() - 1; i >= 0; --i) {
-    v.S[i] = seg_tree(a, c.segs[i].first, c.segs[i].second);
-    chain_link(c, v, i);
-  }
+void tree_init(const ProdTree& t, const double* a, TreeVal& v) {
+  v.T = t.tail_hi > t.tail_lo ? seg_tree(a, t.tail_lo, t.tail_hi) : 1.0;
+  for (int i = 0; i < t.K(); ++i) v.N[i] = tree_id(t, a, v, t.a[i]) * tree_id(t, a, v, t.b[i]);
 }
-// the chain's product: U_0, else the tail, else none (1: fma(D, 1, acc) == acc + D)
-inline double chain_top(const ChainDef& c, const ChainVal& v) { return c.K() ? v.U[0] : (c.tail() ? v.T : 1.0); }
+// re-form the nodes of step class c (index order)
+inline void tree_update(const ProdTree& t, const double* a, TreeVal& v, int c) {
+  for (int i = 0; i < t.K(); ++i)
+    if ((t.sig[i] >> c) & 1u) v.N[i] = tree_id(t, a, v, t.a[i]) * tree_id(t, a, v, t.b[i]);
+}
+// the tree's product: its root, else none (1: fma(D, 1, acc) == acc + D)
+inline double tree_top(const ProdTree& t, const double* a, const TreeVal& v) {
+  return t.root() < 0 ? 1.0 : tree_id(t, a, v, t.root());
+}
 
 // Paired form: Gray steps 2j, 2j+1 differ in walk bit 0 only; segment 0 (the
 // rows walk bit 0 touches) is kept as x (bit 0 clear) and y = x + a_0, and the
-// pair adds (-1)^j (prod_seg0 x - prod_seg0 y) * U1 (U1 = outer chain over the
-// other rows; segment 0's products are sub-segment chains over x and y).
+// pair adds (-1)^j (prod_seg0 x - prod_seg0 y) * U1 (U1 = outer tree over the
+// other rows; segment 0's products are its tree over x and over y).
 // Pair step j flips walk bit k = ctz(j) + 1; walk bits k <= seg_b use their
 // own touched rows, bits > seg_b one shared step over dyn_rows (the generated
 // kernel's straight-line step for those bits).
-struct SegSteps {
-  ChainDef outer, inner;
-  std::vector<std::vector<char>> odirty, idirty;  // [k][q]: segment smax-q dirty
-  std::vector<int> omax, imax;
-  explicit SegSteps(const Plan& P) : odirty(P.lay.m), idirty(P.lay.m), omax(P.lay.m, -1), imax(P.lay.m, -1) {
-    const int nseg = (int)P.seg_start.size() - 1, len0 = P.seg_start[1];
-    for (int i = 1; i < nseg; ++i) outer.segs.push_back({P.seg_start[i], P.seg_start[i + 1]});
-    outer.tail_lo = P.seg_start.back(), outer.tail_hi = P.n;
-    for (size_t i = 0; i + 1 < P.sub_start.size(); ++i) inner.segs.push_back({P.sub_start[i], P.sub_start[i + 1]});
-    inner.tail_lo = P.sub_start.back(), inner.tail_hi = len0;
-    for (int k = 1; k < P.lay.m; ++k) {
-      std::vector<char> od(std::max(outer.K(), 1), 0), id(std::max(inner.K(), 1), 0);
-      for (int r : (k <= P.seg_b ? P.touched[k] : P.dyn_rows)) {
-        const int io = outer.index(r), ii = inner.index(r);
-        if (io >= 0) od[io] = 1, omax[k] = std::max(omax[k], io);
-        if (ii >= 0) id[ii] = 1, imax[k] = std::max(imax[k], ii);
-      }
-      for (int i = omax[k]; i >= 0; --i) odirty[k].push_back(od[i]);
-      for (int i = imax[k]; i >= 0; --i) idirty[k].push_back(id[i]);
-    }
-  }
-};
-
 struct SegLane {
   double y[SUP_MAX_N], D;
-  ChainVal o, ix, iy;
+  TreeVal o, ix, iy;
 };
 
-inline void chain_update(const ChainDef& c, const double* a, ChainVal& v, int smax, const std::vector<char>& dirty) {
-  for (int i = smax, q = 0; i >= 0; --i, ++q) {
-    if (dirty[q]) v.S[i] = seg_tree(a, c.segs[i].first, c.segs[i].second);
-    chain_link(c, v, i);
-  }
-}
-
-void seg_init(Lane& s, SegLane& g, const Plan& P, const SegSteps& st) {
+void seg_init(Lane& s, SegLane& g, const Plan& P) {
   const int len0 = P.seg_start[1];
   for (int r = 0; r < len0; ++r) g.y[r] = s.x[r] + P.jtab[P.jofs[0] + r];
-  chain_init(st.outer, s.x, g.o);
-  chain_init(st.inner, s.x, g.ix);
-  chain_init(st.inner, g.y, g.iy);
-  g.D = chain_top(st.inner, g.ix) - chain_top(st.inner, g.iy);
+  tree_init(P.outer_tree, s.x, g.o);
+  tree_init(P.inner_tree, s.x, g.ix);
+  tree_init(P.inner_tree, g.y, g.iy);
+  g.D = tree_top(P.inner_tree, s.x, g.ix) - tree_top(P.inner_tree, g.y, g.iy);
 }
 
-void seg_step(Lane& s, SegLane& g, const Plan& P, const SegSteps& st, int k, int neg) {
+void seg_step(Lane& s, SegLane& g, const Plan& P, int k, int neg) {
   const int len0 = P.seg_start[1];
   if (k > P.seg_b) {  // shared step: full signed column over dyn_rows (zeros included)
     if (P.dyn_rows.empty()) return;
@@ -198,11 +162,12 @@ void seg_step(Lane& s, SegLane& g, const Plan& P, const SegSteps& st, int k, int
       if (t[i] < len0) g.y[t[i]] += v[i];
     }
   }
-  chain_update(st.outer, s.x, g.o, st.omax[k], st.odirty[k]);
-  if (st.imax[k] >= 0) {
-    chain_update(st.inner, s.x, g.ix, st.imax[k], st.idirty[k]);
-    chain_update(st.inner, g.y, g.iy, st.imax[k], st.idirty[k]);
-    g.D = chain_top(st.inner, g.ix) - chain_top(st.inner, g.iy);
+  const int c = k <= P.seg_b ? k - 1 : P.seg_b;
+  tree_update(P.outer_tree, s.x, g.o, c);
+  if ((P.inner_tree.root_sig() >> c) & 1u) {
+    tree_update(P.inner_tree, s.x, g.ix, c);
+    tree_update(P.inner_tree, g.y, g.iy, c);
+    g.D = tree_top(P.inner_tree, s.x, g.ix) - tree_top(P.inner_tree, g.y, g.iy);
   }
 }
 
@@ -212,7 +177,6 @@ double chunk_partial(const Plan& P, uint64_t ga) {
   const uint32_t T = 1u << m;
   double lane_val[64];
   if (P.kind == kWalkSeg) {
-    const SegSteps st(P);
     for (unsigned l = 0; l < 64; ++l) {
       if (l >= (1u << L)) {
         lane_val[l] = 0.0;
@@ -221,12 +185,12 @@ double chunk_partial(const Plan& P, uint64_t ga) {
       Lane s;
       chunk_start(P, ga, l, s);
       static thread_local SegLane g;
-      seg_init(s, g, P, st);
-      double acc = g.D * chain_top(st.outer, g.o);
+      seg_init(s, g, P);
+      double acc = g.D * tree_top(P.outer_tree, s.x, g.o);
       for (uint32_t j = 1; j < T / 2; ++j) {  // pair steps: walk bit ctz(j) + 1
         const uint32_t pb = __builtin_ctz(j);
-        seg_step(s, g, P, st, (int)pb + 1, (j >> (pb + 1)) & 1u);
-        acc = std::fma((j & 1u) ? -g.D : g.D, chain_top(st.outer, g.o), acc);
+        seg_step(s, g, P, (int)pb + 1, (j >> (pb + 1)) & 1u);
+        acc = std::fma((j & 1u) ? -g.D : g.D, tree_top(P.outer_tree, s.x, g.o), acc);
       }
       const unsigned par = (unsigned)__builtin_popcount(l) & 1u;
       if ((((unsigned)ga) ^ par) & 1u) acc = -acc;

@@ -183,11 +183,76 @@ double cost_of(const std::vector<int>& seg_start, int n, const std::vector<std::
 
 double shape_cost(const SegShape& s, int n) { return cost_of(s.seg_start, n, s.touched); }
 
+// Step class of walk bit k >= 1: k - 1 for the specialised pair bits, seg_b
+// for the shared step of the walk bits above them.
+int step_class(int k, int b) { return k <= b ? k - 1 : b; }
+
+// Greedy product tree over rows [lo, tail_lo) (+ the constant item for rows
+// [tail_lo, tail_hi)): repeatedly join the two clusters whose union is dirty
+// least often, i.e. minimise w(sig_i | sig_j) with w(class c) = 2^(b-1-c) (walk
+// bit c+1 flips on 2^-(c+1) of the pair steps) and w(shared) = 1; ties -> the
+// first pair (i < j) in list order; the joined cluster goes to the end.  Rows
+// that always change together end up under one node, so a step re-forms only
+// the nodes above the rows it touches (the first-touch chain it replaces had
+// to re-form whole segments and every link above them).
+ProdTree make_tree(const std::vector<uint32_t>& rsig, int lo, int tail_lo, int tail_hi, int b) {
+  ProdTree t;
+  t.tail_lo = tail_lo, t.tail_hi = tail_hi;
+  for (int r = lo; r < tail_lo; ++r) t.item_row.push_back(r), t.item_sig.push_back(rsig[r]);
+  if (tail_hi > tail_lo) t.item_row.push_back(-1), t.item_sig.push_back(0u);
+  auto weight = [b](uint32_t s) {
+    uint64_t w = 0;
+    for (int c = 0; c <= b; ++c)
+      if ((s >> c) & 1u) w += c < b ? (1ull << (b - 1 - c)) : 1ull;
+    return w;
+  };
+  std::vector<int> id;
+  std::vector<uint32_t> sg;
+  for (int i = 0; i < t.items(); ++i) id.push_back(i), sg.push_back(t.item_sig[i]);
+  while (id.size() > 1) {
+    size_t bi = 0, bj = 1;
+    uint64_t bw = UINT64_MAX;
+    for (size_t i = 0; i < id.size(); ++i)
+      for (size_t j = i + 1; j < id.size(); ++j) {
+        const uint64_t w = weight(sg[i] | sg[j]);
+        if (w < bw) bw = w, bi = i, bj = j;
+      }
+    const uint32_t ns = sg[bi] | sg[bj];
+    t.a.push_back(id[bi]), t.b.push_back(id[bj]), t.sig.push_back(ns);
+    id.erase(id.begin() + bj), sg.erase(sg.begin() + bj);
+    id.erase(id.begin() + bi), sg.erase(sg.begin() + bi);
+    id.push_back(t.items() + t.K() - 1), sg.push_back(ns);
+  }
+  return t;
+}
+
+int nodes_with(const ProdTree& t, int c) {
+  int k = 0;
+  for (uint32_t s : t.sig) k += (s >> c) & 1u;
+  return k;
+}
+
 }  // namespace
 
 int seg_static_bits(int m) { return std::min(m - 1, 5); }
 
-double seg_walk_cost(const Plan& P) { return cost_of(P.seg_start, P.n, P.touched); }
+// Ops per Gray step of the generated kernel, exactly: per pair step of class
+// c, the adds of its rows (twice on segment 0), the dirty outer nodes, the
+// dirty inner nodes over x and over y, D when segment 0 changed, the fma.
+double seg_walk_cost(const Plan& P) {
+  const int m = P.lay.m, b = P.seg_b, len0 = P.seg_start[1];
+  double c = 0.0, w = 0.5;
+  for (int p = 0; p + 1 < m; ++p, w *= 0.5) {
+    const int k = p + 1, cl = step_class(k, b);
+    const std::vector<int>& t = k <= b ? P.touched[k] : P.dyn_rows;
+    double ops = 1.0 + (double)t.size();
+    for (int r : t) ops += r < len0;
+    ops += nodes_with(P.outer_tree, cl) + 2.0 * nodes_with(P.inner_tree, cl);
+    ops += (P.inner_tree.root_sig() >> cl) & 1u;
+    c += w * ops;
+  }
+  return c / 2.0;
+}
 
 std::vector<int> seg_walk_order(const double* A, int n, int m, int count) {
   const int nb = n - 1;
@@ -277,30 +342,26 @@ std::string tree(int lo, int hi, const char* v = "x") {
   return "(" + tree(lo, mid, v) + " * " + tree(mid, hi, v) + ")";
 }
 
-// A product chain over row ranges: segment products S_i (trees), suffix
-// products U_i = S_i * U_{i+1}, and a constant tail T (rows no walk bit >= 1
-// touches) closing the chain.  Used for the rows outside segment 0 (over x)
-// and for the sub-segments of segment 0 (once over x, once over y).
-struct Chain {
-  std::vector<std::pair<int, int>> segs;  // row ranges [lo, hi)
-  int tail_lo = 0, tail_hi = 0;           // constant rows [tail_lo, tail_hi)
-  std::string arr, S, U, T;               // array, name prefixes, tail name
-  bool tail() const { return tail_hi > tail_lo; }
-  int K() const { return (int)segs.size(); }
-  int len(int i) const { return segs[i].second - segs[i].first; }
-  std::string seg(int i) const {
-    return len(i) == 1 ? arr + "[" + std::to_string(segs[i].first) + "]" : S + std::to_string(i);
+// Signature of node i's parent (-1 for the root): a node dirty exactly when
+// its parent is need not stay live between steps.
+int parent_sig(const ProdTree& t, int i) {
+  const int id = t.items() + i;
+  for (int j = i + 1; j < t.K(); ++j)
+    if (t.a[j] == id || t.b[j] == id) return (int)t.sig[j];
+  return -1;
+}
+
+// Names of one product tree's values in the generated code: items are the
+// row array `arr` and the constant item `T`; node i is `N<i>`.
+struct TreeNames {
+  const ProdTree* t;
+  std::string arr, N, T;
+  std::string id(int i) const {
+    if (i < t->items()) return t->item_row[i] < 0 ? T : arr + "[" + std::to_string(t->item_row[i]) + "]";
+    return N + std::to_string(i - t->items());
   }
-  std::string chain(int i) const {
-    if (i + 1 < K()) return seg(i) + " * " + U + std::to_string(i + 1);
-    return tail() ? seg(i) + " * " + T : seg(i);
-  }
-  std::string top() const { return K() ? U + "0" : (tail() ? T : std::string()); }
-  int index(int row) const {
-    for (int i = 0; i < K(); ++i)
-      if (row >= segs[i].first && row < segs[i].second) return i;
-    return -1;
-  }
+  std::string top() const { return t->root() < 0 ? std::string() : id(t->root()); }
+  std::string node(int i) const { return id(t->a[i]) + " * " + id(t->b[i]); }
 };
 
 // Generated kernel (paired segmented walk).  Gray steps 2j and 2j+1 differ in
@@ -308,45 +369,29 @@ struct Chain {
 // bit 0 touches) is held twice, x (bit 0 clear) and y = x + a_0 (bit 0 set),
 // and the pair contributes (-1)^j (prod_seg0 x - prod_seg0 y) * U1, U1 being
 // the product of every other row.  The pair walk is a Gray walk over walk
-// bits 1..m-1 (pair bit p = walk bit p+1).
+// bits 1..m-1 (pair bit p = walk bit p+1).  Both products are product trees
+// (make_tree): a step re-forms the nodes above the rows it touches.
 struct Gen {
   const Plan& P;
   int len0;
-  Chain outer, inx, iny;
+  TreeNames outer, inx, iny;
   std::ostringstream o;
   explicit Gen(const Plan& p) : P(p), len0(p.seg_start[1]) {
-    const int nseg = (int)p.seg_start.size() - 1;
-    for (int i = 1; i < nseg; ++i) outer.segs.push_back({p.seg_start[i], p.seg_start[i + 1]});
-    outer.tail_lo = p.seg_start.back(), outer.tail_hi = p.n;
-    outer.arr = "x", outer.S = "So", outer.U = "Uo", outer.T = "Ro";
-    for (size_t i = 0; i + 1 < p.sub_start.size(); ++i) inx.segs.push_back({p.sub_start[i], p.sub_start[i + 1]});
-    inx.tail_lo = p.sub_start.back(), inx.tail_hi = len0;
-    iny = inx;
-    inx.arr = "x", inx.S = "Sx", inx.U = "Vx", inx.T = "Cx";
-    iny.arr = "y", iny.S = "Sy", iny.U = "Vy", iny.T = "Cy";
+    outer = {&p.outer_tree, "x", "o", "Ro"};
+    inx = {&p.inner_tree, "x", "px", "Cx"};
+    iny = {&p.inner_tree, "y", "py", "Cy"};
   }
 
-  void chain_init(const Chain& c, const char* ind) {
-    if (c.tail()) o << ind << "const double " << c.T << " = " << tree(c.tail_lo, c.tail_hi, c.arr.c_str()) << ";\n";
-    for (int i = 0; i < c.K(); ++i)
-      if (c.len(i) > 1)
-        o << ind << "double " << c.S << i << " = " << tree(c.segs[i].first, c.segs[i].second, c.arr.c_str()) << ";\n";
-    for (int i = c.K() - 1; i >= 0; --i) o << ind << "double " << c.U << i << " = " << c.chain(i) << ";\n";
+  void tree_init(const TreeNames& t, const char* ind) {
+    if (t.t->tail_hi > t.t->tail_lo)
+      o << ind << "const double " << t.T << " = " << tree(t.t->tail_lo, t.t->tail_hi, t.arr.c_str()) << ";\n";
+    for (int i = 0; i < t.t->K(); ++i) o << ind << "double " << t.N << i << " = " << t.node(i) << ";\n";
   }
-  // returns whether the chain changed
-  bool chain_update(const Chain& c, const std::vector<int>& rows, const char* ind) {
-    std::vector<char> dirty(std::max(c.K(), 1), 0);
-    int smax = -1;
-    for (int r : rows) {
-      const int i = c.index(r);
-      if (i >= 0) dirty[i] = 1, smax = std::max(smax, i);
-    }
-    for (int i = smax; i >= 0; --i) {
-      if (dirty[i] && c.len(i) > 1)
-        o << ind << "  " << c.S << i << " = " << tree(c.segs[i].first, c.segs[i].second, c.arr.c_str()) << ";\n";
-      o << ind << "  " << c.U << i << " = " << c.chain(i) << ";\n";
-    }
-    return smax >= 0;
+  // re-form the nodes of step class c; returns whether the root changed
+  bool tree_update(const TreeNames& t, int c, const char* ind) {
+    for (int i = 0; i < t.t->K(); ++i)
+      if ((t.t->sig[i] >> c) & 1u) o << ind << "  " << t.N << i << " = " << t.node(i) << ";\n";
+    return (t.t->root_sig() >> c) & 1u;
   }
   std::string dexpr() const { return inx.top() + " - " + iny.top(); }
   void accumulate(bool neg, const char* ind) {
@@ -380,10 +425,10 @@ struct Gen {
     }
   }
 
-  void products(const std::vector<int>& rows, const char* ind) {
-    chain_update(outer, rows, ind);
-    if (chain_update(inx, rows, ind)) {
-      chain_update(iny, rows, ind);
+  void products(int c, const char* ind) {
+    tree_update(outer, c, ind);
+    if (tree_update(inx, c, ind)) {
+      tree_update(iny, c, ind);
       o << ind << "  D = " << dexpr() << ";\n";
     }
   }
@@ -395,7 +440,7 @@ struct Gen {
     o << ind << "{\n";
     o << ind << "  cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off << ");\n";
     adds(t, false, ind);
-    products(t, ind);
+    products(step_class(k, P.seg_b), ind);
     o << ind << "}\n";
   }
 
@@ -412,7 +457,7 @@ struct Gen {
     const int n = P.n, L = P.lay.L, m = P.lay.m, b = P.seg_b;
     const unsigned B = 1u << b, Q = 1u << (m - 1 - b);
     o << "// generated by superman_amd jit.cpp: paired segmented Gray walk, n=" << n << " L=" << L << " m=" << m
-      << " segment0=" << len0 << " (" << inx.K() << " sub-segments) outer segments=" << outer.K()
+      << " segment0=" << len0 << " (" << P.inner_tree.K() << " tree nodes) outer tree nodes=" << P.outer_tree.K()
       << " pair bits specialised=" << b << "\n";
     o << "#include \"walk_common.hpp\"\n";
     o << "namespace sup {\n";
@@ -423,9 +468,12 @@ struct Gen {
     // choice trades occupancy 2 for scheduling freedom, which costs more
     // latency hiding than it buys.  SUP_JIT_WAVES overrides (experiments).
     int vals = n + len0 + 4;
-    for (const Chain* c : {&outer, &inx, &iny}) {
-      vals += c->K() + (c->tail() ? 1 : 0);
-      for (int i = 0; i < c->K(); ++i) vals += c->len(i) > 1;
+    for (const TreeNames* t : {&outer, &inx, &iny}) {  // nodes kept across steps
+      vals += t->t->tail_hi > t->t->tail_lo;
+      for (int i = 0; i < t->t->K(); ++i) {
+        const int par = parent_sig(*t->t, i);
+        vals += par < 0 || (uint32_t)par != t->t->sig[i];
+      }
     }
     int waves = 2 * vals <= 116 ? 4 : 3;  // (occupancy 2 is never worth it: measured)
     if (const char* e = std::getenv("SUP_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
@@ -447,9 +495,9 @@ struct Gen {
     o << "        cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off_const(0, 0) << ");\n";
     for (int r = 0; r < len0; ++r) o << "        y[" << r << "] = x[" << r << "] + cv[" << r / 8 << "][" << r % 8 << "];\n";
     o << "      }\n";
-    chain_init(outer, "      ");
-    chain_init(inx, "      ");
-    chain_init(iny, "      ");
+    tree_init(outer, "      ");
+    tree_init(inx, "      ");
+    tree_init(iny, "      ");
     o << "      double D = " << dexpr() << ";\n";
     o << "      double acc = " << (outer.top().empty() ? std::string("D") : "D * " + outer.top()) << ";\n";
     o << "      for (uint32_t q = 0; q < " << Q << "u; ++q) {\n";
@@ -479,7 +527,7 @@ struct Gen {
       o << ind << "  cjdbl8* cv = (cjdbl8*)opaque_c(p.cols, (2u * (" << (L + b + 1) << "u + kk) + ng) * "
         << P.NP * 8 << "u);\n";
       adds(P.dyn_rows, true, ind);
-      products(P.dyn_rows, ind);
+      products(P.seg_b, ind);
       accumulate(false, "          ");
       o << ind << "}\n";
     }
@@ -564,6 +612,14 @@ int build_seg(Plan& P) {
       for (int r : P.touched[k]) in[r] = 1;
     for (int j = 0; j < n; ++j)
       if (in[j]) P.dyn_rows.push_back(j);
+  }
+  {  // product trees: rows outside segment 0 and segment 0's rows, by step class
+    std::vector<uint32_t> rsig(n, 0u);
+    for (int k = 1; k < m; ++k)
+      for (int r : P.touched[k]) rsig[r] |= 1u << step_class(k, P.seg_b);
+    const int len0 = P.seg_start[1];
+    P.outer_tree = make_tree(rsig, len0, P.seg_start.back(), n, P.seg_b);
+    P.inner_tree = make_tree(rsig, 0, P.sub_start.back(), len0, P.seg_b);
   }
   P.jofs.assign(m, 0);
   P.jtab.clear();
