@@ -32,8 +32,8 @@ def load() -> C.CDLL:
         lib.orc_ref_sparse_partial.argtypes = [P, I, LL, LL, I]
         lib.orc_ref_skip.argtypes = [P, I, I, C.POINTER(U)]
         lib.orc_ref_skip_partial.argtypes = [P, I, LL, LL, I]
-        lib.orc_engine_range.argtypes = [P, I, I, P, I, I, U, U, I, C.POINTER(U)]
-        lib.orc_engine_perman.argtypes = [P, I, I, P, I]
+        lib.orc_engine_range.argtypes = [P, I, I, P, I, I, I, U, U, I, C.POINTER(U)]
+        lib.orc_engine_perman.argtypes = [P, I, I, P, I, I]
         lib.orc_nw_start.argtypes = [P, I, P, P]
         lib.orc_engine_layout.argtypes = [I, C.POINTER(I), C.POINTER(I), C.POINTER(I)]
         for f in ("orc_ref_dense", "orc_ref_dense_partial", "orc_ref_sparse", "orc_ref_sparse_partial",
@@ -110,29 +110,33 @@ def _colmap(colmap):
     return cm, cm.ctypes.data
 
 
-def engine_range(a, kind, c0: int, c1: int, L: int, m: int, colmap=None, threads: int = 8) -> tuple[float, int]:
+def engine_range(a, kind, c0: int, c1: int, L: int, m: int, colmap=None, threads: int = 8,
+                 cached: int = 0) -> tuple[float, int]:
     """Engine-schedule mirror over wave-chunks [c0, c1): (partial, visited).
-    colmap: engine bit -> matrix column (None = identity)."""
+    colmap: engine bit -> matrix column (None = identity); cached: the
+    segmented walk's cached walk bits (plan_info()["cached"])."""
     a = _d(a)
     v = C.c_ulonglong(0)
     keep, ptr = _colmap(colmap)
-    r = load().orc_engine_range(a.ctypes.data, a.shape[0], KINDS[kind], ptr, L, m, c0, c1, threads, C.byref(v))
+    r = load().orc_engine_range(a.ctypes.data, a.shape[0], KINDS[kind], ptr, int(cached), L, m, c0, c1, threads,
+                                C.byref(v))
     return r, v.value
 
 
-def engine_perman(a, kind="dense", colmap=None, threads: int = 8) -> float:
+def engine_perman(a, kind="dense", colmap=None, threads: int = 8, cached: int = 0) -> float:
     """Full permanent enumerated exactly as the gfx950 kernels do (bit-exact
-    mirror), for walk `kind` and engine column map `colmap`."""
+    mirror), for walk `kind`, engine column map `colmap` and (segmented walk)
+    `cached` walk bits."""
     a = _d(a)
     keep, ptr = _colmap(colmap)
-    return load().orc_engine_perman(a.ctypes.data, a.shape[0], KINDS[kind], ptr, threads)
+    return load().orc_engine_perman(a.ctypes.data, a.shape[0], KINDS[kind], ptr, int(cached), threads)
 
 
 def engine_perman_as(sup_module, a, kernel="dense", threads: int = 8, jit: int = 0) -> float:
-    """Mirror of exactly the plan the product runs for `kernel` (walk kind and
-    column map queried through the C ABI's sup_plan_info)."""
+    """Mirror of exactly the plan the product runs for `kernel` (walk kind,
+    column map and cached walk bits queried through the C ABI's sup_plan_info)."""
     info = sup_module.plan_info(a, kernel, jit=jit)
-    return engine_perman(a, info["kind"], info["colmap"], threads)
+    return engine_perman(a, info["kind"], info["colmap"], threads, info.get("cached", 0))
 
 
 def exact_perman(a) -> Fraction:

@@ -387,7 +387,7 @@ typedef struct {
   double x0[ORC_MAXN];
   double col[2 * ORC_MAXN][ORC_MAXN]; /* [2e+neg][j] */
   /* segmented walk (kind 3): segment i = rows [seg[i], seg[i+1]), rest = [seg[nseg], n) */
-  int nseg, seg[ORC_MAXN + 1], segb, len0;
+  int nseg, seg[ORC_MAXN + 1], segb, len0, cc; /* cc: cached walk bits 1..cc */
   int nsub, sub[ORC_MAXN + 1];    /* sub-segments of segment 0 */
   char dyn[ORC_MAXN];             /* rows some walk bit > segb touches */
 } eplan;
@@ -405,8 +405,9 @@ void orc_engine_layout(int n, int* L, int* m, int* h) {
   *h = rest - mm;
 }
 
-static void engine_plan(const double* a, int n, int kind, const int* colmap, int L, int m, eplan* P) {
+static void engine_plan(const double* a, int n, int kind, const int* colmap, int L, int m, int cc, eplan* P) {
   memset(P, 0, sizeof(*P));
+  P->cc = cc;
   P->n = n;
   P->NP = (n + 7) & ~7;
   P->kind = kind;
@@ -561,7 +562,8 @@ static double e_tree(const double* x, int lo, int hi) {
  * if rows [tlo, thi) exist, one constant item = e_tree over them.  Built
  * greedily: join the two clusters (in list order, first pair i < j on ties)
  * whose union of classes has the least weight, weight(class c < segb) =
- * 2^(segb-1-c), weight(class segb) = 1; the joined cluster is appended.  A
+ * 2^(segb-1-c), weight(class segb) = 1, cached classes (c < cc) weigh 0 and
+ * double the weight of the rest; the joined cluster is appended.  A
  * step of class c re-forms the nodes whose class set holds c, in creation
  * order (jit.cpp make_tree). */
 typedef struct {
@@ -575,14 +577,14 @@ typedef struct {
   double N[2 * ORC_MAXN], T;
 } etv;
 
-static unsigned long long e_weight(unsigned s, int segb) {
+static unsigned long long e_weight(unsigned s, int segb, int cc) {
   unsigned long long w = 0;
-  for (int c = 0; c <= segb; ++c)
+  for (int c = cc; c <= segb; ++c)
     if ((s >> c) & 1u) w += c < segb ? (1ULL << (segb - 1 - c)) : 1ULL;
-  return w;
+  return w << __builtin_popcount(s & ((1u << cc) - 1u)); /* one copy per cached state it depends on */
 }
 
-static void e_tree_build(etree* t, const unsigned* rsig, int lo, int tlo, int thi, int segb) {
+static void e_tree_build(etree* t, const unsigned* rsig, int lo, int tlo, int thi, int segb, int cc) {
   int id[ORC_MAXN + 1], cnt = 0;
   unsigned sg[ORC_MAXN + 1];
   t->ni = 0, t->K = 0, t->tlo = tlo, t->thi = thi;
@@ -594,7 +596,7 @@ static void e_tree_build(etree* t, const unsigned* rsig, int lo, int tlo, int th
     unsigned long long bw = ~0ULL;
     for (int i = 0; i < cnt; ++i)
       for (int j = i + 1; j < cnt; ++j) {
-        unsigned long long w = e_weight(sg[i] | sg[j], segb);
+        unsigned long long w = e_weight(sg[i] | sg[j], segb, cc);
         if (w < bw) bw = w, bi = i, bj = j;
       }
     unsigned ns = sg[bi] | sg[bj];
@@ -636,16 +638,19 @@ static void e_seg_trees(const eplan* P, etree* outer, etree* inner) {
     for (int j = 0; j < P->n; ++j)
       if (P->col[2 * (P->L + k)][j] != 0.0) rsig[j] |= 1u << c;
   }
-  e_tree_build(outer, rsig, P->len0, P->seg[P->nseg], P->n, P->segb);
-  e_tree_build(inner, rsig, 0, P->sub[P->nsub], P->len0, P->segb);
+  e_tree_build(outer, rsig, P->len0, P->seg[P->nseg], P->n, P->segb, P->cc);
+  e_tree_build(inner, rsig, 0, P->sub[P->nsub], P->len0, P->segb, P->cc);
 }
 
-/* one pair step flipping walk bit k >= 1: its rows (x, and y on segment 0),
- * the outer tree, and segment 0's trees over x and y with D = top_x - top_y */
+/* one pair step flipping walk bit k >= 1 in one cached state: its rows (x,
+ * and y on segment 0), the outer tree, and segment 0's trees over x and y with
+ * D = top_x - top_y */
 static void e_seg_step(const eplan* P, const etree* outer, const etree* inner, double* x, double* y, etv* vo,
                        etv* vx, etv* vy, double* D, int k, int neg) {
   const double* c = P->col[2 * (P->L + k) + neg];
   int any = 0;
+  int cl = k <= P->segb ? k - 1 : P->segb;
+  if (cl < P->cc) return; /* cached walk bit: every state already held */
   for (int j = 0; j < P->n; ++j)
     if (k <= P->segb ? c[j] != 0.0 : P->dyn[j]) {
       x[j] += c[j];
@@ -653,7 +658,6 @@ static void e_seg_step(const eplan* P, const etree* outer, const etree* inner, d
       any = 1;
     }
   if (!any) return;
-  int cl = k <= P->segb ? k - 1 : P->segb;
   e_tree_update(outer, x, vo, cl);
   if ((e_root_sig(inner) >> cl) & 1u) {
     e_tree_update(inner, x, vx, cl);
@@ -687,21 +691,44 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
       double x[ORC_MAXN], U[ORC_MAXN / 8 + 2], acc;
       e_start(P, ga, l, x);
       if (P->kind == 3) {
-        static __thread etv vo, vx, vy;
+        /* cached walk bits 1..cc: one full state per assignment S of them;
+         * state S = state S^low + the + column of walk bit ctz(low)+1 on the
+         * rows it touches (low = lowest set bit of S) */
+        static __thread etv vo[4], vx[4], vy[4];
         static __thread etree outer, inner;
-        double y[ORC_MAXN], D;
+        static __thread double xs[4][ORC_MAXN], ys[4][ORC_MAXN];
+        double D[4];
+        int NS = 1 << P->cc;
         e_seg_trees(P, &outer, &inner);
-        for (int r = 0; r < P->len0; ++r) y[r] = x[r] + P->col[2 * L][r];
-        e_tree_init(&outer, x, &vo);
-        e_tree_init(&inner, x, &vx);
-        e_tree_init(&inner, y, &vy);
-        D = e_tree_top(&inner, x, &vx) - e_tree_top(&inner, y, &vy);
-        acc = D * e_tree_top(&outer, x, &vo);
-        /* pair j = Gray steps 2j, 2j+1: contributes (-1)^j D U1 */
+        memcpy(xs[0], x, sizeof(double) * n);
+        for (int r = 0; r < P->len0; ++r) ys[0][r] = xs[0][r] + P->col[2 * L][r];
+        for (int S = 1; S < NS; ++S) {
+          int low = S & -S, k = __builtin_ctz(low) + 1;
+          const double* cp = P->col[2 * (L + k)];
+          memcpy(xs[S], xs[S ^ low], sizeof(double) * n);
+          memcpy(ys[S], ys[S ^ low], sizeof(double) * P->len0);
+          for (int r = 0; r < n; ++r)
+            if (cp[r] != 0.0) {
+              xs[S][r] = xs[S ^ low][r] + cp[r];
+              if (r < P->len0) ys[S][r] = ys[S ^ low][r] + cp[r];
+            }
+        }
+        for (int S = 0; S < NS; ++S) {
+          e_tree_init(&outer, xs[S], &vo[S]);
+          e_tree_init(&inner, xs[S], &vx[S]);
+          e_tree_init(&inner, ys[S], &vy[S]);
+          D[S] = e_tree_top(&inner, xs[S], &vx[S]) - e_tree_top(&inner, ys[S], &vy[S]);
+        }
+        acc = D[0] * e_tree_top(&outer, xs[0], &vo[0]);
+        /* pair j = Gray steps 2j, 2j+1: contributes (-1)^j D U1, in the
+         * state of its Gray bits 1..cc */
         for (unsigned j = 1; j < T / 2; ++j) {
           unsigned pb = __builtin_ctz(j), neg = (j >> (pb + 1)) & 1u;
-          e_seg_step(P, &outer, &inner, x, y, &vo, &vx, &vy, &D, (int)pb + 1, (int)neg);
-          acc = fma((j & 1u) ? -D : D, e_tree_top(&outer, x, &vo), acc);
+          int S = 0;
+          for (int S2 = 0; S2 < NS; ++S2)
+            e_seg_step(P, &outer, &inner, xs[S2], ys[S2], &vo[S2], &vx[S2], &vy[S2], &D[S2], (int)pb + 1, (int)neg);
+          for (int i = 0; i < P->cc; ++i) S |= (int)(((j >> i) ^ (j >> (i + 1))) & 1u) << i;
+          acc = fma((j & 1u) ? -D[S] : D[S], e_tree_top(&outer, xs[S], &vo[S]), acc);
         }
       } else if (P->kind == 0) {
         acc = e_prod4(x, n);
@@ -791,11 +818,12 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
 /* Engine-mirror partial over wave-chunks [c0, c1) with layout (L, m).
  * kind: 0 dense, 1 SpaRyser (prefix blocks), 2 SkipPer, 3 segmented walk
  * (jit.cpp's generated kernel).  colmap: engine bit e
- * -> matrix column (n-1 entries; NULL = identity). */
-double orc_engine_range(const double* a, int n, int kind, const int* colmap, int L, int m, unsigned long long c0,
-                        unsigned long long c1, int threads, unsigned long long* visited) {
+ * -> matrix column (n-1 entries; NULL = identity).  cc (kind 3): walk bits
+ * 1..cc held in every state (the engine plan's choice, sup_plan_info). */
+double orc_engine_range(const double* a, int n, int kind, const int* colmap, int cc, int L, int m,
+                        unsigned long long c0, unsigned long long c1, int threads, unsigned long long* visited) {
   eplan* P = (eplan*)malloc(sizeof(eplan));
-  engine_plan(a, n, kind, colmap, L, m, P);
+  engine_plan(a, n, kind, colmap, L, m, cc, P);
   unsigned long long count = c1 > c0 ? c1 - c0 : 0;
   if (count == 0) {
     free(P);
@@ -829,9 +857,9 @@ double orc_engine_range(const double* a, int n, int kind, const int* colmap, int
 }
 
 /* Full permanent with the engine's default layout and the given column map. */
-double orc_engine_perman(const double* a, int n, int kind, const int* colmap, int threads) {
+double orc_engine_perman(const double* a, int n, int kind, const int* colmap, int cc, int threads) {
   int L, m, h;
   orc_engine_layout(n, &L, &m, &h);
-  double s = orc_engine_range(a, n, kind, colmap, L, m, 0, 1ULL << h, threads, 0);
+  double s = orc_engine_range(a, n, kind, colmap, cc, L, m, 0, 1ULL << h, threads, 0);
   return (4 * (n & 1) - 2) * s;
 }

@@ -174,15 +174,16 @@ def perman_shard(mat, shard: int, nshards: int, kernel: str = "dense", device_id
 
 def plan_info(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1) -> dict:
     """The plan the engine runs for `kernel` (and options jit / gpu_num): walk
-    kind, column map, layout."""
+    kind, column map, layout, cached walk bits of the segmented walk."""
     a, dt, n = _mat(mat)
     lib = _lib.load()
-    kind, L, m = C.c_int(), C.c_int(), C.c_int()
+    kind, L, m, cc = C.c_int(), C.c_int(), C.c_int(), C.c_int()
     cm = np.zeros(max(n - 1, 1), np.int32)
     o = _opts(gpu_num=gpu_num, jit=jit)
     _lib.check(lib.sup_plan_info(a.ctypes.data, dt, n, _KERNELS[kernel], C.byref(o), C.byref(kind), cm.ctypes.data,
-                                 C.byref(L), C.byref(m)), "plan_info")
-    return {"kind": WALK_NAMES[kind.value], "colmap": cm[: n - 1].copy(), "L": L.value, "m": m.value}
+                                 C.byref(L), C.byref(m), C.byref(cc)), "plan_info")
+    return {"kind": WALK_NAMES[kind.value], "colmap": cm[: n - 1].copy(), "L": L.value, "m": m.value,
+            "cached": cc.value}
 
 
 def prepare(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1) -> dict:

@@ -144,7 +144,8 @@ def _declare(lib: C.CDLL) -> None:
                                 C.POINTER(SupStats)]
     lib.sup_perman_cpu.argtypes = [P, I, I, I, I, C.POINTER(D), C.POINTER(SupStats)]
     lib.sup_perman_shard.argtypes = [P, I, I, I, I, I, C.POINTER(SupOpts), C.POINTER(D), C.POINTER(SupStats)]
-    lib.sup_plan_info.argtypes = [P, I, I, I, C.POINTER(SupOpts), C.POINTER(I), P, C.POINTER(I), C.POINTER(I)]
+    lib.sup_plan_info.argtypes = [P, I, I, I, C.POINTER(SupOpts), C.POINTER(I), P, C.POINTER(I), C.POINTER(I),
+                                  C.POINTER(I)]
     lib.sup_prepare.argtypes = [P, I, I, I, C.POINTER(SupOpts), C.POINTER(I), C.POINTER(C.c_double)]
     lib.sup_nw_start.argtypes = [P, I, I, C.POINTER(D), C.POINTER(D)]
     lib.sup_read_matrix.argtypes = [C.c_char_p, I, C.POINTER(P), C.POINTER(I), C.POINTER(I), C.POINTER(I)]

@@ -195,7 +195,7 @@ int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int
 }
 
 int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o_in, int* walk_kind,
-                  int* colmap, int* L, int* m) {
+                  int* colmap, int* L, int* m, int* cached_bits) {
   std::vector<double> A;
   int rc = to_double(mat, t, n, A);
   if (rc) return rc;
@@ -205,6 +205,7 @@ int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const 
   Plan P;
   if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num))) return rc;
   if (walk_kind) *walk_kind = (int)P.kind;
+  if (cached_bits) *cached_bits = P.kind == kWalkSeg ? P.seg_cc : 0;
   if (colmap)
     for (int e = 0; e < n - 1; ++e) colmap[e] = P.colmap[e];
   if (L) *L = P.lay.L;

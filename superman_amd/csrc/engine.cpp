@@ -8,6 +8,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -281,6 +282,7 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
   }
   // ndev only feeds auto mode's compile-or-not decision
   const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0};
+  if (std::getenv("SUP_JIT_CC")) return plan_for_uncached(A, n, kernel, lay, P, jit, ndev);  // experiments
   {
     std::lock_guard<std::mutex> g(g_plan_mu);
     auto it = g_plans.find(key);

@@ -129,46 +129,79 @@ inline double tree_top(const ProdTree& t, const double* a, const TreeVal& v) {
 // Pair step j flips walk bit k = ctz(j) + 1; walk bits k <= seg_b use their
 // own touched rows, bits > seg_b one shared step over dyn_rows (the generated
 // kernel's straight-line step for those bits).
+// Cached walk bits 1..seg_cc: the kernel holds every value that depends on them
+// once per state of those bits and their steps only accumulate.  Restated here
+// as one full lane state per cached state S (copies of rows and nodes that do
+// not depend on a bit are equal in every state, computed from equal operands):
+// state S = state S' (S without its lowest bit, walk bit k) + the + column of
+// walk bit k on the rows it touches, then every non-cached step updates every
+// state the same way, and pair j accumulates with the state of its Gray bits.
+constexpr int kMaxCached = 2;
 struct SegLane {
-  double y[SUP_MAX_N], D;
-  TreeVal o, ix, iy;
+  double x[1 << kMaxCached][SUP_MAX_N], y[1 << kMaxCached][SUP_MAX_N], D[1 << kMaxCached];
+  TreeVal o[1 << kMaxCached], ix[1 << kMaxCached], iy[1 << kMaxCached];
 };
 
-void seg_init(Lane& s, SegLane& g, const Plan& P) {
-  const int len0 = P.seg_start[1];
-  for (int r = 0; r < len0; ++r) g.y[r] = s.x[r] + P.jtab[P.jofs[0] + r];
-  tree_init(P.outer_tree, s.x, g.o);
-  tree_init(P.inner_tree, s.x, g.ix);
-  tree_init(P.inner_tree, g.y, g.iy);
-  g.D = tree_top(P.inner_tree, s.x, g.ix) - tree_top(P.inner_tree, g.y, g.iy);
+void seg_init(const Lane& s, SegLane& g, const Plan& P) {
+  const int len0 = P.seg_start[1], NS = 1 << P.seg_cc;
+  std::copy(s.x, s.x + P.n, g.x[0]);
+  for (int r = 0; r < len0; ++r) g.y[0][r] = g.x[0][r] + P.jtab[P.jofs[0] + r];
+  for (int S = 1; S < NS; ++S) {
+    const int low = S & -S, k = __builtin_ctz(low) + 1;
+    std::copy(g.x[S ^ low], g.x[S ^ low] + P.n, g.x[S]);
+    std::copy(g.y[S ^ low], g.y[S ^ low] + len0, g.y[S]);
+    const std::vector<int>& t = P.touched[k];
+    for (size_t i = 0; i < t.size(); ++i) {
+      const double v = P.jtab[P.jofs[k] + i];
+      g.x[S][t[i]] = g.x[S ^ low][t[i]] + v;
+      if (t[i] < len0) g.y[S][t[i]] = g.y[S ^ low][t[i]] + v;
+    }
+  }
+  for (int S = 0; S < NS; ++S) {
+    tree_init(P.outer_tree, g.x[S], g.o[S]);
+    tree_init(P.inner_tree, g.x[S], g.ix[S]);
+    tree_init(P.inner_tree, g.y[S], g.iy[S]);
+    g.D[S] = tree_top(P.inner_tree, g.x[S], g.ix[S]) - tree_top(P.inner_tree, g.y[S], g.iy[S]);
+  }
 }
 
-void seg_step(Lane& s, SegLane& g, const Plan& P, int k, int neg) {
-  const int len0 = P.seg_start[1];
-  if (k > P.seg_b) {  // shared step: full signed column over dyn_rows (zeros included)
-    if (P.dyn_rows.empty()) return;
-    const double* c = col_of(P, P.lay.L + k, neg);
-    for (int r : P.dyn_rows) {
-      s.x[r] += c[r];
-      if (r < len0) g.y[r] += c[r];
+void seg_step(SegLane& g, const Plan& P, int k, int neg) {
+  const int len0 = P.seg_start[1], c = k <= P.seg_b ? k - 1 : P.seg_b;
+  if (c < P.seg_cc) return;  // cached walk bit: nothing changes
+  for (int S = 0; S < (1 << P.seg_cc); ++S) {
+    double* x = g.x[S];
+    double* y = g.y[S];
+    if (k > P.seg_b) {  // shared step: full signed column over dyn_rows (zeros included)
+      if (P.dyn_rows.empty()) return;
+      const double* col = col_of(P, P.lay.L + k, neg);
+      for (int r : P.dyn_rows) {
+        x[r] += col[r];
+        if (r < len0) y[r] += col[r];
+      }
+    } else {
+      const std::vector<int>& t = P.touched[k];
+      if (t.empty()) return;
+      const size_t blk = (t.size() + 7) & ~(size_t)7;
+      const double* v = P.jtab.data() + P.jofs[k] + (neg ? blk : 0);
+      for (size_t i = 0; i < t.size(); ++i) {
+        x[t[i]] += v[i];
+        if (t[i] < len0) y[t[i]] += v[i];
+      }
     }
-  } else {
-    const std::vector<int>& t = P.touched[k];
-    if (t.empty()) return;
-    const size_t blk = (t.size() + 7) & ~(size_t)7;
-    const double* v = P.jtab.data() + P.jofs[k] + (neg ? blk : 0);
-    for (size_t i = 0; i < t.size(); ++i) {
-      s.x[t[i]] += v[i];
-      if (t[i] < len0) g.y[t[i]] += v[i];
+    tree_update(P.outer_tree, x, g.o[S], c);
+    if ((P.inner_tree.root_sig() >> c) & 1u) {
+      tree_update(P.inner_tree, x, g.ix[S], c);
+      tree_update(P.inner_tree, y, g.iy[S], c);
+      g.D[S] = tree_top(P.inner_tree, x, g.ix[S]) - tree_top(P.inner_tree, y, g.iy[S]);
     }
   }
-  const int c = k <= P.seg_b ? k - 1 : P.seg_b;
-  tree_update(P.outer_tree, s.x, g.o, c);
-  if ((P.inner_tree.root_sig() >> c) & 1u) {
-    tree_update(P.inner_tree, s.x, g.ix, c);
-    tree_update(P.inner_tree, g.y, g.iy, c);
-    g.D = tree_top(P.inner_tree, s.x, g.ix) - tree_top(P.inner_tree, g.y, g.iy);
-  }
+}
+
+// cached state at pair index j: Gray bits 1..cc of the walk (pair bits 0..cc-1)
+inline int seg_state(uint32_t j, int cc) {
+  int S = 0;
+  for (int i = 0; i < cc; ++i) S |= (int)(((j >> i) ^ (j >> (i + 1))) & 1u) << i;
+  return S;
 }
 
 // One wave-chunk: returns the wave's pairwise lane sum.
@@ -186,11 +219,12 @@ double chunk_partial(const Plan& P, uint64_t ga) {
       chunk_start(P, ga, l, s);
       static thread_local SegLane g;
       seg_init(s, g, P);
-      double acc = g.D * tree_top(P.outer_tree, s.x, g.o);
+      double acc = g.D[0] * tree_top(P.outer_tree, g.x[0], g.o[0]);
       for (uint32_t j = 1; j < T / 2; ++j) {  // pair steps: walk bit ctz(j) + 1
         const uint32_t pb = __builtin_ctz(j);
-        seg_step(s, g, P, (int)pb + 1, (j >> (pb + 1)) & 1u);
-        acc = std::fma((j & 1u) ? -g.D : g.D, tree_top(P.outer_tree, s.x, g.o), acc);
+        seg_step(g, P, (int)pb + 1, (j >> (pb + 1)) & 1u);
+        const int S = seg_state(j, P.seg_cc);
+        acc = std::fma((j & 1u) ? -g.D[S] : g.D[S], tree_top(P.outer_tree, g.x[S], g.o[S]), acc);
       }
       const unsigned par = (unsigned)__builtin_popcount(l) & 1u;
       if ((((unsigned)ga) ^ par) & 1u) acc = -acc;

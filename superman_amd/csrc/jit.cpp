@@ -62,150 +62,42 @@ namespace {
 
 // ---------------------------------------------------------------- planning --
 
-struct SegShape {
-  std::vector<int> seg_start;               // boundaries, rows in first-touch order
-  std::vector<std::vector<int>> touched;    // per walk bit, engine rows
-};
-
-// Segment structure of walk columns `walk` (matrix columns, in walk-bit order):
-// rows are numbered in first-touch order.
-SegShape seg_shape(const double* A, int n, const std::vector<int>& walk) {
-  SegShape s;
-  std::vector<int> pos(n, -1);
-  int R = 0;
-  s.seg_start.push_back(0);
-  for (int c : walk) {
-    for (int i = 0; i < n; ++i)
-      if (pos[i] < 0 && A[(size_t)i * n + c] != 0.0) pos[i] = R++;
-    if (R > s.seg_start.back()) s.seg_start.push_back(R);
-  }
-  for (int c : walk) {
-    std::vector<int> t;
-    for (int i = 0; i < n; ++i)
-      if (A[(size_t)i * n + c] != 0.0) t.push_back(pos[i]);
-    std::sort(t.begin(), t.end());
-    s.touched.push_back(std::move(t));
-  }
-  return s;
-}
-
-int seg_index(const std::vector<int>& seg_start, int row) {
-  return (int)(std::upper_bound(seg_start.begin(), seg_start.end(), row) - seg_start.begin()) - 1;
-}
-
-// Segment 0 is split the same way as the whole matrix: its rows are ordered
-// by the first walk bit >= 1 that touches them (sub-segments), rows no such
-// bit touches last (constant within a wave-chunk).  Sub-segment of each
-// segment-0 row, -1 for the constant ones; *nsub, *srest = counts.
-std::vector<int> sub_of(const std::vector<int>& seg_start, const std::vector<std::vector<int>>& touched, int* nsub,
-                        int* srest) {
-  const int len0 = seg_start[1];
-  std::vector<int> sub(len0, -1);
-  int cnt = 0, ns = 0;
-  for (size_t k = 1; k < touched.size(); ++k) {
-    bool grew = false;
-    for (int r : touched[k])
-      if (r < len0 && sub[r] < 0) sub[r] = ns, ++cnt, grew = true;
-    if (grew) ++ns;
-  }
-  *nsub = ns;
-  *srest = len0 - cnt;
-  return sub;
-}
-
-// Ops of one chain update (segments of sizes len[], constant tail present or
-// not) for dirty segments `dirty` up to `smax`: (len - 1) muls per dirty
-// segment of the tree, one chain mul per segment (none for the last one
-// without a tail).
-double chain_ops(const std::vector<int>& len, bool tail, const std::vector<char>& dirty, int smax) {
-  double ops = 0.0;
-  const int ns = (int)len.size();
-  for (int i = 0; i <= smax; ++i) {
-    if (dirty[i]) ops += len[i] - 1;
-    if (i < ns - 1 || tail) ops += 1.0;
-  }
-  return ops;
-}
-
-// VALU ops of one pair step flipping a walk bit k >= 1 that touches rows t
-// (the generated code, exactly): |t| adds, plus one more per touched row of
-// segment 0 (its bit-0-set copy y); the outer chain over segments >= 1; when
-// segment 0 is touched, its sub-segment chains for x and for y and their
-// difference D; one fma into the accumulator.
-double step_ops(const std::vector<int>& seg_start, int n, const std::vector<int>& t, const std::vector<int>& sub,
-                int nsub, int srest) {
-  if (t.empty()) return 1.0;
-  const int nseg = (int)seg_start.size() - 1, len0 = seg_start[1];
-  std::vector<int> olen;
-  for (int i = 1; i < nseg; ++i) olen.push_back(seg_start[i + 1] - seg_start[i]);
-  std::vector<int> slen(nsub, 0);
-  for (int r = 0; r < len0; ++r)
-    if (sub[r] >= 0) ++slen[sub[r]];
-  std::vector<char> od(std::max(nseg - 1, 1), 0), sd(std::max(nsub, 1), 0);
-  int omax = -1, smax = -1;
-  double ops = (double)t.size() + 1.0;
-  for (int r : t) {
-    if (r < len0) {
-      ops += 1.0;
-      sd[sub[r]] = 1;
-      smax = std::max(smax, sub[r]);
-    } else {
-      const int i = seg_index(seg_start, r) - 1;
-      od[i] = 1;
-      omax = std::max(omax, i);
-    }
-  }
-  if (omax >= 0) ops += chain_ops(olen, seg_start.back() < n, od, omax);
-  if (smax >= 0) ops += 2.0 * chain_ops(slen, srest > 0, sd, smax) + 1.0;
-  return ops;
-}
-
-// Gray steps come in pairs that differ in walk bit 0 only, so a pair step
-// flips walk bit k >= 1 (pair bit k-1); pair bits p < b get a specialised
-// step each, bits p >= b (1/2^b of the pair steps) share one step over the
-// union of their rows.  Ops per Gray step = ops per pair step / 2.
-double cost_of(const std::vector<int>& seg_start, int n, const std::vector<std::vector<int>>& touched) {
-  const int m = (int)touched.size(), b = seg_static_bits(m);
-  int nsub = 0, srest = 0;
-  const std::vector<int> sub = sub_of(seg_start, touched, &nsub, &srest);
-  std::vector<char> in(n, 0);
-  for (int k = b + 1; k < m; ++k)
-    for (int r : touched[k]) in[r] = 1;
-  std::vector<int> dyn;
-  for (int j = 0; j < n; ++j)
-    if (in[j]) dyn.push_back(j);
-  const double dyn_ops = step_ops(seg_start, n, dyn, sub, nsub, srest);
-  double c = 0.0, w = 0.5;
-  for (int p = 0; p + 1 < m; ++p, w *= 0.5)
-    c += w * (p < b ? step_ops(seg_start, n, touched[p + 1], sub, nsub, srest) : dyn_ops);
-  return c / 2.0;
-}
-
-double shape_cost(const SegShape& s, int n) { return cost_of(s.seg_start, n, s.touched); }
-
 // Step class of walk bit k >= 1: k - 1 for the specialised pair bits, seg_b
 // for the shared step of the walk bits above them.
 int step_class(int k, int b) { return k <= b ? k - 1 : b; }
 
-// Greedy product tree over rows [lo, tail_lo) (+ the constant item for rows
-// [tail_lo, tail_hi)): repeatedly join the two clusters whose union is dirty
-// least often, i.e. minimise w(sig_i | sig_j) with w(class c) = 2^(b-1-c) (walk
-// bit c+1 flips on 2^-(c+1) of the pair steps) and w(shared) = 1; ties -> the
-// first pair (i < j) in list order; the joined cluster goes to the end.  Rows
-// that always change together end up under one node, so a step re-forms only
-// the nodes above the rows it touches (the first-touch chain it replaces had
-// to re-form whole segments and every link above them).
-ProdTree make_tree(const std::vector<uint32_t>& rsig, int lo, int tail_lo, int tail_hi, int b) {
+// Copies of a value whose step classes are `sig`: one per state of the cached
+// classes (the lowest cc classes) it depends on.
+inline int copies(uint32_t sig, int cc) { return 1 << __builtin_popcount(sig & ((1u << cc) - 1u)); }
+
+// Dirty weight of a step-class set: how often (x 2^b per pair step) a value
+// with these classes is re-formed, times its copies.  Cached classes never
+// re-form anything; class c < b flips on 2^-(c+1) of the pair steps, the
+// shared class on ~2^-b.
+struct ClassWeights {
+  uint64_t w[64];
+  ClassWeights(int b, int cc) {
+    for (uint32_t s = 0; s < 64; ++s) {
+      uint64_t v = 0;
+      for (int c = cc; c <= b && c < 6; ++c)
+        if ((s >> c) & 1u) v += c < b ? (1ull << (b - 1 - c)) : 1ull;
+      w[s] = v * (uint64_t)copies(s, cc);
+    }
+  }
+};
+
+// Greedy product tree over the item rows `rows` (+ one constant item for the
+// rows [tail_lo, tail_hi), which no walk bit >= 1 touches): repeatedly join the
+// two clusters whose union is cheapest to keep, i.e. minimise W(sig_i | sig_j)
+// (ClassWeights); ties -> the first pair (i < j) in list order; the joined
+// cluster goes to the end.  Rows that change together end up under one node,
+// so a step re-forms only the nodes above the rows it touches.
+ProdTree make_tree(const std::vector<int>& rows, const std::vector<uint32_t>& rsig, int tail_lo, int tail_hi,
+                   const ClassWeights& W) {
   ProdTree t;
   t.tail_lo = tail_lo, t.tail_hi = tail_hi;
-  for (int r = lo; r < tail_lo; ++r) t.item_row.push_back(r), t.item_sig.push_back(rsig[r]);
+  for (int r : rows) t.item_row.push_back(r), t.item_sig.push_back(rsig[r]);
   if (tail_hi > tail_lo) t.item_row.push_back(-1), t.item_sig.push_back(0u);
-  auto weight = [b](uint32_t s) {
-    uint64_t w = 0;
-    for (int c = 0; c <= b; ++c)
-      if ((s >> c) & 1u) w += c < b ? (1ull << (b - 1 - c)) : 1ull;
-    return w;
-  };
   std::vector<int> id;
   std::vector<uint32_t> sg;
   for (int i = 0; i < t.items(); ++i) id.push_back(i), sg.push_back(t.item_sig[i]);
@@ -214,7 +106,7 @@ ProdTree make_tree(const std::vector<uint32_t>& rsig, int lo, int tail_lo, int t
     uint64_t bw = UINT64_MAX;
     for (size_t i = 0; i < id.size(); ++i)
       for (size_t j = i + 1; j < id.size(); ++j) {
-        const uint64_t w = weight(sg[i] | sg[j]);
+        const uint64_t w = W.w[(sg[i] | sg[j]) & 63u];
         if (w < bw) bw = w, bi = i, bj = j;
       }
     const uint32_t ns = sg[bi] | sg[bj];
@@ -226,33 +118,136 @@ ProdTree make_tree(const std::vector<uint32_t>& rsig, int lo, int tail_lo, int t
   return t;
 }
 
-int nodes_with(const ProdTree& t, int c) {
-  int k = 0;
-  for (uint32_t s : t.sig) k += (s >> c) & 1u;
-  return k;
+// Signature of node i's parent (-1 for the root): a node dirty exactly when
+// its parent is need not stay live between steps.
+int parent_sig(const ProdTree& t, int i) {
+  const int id = t.items() + i;
+  for (int j = i + 1; j < t.K(); ++j)
+    if (t.a[j] == id || t.b[j] == id) return (int)t.sig[j];
+  return -1;
+}
+
+// The segmented walk's structure in engine rows (rows in seg_row_order):
+// touched[k] = rows walk bit k touches; segment 0 = rows [0, len0) (walk bit
+// 0's rows; [0, s_end) touched by some walk bit >= 1, [s_end, len0) not);
+// other rows [len0, r_end) touched by some walk bit >= 1, [r_end, n) by none.
+struct SegRows {
+  int n = 0, m = 0, b = 0, len0 = 0, s_end = 0, r_end = 0;
+  std::vector<std::vector<int>> touched;
+  std::vector<int> dyn_rows;      // rows of walk bits > b (the shared step)
+  std::vector<uint32_t> rsig;     // step classes of each row
+};
+
+void seg_rows_finish(SegRows& R) {
+  R.b = std::min(R.m - 1, 5);  // seg_static_bits
+  R.rsig.assign(R.n, 0u);
+  std::vector<char> dyn(R.n, 0);
+  for (int k = 1; k < R.m; ++k)
+    for (int r : R.touched[k]) {
+      R.rsig[r] |= 1u << step_class(k, R.b);
+      if (k > R.b) dyn[r] = 1;
+    }
+  R.dyn_rows.clear();
+  for (int r = 0; r < R.n; ++r)
+    if (dyn[r]) R.dyn_rows.push_back(r);
+}
+
+struct SegFit {
+  int cc = 0;
+  double ops = 1e300;   // fp64 VALU ops per Gray step (the generated code, exactly)
+  int regs = 0;         // values live across steps (doubles), estimate
+  ProdTree outer, inner;
+};
+
+// Trees, cost and live values with cc cached classes.
+SegFit seg_fit(const SegRows& R, int cc) {
+  SegFit f;
+  f.cc = cc;
+  const ClassWeights W(R.b, cc);
+  std::vector<int> orow, irow;
+  for (int r = R.len0; r < R.r_end; ++r) orow.push_back(r);
+  for (int r = 0; r < R.s_end; ++r) irow.push_back(r);
+  f.outer = make_tree(orow, R.rsig, R.r_end, R.n, W);
+  f.inner = make_tree(irow, R.rsig, R.s_end, R.len0, W);
+  // ops per pair step of class c: the row adds (all copies, y too), the
+  // dirty nodes (all copies; segment 0's over x and over y), D, the fma
+  double c = 0.0, w = 0.5;
+  for (int p = 0; p + 1 < R.m; ++p, w *= 0.5) {
+    const int k = p + 1, cl = step_class(k, R.b);
+    double ops = 1.0;
+    if (cl >= cc) {
+      for (int r : (k <= R.b ? R.touched[k] : R.dyn_rows)) ops += copies(R.rsig[r], cc) * (r < R.len0 ? 2.0 : 1.0);
+      for (int i = 0; i < f.outer.K(); ++i)
+        if ((f.outer.sig[i] >> cl) & 1u) ops += copies(f.outer.sig[i], cc);
+      for (int i = 0; i < f.inner.K(); ++i)
+        if ((f.inner.sig[i] >> cl) & 1u) ops += 2.0 * copies(f.inner.sig[i], cc);
+      if ((f.inner.root_sig() >> cl) & 1u) ops += copies(f.inner.root_sig(), cc);
+    }
+    c += w * ops;
+  }
+  f.ops = c / 2.0;
+  // live across steps: rows (x, y on segment 0) with their copies, the nodes
+  // whose parent is not re-formed with them, D, acc and loop state
+  int regs = 6 + copies(f.inner.root_sig(), cc);
+  for (int r = 0; r < R.n; ++r) regs += copies(R.rsig[r], cc) * (r < R.len0 ? 2 : 1);
+  for (const ProdTree* t : {&f.outer, &f.inner})
+    for (int i = 0; i < t->K(); ++i) {
+      const int ps = parent_sig(*t, i);
+      if (ps < 0 || (uint32_t)ps != t->sig[i]) regs += copies(t->sig[i], cc) * (t == &f.inner ? 2 : 1);
+    }
+  f.regs = regs;
+  return f;
+}
+
+// Live-value budgets (seg_fit's estimate, doubles): <= kRegs3 fits 3 waves
+// per SIMD (168 VGPRs), <= kRegsMax fits 2 (256 VGPRs) without spills.  The
+// estimate runs ~10% above what the compiler allocates (n = 40 bench matrix:
+// 102 -> 188 VGPRs, 142 -> 246 VGPRs no spill, 205 -> 175 spilled VGPRs).
+// Occupancy 2 costs ~2% against 3 on this walk (measured, n = 40), 1 ~35%.
+constexpr int kRegs3 = 90, kRegsMax = 142;
+constexpr double kOcc2Penalty = 1.02;
+
+// Best number of cached classes (0 .. min(2, b-1)) within the register budget.
+SegFit seg_best(const SegRows& R, int cc_max = 2) {
+  SegFit best = seg_fit(R, 0);
+  double bscore = best.ops * (best.regs <= kRegs3 ? 1.0 : kOcc2Penalty);
+  for (int cc = 1; cc <= std::min(cc_max, R.b - 1); ++cc) {
+    SegFit f = seg_fit(R, cc);
+    if (f.regs > kRegsMax) continue;
+    const double score = f.ops * (f.regs <= kRegs3 ? 1.0 : kOcc2Penalty);
+    if (score < bscore) bscore = score, best = std::move(f);
+  }
+  return best;
+}
+
+// SegRows of walk columns `walk` in the engine row order make_plan uses.
+SegRows seg_rows_of(const double* A, int n, const std::vector<int>& walk) {
+  SegRows R;
+  R.n = n, R.m = (int)walk.size();
+  const std::vector<int> order = seg_row_order(A, n, walk);
+  auto nz = [&](int row, int c) { return A[(size_t)row * n + c] != 0.0; };
+  R.touched.assign(R.m, {});
+  std::vector<char> any1(n, 0);
+  for (int k = 0; k < R.m; ++k)
+    for (int j = 0; j < n; ++j)
+      if (nz(order[j], walk[k])) {
+        R.touched[k].push_back(j);
+        if (k >= 1) any1[j] = 1;
+      }
+  R.len0 = (int)R.touched[0].size();
+  R.s_end = 0;
+  while (R.s_end < R.len0 && any1[R.s_end]) ++R.s_end;
+  R.r_end = R.len0;
+  while (R.r_end < n && any1[R.r_end]) ++R.r_end;
+  seg_rows_finish(R);
+  return R;
 }
 
 }  // namespace
 
 int seg_static_bits(int m) { return std::min(m - 1, 5); }
 
-// Ops per Gray step of the generated kernel, exactly: per pair step of class
-// c, the adds of its rows (twice on segment 0), the dirty outer nodes, the
-// dirty inner nodes over x and over y, D when segment 0 changed, the fma.
-double seg_walk_cost(const Plan& P) {
-  const int m = P.lay.m, b = P.seg_b, len0 = P.seg_start[1];
-  double c = 0.0, w = 0.5;
-  for (int p = 0; p + 1 < m; ++p, w *= 0.5) {
-    const int k = p + 1, cl = step_class(k, b);
-    const std::vector<int>& t = k <= b ? P.touched[k] : P.dyn_rows;
-    double ops = 1.0 + (double)t.size();
-    for (int r : t) ops += r < len0;
-    ops += nodes_with(P.outer_tree, cl) + 2.0 * nodes_with(P.inner_tree, cl);
-    ops += (P.inner_tree.root_sig() >> cl) & 1u;
-    c += w * ops;
-  }
-  return c / 2.0;
-}
+double seg_walk_cost(const Plan& P) { return P.seg_ops; }
 
 std::vector<int> seg_walk_order(const double* A, int n, int m, int count) {
   const int nb = n - 1;
@@ -282,10 +277,14 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count) {
     }
     return order;
   };
-  // walk bit 0 defines segment 0 (the paired rows): it must touch a row
+  // the exact op count of the generated code (best cached-class count within
+  // the register budget); walk bit 0 defines segment 0 (the paired rows) and
+  // must touch a row
   auto cost = [&](const std::vector<int>& o) {
     if (nnz[o[0]] == 0) return 1e300;
-    return shape_cost(seg_shape(A, n, std::vector<int>(o.begin(), o.begin() + m)), n);
+    if (m < 3) return 0.0;
+    const SegFit f = seg_best(seg_rows_of(A, n, std::vector<int>(o.begin(), o.begin() + m)));
+    return f.ops * (f.regs <= kRegs3 ? 1.0 : kOcc2Penalty);
   };
   std::vector<int> best;
   double bcost = 1e300;
@@ -297,8 +296,8 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count) {
   if (m == 0) return extend({}, count);
   // descent: swap a walk position with another walk position or an unused
   // column while the cost drops (positions whose weight 2^-(k+1) is visible)
-  const int hot = std::min(m, 12);
-  for (int pass = 0; pass < 8; ++pass) {
+  const int hot = std::min(m, 8);
+  for (int pass = 0; pass < 6; ++pass) {
     bool improved = false;
     for (int a = 0; a < hot; ++a) {
       for (int c = 0; c < nb; ++c) {
@@ -342,27 +341,47 @@ std::string tree(int lo, int hi, const char* v = "x") {
   return "(" + tree(lo, mid, v) + " * " + tree(mid, hi, v) + ")";
 }
 
-// Signature of node i's parent (-1 for the root): a node dirty exactly when
-// its parent is need not stay live between steps.
-int parent_sig(const ProdTree& t, int i) {
-  const int id = t.items() + i;
-  for (int j = i + 1; j < t.K(); ++j)
-    if (t.a[j] == id || t.b[j] == id) return (int)t.sig[j];
-  return -1;
-}
+// Values in the generated code.  With cc cached classes every value exists
+// once per state of the cached walk bits it depends on (copy index = that
+// state masked to its classes): row r's copy i is x[r] (i = 0) or x<r>_<i>,
+// y likewise; node i of a tree is <N><i>_<copy>; constant items are <T>.
+struct Names {
+  uint32_t ccmask = 0;
+  std::string X(int r, uint32_t s, uint32_t rsig, const char* arr) const {
+    const uint32_t i = s & rsig & ccmask;
+    return i ? std::string(arr) + std::to_string(r) + "_" + std::to_string(i)
+             : std::string(arr) + "[" + std::to_string(r) + "]";
+  }
+};
 
-// Names of one product tree's values in the generated code: items are the
-// row array `arr` and the constant item `T`; node i is `N<i>`.
 struct TreeNames {
   const ProdTree* t;
+  const Names* nm;
+  const std::vector<uint32_t>* rsig;
   std::string arr, N, T;
-  std::string id(int i) const {
-    if (i < t->items()) return t->item_row[i] < 0 ? T : arr + "[" + std::to_string(t->item_row[i]) + "]";
-    return N + std::to_string(i - t->items());
+  uint32_t csig(int id) const {
+    const uint32_t s = id < t->items() ? t->item_sig[id] : t->sig[id - t->items()];
+    return s & nm->ccmask;
   }
-  std::string top() const { return t->root() < 0 ? std::string() : id(t->root()); }
-  std::string node(int i) const { return id(t->a[i]) + " * " + id(t->b[i]); }
+  std::string id(int i, uint32_t s) const {
+    if (i < t->items()) {
+      const int r = t->item_row[i];
+      return r < 0 ? T : nm->X(r, s, (*rsig)[r], arr.c_str());
+    }
+    return N + std::to_string(i - t->items()) + "_" + std::to_string(s & csig(i));
+  }
+  std::string top(uint32_t s) const { return t->root() < 0 ? std::string() : id(t->root(), s); }
+  std::string node(int i, uint32_t s) const { return id(t->a[i], s) + " * " + id(t->b[i], s); }
+  uint32_t root_csig() const { return t->root() < 0 ? 0u : csig(t->root()); }
 };
+
+// submasks of m in increasing order (0 included)
+std::vector<uint32_t> submasks(uint32_t m) {
+  std::vector<uint32_t> v;
+  for (uint32_t s = 0; s <= m; ++s)
+    if ((s & ~m) == 0) v.push_back(s);
+  return v;
+}
 
 // Generated kernel (paired segmented walk).  Gray steps 2j and 2j+1 differ in
 // walk bit 0 only, so they are evaluated together: segment 0 (the rows walk
@@ -371,37 +390,56 @@ struct TreeNames {
 // the product of every other row.  The pair walk is a Gray walk over walk
 // bits 1..m-1 (pair bit p = walk bit p+1).  Both products are product trees
 // (make_tree): a step re-forms the nodes above the rows it touches.
+// Cached classes (walk bits 1..cc): every value that depends on them is held
+// in each of their states, so their pair steps only accumulate (the state is
+// known at compile time inside the unrolled block) and every other step
+// updates all copies.
 struct Gen {
   const Plan& P;
   int len0;
+  std::vector<uint32_t> rsig;
+  Names nm;
   TreeNames outer, inx, iny;
   std::ostringstream o;
-  explicit Gen(const Plan& p) : P(p), len0(p.seg_start[1]) {
-    outer = {&p.outer_tree, "x", "o", "Ro"};
-    inx = {&p.inner_tree, "x", "px", "Cx"};
-    iny = {&p.inner_tree, "y", "py", "Cy"};
+  explicit Gen(const Plan& p) : P(p), len0(p.seg_start[1]), rsig(p.n, 0u) {
+    for (int k = 1; k < p.lay.m; ++k)
+      for (int r : p.touched[k]) rsig[r] |= 1u << step_class(k, p.seg_b);
+    nm.ccmask = (1u << p.seg_cc) - 1u;
+    outer = {&p.outer_tree, &nm, &rsig, "x", "o", "Ro"};
+    inx = {&p.inner_tree, &nm, &rsig, "x", "px", "Cx"};
+    iny = {&p.inner_tree, &nm, &rsig, "y", "py", "Cy"};
   }
 
   void tree_init(const TreeNames& t, const char* ind) {
     if (t.t->tail_hi > t.t->tail_lo)
       o << ind << "const double " << t.T << " = " << tree(t.t->tail_lo, t.t->tail_hi, t.arr.c_str()) << ";\n";
-    for (int i = 0; i < t.t->K(); ++i) o << ind << "double " << t.N << i << " = " << t.node(i) << ";\n";
+    for (int i = 0; i < t.t->K(); ++i)
+      for (uint32_t s : submasks(t.csig(t.t->items() + i)))
+        o << ind << "double " << t.N << i << "_" << s << " = " << t.node(i, s) << ";\n";
   }
-  // re-form the nodes of step class c; returns whether the root changed
+  // re-form the nodes of step class c (every copy); returns whether the root changed
   bool tree_update(const TreeNames& t, int c, const char* ind) {
     for (int i = 0; i < t.t->K(); ++i)
-      if ((t.t->sig[i] >> c) & 1u) o << ind << "  " << t.N << i << " = " << t.node(i) << ";\n";
+      if ((t.t->sig[i] >> c) & 1u)
+        for (uint32_t s : submasks(t.csig(t.t->items() + i)))
+          o << ind << "  " << t.N << i << "_" << s << " = " << t.node(i, s) << ";\n";
     return (t.t->root_sig() >> c) & 1u;
   }
-  std::string dexpr() const { return inx.top() + " - " + iny.top(); }
-  void accumulate(bool neg, const char* ind) {
-    if (outer.top().empty()) o << ind << (neg ? "acc -= D;\n" : "acc += D;\n");
-    else o << ind << "acc = __builtin_fma(" << (neg ? "-D" : "D") << ", " << outer.top() << ", acc);\n";
+  std::string dname(uint32_t s) const { return "D" + std::to_string(s & inx.root_csig()); }
+  void set_d(const char* ind, bool decl) {
+    for (uint32_t s : submasks(inx.root_csig()))
+      o << ind << (decl ? "double " : "") << dname(s) << " = " << inx.top(s) << " - " << iny.top(s) << ";\n";
+  }
+  // accumulate pair term with cached state S
+  void accumulate(bool neg, uint32_t S, const char* ind) {
+    const std::string D = dname(S), U = outer.top(S);
+    if (U.empty()) o << ind << "acc " << (neg ? "-= " : "+= ") << D << ";\n";
+    else o << ind << "acc = __builtin_fma(" << (neg ? "-" : "") << D << ", " << U << ", acc);\n";
   }
 
-  // Add the values at table pointer `cv` (dbl8 pieces) to rows `rows` (and
-  // to their y copies in segment 0): value i of the block belongs to row
-  // rows[i] (packed table), or value rows[i] of the block (full column,
+  // Add the values at table pointer `cv` (dbl8 pieces) to rows `rows` (every
+  // copy, and their y copies in segment 0): value i of the block belongs to
+  // row rows[i] (packed table), or value rows[i] of the block (full column,
   // `full`).  At most 2 pieces (32 SGPRs) are pinned at a time.
   void adds(const std::vector<int>& rows, bool full, const char* ind) {
     std::vector<std::pair<int, int>> vr;  // (value index, row)
@@ -418,8 +456,11 @@ struct Gen {
       for (auto& e : vr)
         if (e.first / 8 >= pieces[g] && e.first / 8 <= pieces[ge - 1]) {
           const std::string v = "v" + std::to_string(e.first / 8) + "[" + std::to_string(e.first % 8) + "]";
-          o << ind << "  x[" << e.second << "] += " << v << ";\n";
-          if (e.second < len0) o << ind << "  y[" << e.second << "] += " << v << ";\n";
+          const int r = e.second;
+          for (uint32_t s : submasks(rsig[r] & nm.ccmask)) {
+            o << ind << "  " << nm.X(r, s, rsig[r], "x") << " += " << v << ";\n";
+            if (r < len0) o << ind << "  " << nm.X(r, s, rsig[r], "y") << " += " << v << ";\n";
+          }
         }
       if (ge < pieces.size()) o << ind << "  __builtin_amdgcn_sched_barrier(0);\n";
     }
@@ -429,7 +470,7 @@ struct Gen {
     tree_update(outer, c, ind);
     if (tree_update(inx, c, ind)) {
       tree_update(iny, c, ind);
-      o << ind << "  D = " << dexpr() << ";\n";
+      set_d((std::string(ind) + "  ").c_str(), false);
     }
   }
 
@@ -453,29 +494,29 @@ struct Gen {
     return std::to_string(P.jofs[k] * 8) + "u + " + negv + " * " + std::to_string(blk * 8) + "u";
   }
 
+  // cached state (walk bits 1..cc) at pair index j with j mod B = st:
+  // gray bit i = bit i ^ bit i+1 of st (i + 1 < b)
+  uint32_t state(unsigned st) const {
+    uint32_t S = 0;
+    for (int i = 0; i < P.seg_cc; ++i) S |= (((st >> i) ^ (st >> (i + 1))) & 1u) << i;
+    return S;
+  }
+
   std::string source() {
-    const int n = P.n, L = P.lay.L, m = P.lay.m, b = P.seg_b;
+    const int n = P.n, L = P.lay.L, m = P.lay.m, b = P.seg_b, cc = P.seg_cc;
     const unsigned B = 1u << b, Q = 1u << (m - 1 - b);
     o << "// generated by superman_amd jit.cpp: paired segmented Gray walk, n=" << n << " L=" << L << " m=" << m
       << " segment0=" << len0 << " (" << P.inner_tree.K() << " tree nodes) outer tree nodes=" << P.outer_tree.K()
-      << " pair bits specialised=" << b << "\n";
+      << " pair bits specialised=" << b << " cached=" << cc << " live values~" << P.seg_regs << "\n";
     o << "#include \"walk_common.hpp\"\n";
     o << "namespace sup {\n";
     o << "typedef double jdbl8 __attribute__((ext_vector_type(8)));\n";
     o << "typedef const __attribute__((address_space(4))) jdbl8 cjdbl8;\n";
-    // occupancy target from the values live across the walk loop (x, y,
-    // chain values, D, acc, loop state; 2 VGPRs each): the compiler's own
-    // choice trades occupancy 2 for scheduling freedom, which costs more
-    // latency hiding than it buys.  SUP_JIT_WAVES overrides (experiments).
-    int vals = n + len0 + 4;
-    for (const TreeNames* t : {&outer, &inx, &iny}) {  // nodes kept across steps
-      vals += t->t->tail_hi > t->t->tail_lo;
-      for (int i = 0; i < t->t->K(); ++i) {
-        const int par = parent_sig(*t->t, i);
-        vals += par < 0 || (uint32_t)par != t->t->sig[i];
-      }
-    }
-    int waves = 2 * vals <= 116 ? 4 : 3;  // (occupancy 2 is never worth it: measured)
+    // occupancy target from the values live across the walk loop (seg_fit's
+    // estimate): 3 waves per SIMD when they fit 168 VGPRs, else 2 (~2% slower
+    // on this walk; the compiler's own choice may trade occupancy for
+    // scheduling freedom).  SUP_JIT_WAVES overrides (experiments).
+    int waves = P.seg_regs <= 64 ? 4 : (P.seg_regs <= kRegs3 ? 3 : 2);
     if (const char* e = std::getenv("SUP_JIT_WAVES")) waves = std::max(1, std::min(8, std::atoi(e)));
     o << "extern \"C\" __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(" << waves
       << "))) void sup_walk_seg(WalkParams p) {\n";
@@ -495,32 +536,54 @@ struct Gen {
     o << "        cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off_const(0, 0) << ");\n";
     for (int r = 0; r < len0; ++r) o << "        y[" << r << "] = x[" << r << "] + cv[" << r / 8 << "][" << r % 8 << "];\n";
     o << "      }\n";
+    // copies for the cached states: copy i = copy (i without its lowest bit)
+    // + the + column of that bit's walk bit (rows it touches)
+    for (int r = 0; r < n; ++r)
+      for (uint32_t s : submasks(rsig[r] & nm.ccmask)) {
+        if (!s) continue;
+        const uint32_t low = s & (0u - s);
+        const int k = __builtin_ctz(low) + 1;
+        const auto& t = P.touched[k];
+        const int pos = (int)(std::lower_bound(t.begin(), t.end(), r) - t.begin());
+        const std::string v = "((cjdbl8*)opaque_c(p.jtab, " + off_const(k, 0) + "))[" + std::to_string(pos / 8) +
+                              "][" + std::to_string(pos % 8) + "]";
+        o << "      double " << nm.X(r, s, rsig[r], "x") << " = " << nm.X(r, s ^ low, rsig[r], "x") << " + " << v
+          << ";\n";
+        if (r < len0)
+          o << "      double " << nm.X(r, s, rsig[r], "y") << " = " << nm.X(r, s ^ low, rsig[r], "y") << " + " << v
+            << ";\n";
+      }
     tree_init(outer, "      ");
     tree_init(inx, "      ");
     tree_init(iny, "      ");
-    o << "      double D = " << dexpr() << ";\n";
-    o << "      double acc = " << (outer.top().empty() ? std::string("D") : "D * " + outer.top()) << ";\n";
+    set_d("      ", true);
+    {
+      const std::string U = outer.top(0);
+      o << "      double acc = " << (U.empty() ? dname(0) : dname(0) + " * " + U) << ";\n";
+    }
     o << "      for (uint32_t q = 0; q < " << Q << "u; ++q) {\n";
     const char* ind = "        ";
     // pair index j = B*q + s, s = 1 .. B-1: pair bit p = ctz(s) (walk bit p+1);
     // neg = (j >> (p+1)) & 1 = bit p+1 of s for p < b-1, bit 0 of q for p = b-1
     for (unsigned st = 1; st < B; ++st) {
       const int pb = __builtin_ctz(st);
-      if (pb < b - 1) {
+      if (pb < cc) {
+        // cached walk bit: its state's copies are already there
+      } else if (pb < b - 1) {
         step(pb + 1, off_const(pb + 1, (st >> (pb + 1)) & 1u), ind);
       } else {
         o << ind << "{\n" << ind << "  const uint32_t ng = q & 1u;\n";
         step(pb + 1, off_dyn(pb + 1, "ng"), "          ");
         o << ind << "}\n";
       }
-      accumulate(st & 1u, ind);
+      accumulate(st & 1u, state(st), ind);
     }
     if (Q > 1) {
       // j = B(q+1): pair bit b + ctz(q+1) (walk bit b+1+ctz(q+1)), neg =
       // ((q+1) >> (ctz(q+1)+1)) & 1.  One straight-line step for all of them
       // (no per-bit branches): the full signed column is added to every row
-      // some walk bit > b touches (zeros elsewhere) and every segment such a
-      // row lies in is re-multiplied.
+      // some walk bit > b touches (zeros elsewhere) and every node above such
+      // a row is re-formed.  Cached state 0.
       o << ind << "if (q + 1u < " << Q << "u) {\n";
       o << ind << "  const uint32_t kk = (uint32_t)__builtin_ctz(q + 1u);\n";
       o << ind << "  const uint32_t ng = ((q + 1u) >> (kk + 1u)) & 1u;\n";
@@ -528,7 +591,7 @@ struct Gen {
         << P.NP * 8 << "u);\n";
       adds(P.dyn_rows, true, ind);
       products(P.seg_b, ind);
-      accumulate(false, "          ");
+      accumulate(false, 0u, "          ");
       o << ind << "}\n";
     }
     o << "      }\n";
@@ -613,13 +676,19 @@ int build_seg(Plan& P) {
     for (int j = 0; j < n; ++j)
       if (in[j]) P.dyn_rows.push_back(j);
   }
-  {  // product trees: rows outside segment 0 and segment 0's rows, by step class
-    std::vector<uint32_t> rsig(n, 0u);
-    for (int k = 1; k < m; ++k)
-      for (int r : P.touched[k]) rsig[r] |= 1u << step_class(k, P.seg_b);
-    const int len0 = P.seg_start[1];
-    P.outer_tree = make_tree(rsig, len0, P.seg_start.back(), n, P.seg_b);
-    P.inner_tree = make_tree(rsig, 0, P.sub_start.back(), len0, P.seg_b);
+  {  // product trees and cached classes (seg_best; SUP_JIT_CC forces cc, experiments)
+    SegRows R;
+    R.n = n, R.m = m, R.touched = P.touched;
+    R.len0 = P.seg_start[1], R.s_end = P.sub_start.back(), R.r_end = P.seg_start.back();
+    seg_rows_finish(R);
+    SegFit f;
+    if (const char* e = std::getenv("SUP_JIT_CC")) f = seg_fit(R, std::max(0, std::min({std::atoi(e), R.b - 1, 2})));
+    else f = seg_best(R);
+    P.outer_tree = std::move(f.outer);
+    P.inner_tree = std::move(f.inner);
+    P.seg_cc = f.cc;
+    P.seg_ops = f.ops;
+    P.seg_regs = f.regs;
   }
   P.jofs.assign(m, 0);
   P.jtab.clear();
@@ -650,6 +719,13 @@ std::map<uint64_t, std::shared_ptr<std::vector<char>>> g_code;        // key -> 
 std::map<std::pair<int, uint64_t>, hipFunction_t> g_fn;               // (device, key) -> kernel
 std::map<std::pair<int, uint64_t>, int> g_occ;
 double g_compile_ms = 0.0;
+
+// SUP_JIT_LDS (experiments): dynamic LDS bytes per block, to cap residency
+// and measure the walk's sensitivity to occupancy.
+unsigned jit_lds_bytes() {
+  const char* e = std::getenv("SUP_JIT_LDS");
+  return e ? (unsigned)std::strtoul(e, nullptr, 10) : 0u;
+}
 
 std::string cache_dir() {
   const char* e = std::getenv("SUP_JIT_CACHE_DIR");
@@ -803,7 +879,7 @@ int jit_occupancy(int dev, const Plan& P, int* blocks_per_cu, double* compile_ms
     return SUP_OK;
   }
   int b = 0;
-  hipError_t e = hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kBlock, 0);
+  hipError_t e = hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&b, fn, kBlock, jit_lds_bytes());
   if (e != hipSuccess) {
     set_error(std::string("occupancy query (segmented walk): ") + hipGetErrorString(e));
     return SUP_EHIP;
@@ -819,7 +895,7 @@ int jit_launch(int dev, const Plan& P, const WalkParams& p, int grid, hipStream_
   if (rc) return rc;
   WalkParams arg = p;
   void* args[] = {&arg};
-  hipError_t e = hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, kBlock, 1, 1, 0, s, args, nullptr);
+  hipError_t e = hipModuleLaunchKernel(fn, (unsigned)grid, 1, 1, kBlock, 1, 1, jit_lds_bytes(), s, args, nullptr);
   if (e != hipSuccess) {
     set_error(std::string("hipModuleLaunchKernel (segmented walk): ") + hipGetErrorString(e));
     return SUP_EHIP;

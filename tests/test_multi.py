@@ -34,7 +34,8 @@ def _worker(rank, world, port, mat, q):
     n = mat.shape[0]
     c0, c1 = bench.shard_chunks(n, rank, world)
     info = S.plan_info(mat, "dense")  # the plan sup_perman_shard runs
-    part, _ = oracle.engine_range(mat, info["kind"], c0, c1, info["L"], info["m"], info["colmap"], 1)
+    part, _ = oracle.engine_range(mat, info["kind"], c0, c1, info["L"], info["m"], info["colmap"], 1,
+                                  info["cached"])
     t = torch.tensor([part], dtype=torch.float64)
     dist.all_reduce(t)
     el = torch.tensor([float(rank)], dtype=torch.float64)

@@ -22,8 +22,22 @@ def test_cpu_seg_vs_mirror_and_exact(sup, orc, n, d, seed):
     a = _rand(n, d, seed)
     got = sup.perman_cpu(a, "seg", threads=4)
     assert got == orc.engine_perman_as(sup, a, "seg", threads=4)
+    assert sup.plan_info(a, "seg")["cached"] in (0, 1, 2)
     exact = float(orc.exact_perman(a))
     assert abs(got - exact) <= 1e-12 * max(abs(exact), 1.0)
+
+
+@pytest.mark.parametrize("cc", [0, 1, 2])
+@pytest.mark.parametrize("n,d,seed", [(13, 0.5, 11), (16, 0.35, 12)])
+def test_cpu_seg_cached_bits(sup, orc, monkeypatch, cc, n, d, seed):
+    """Every cached-bit count (walk bits held in every state, SUP_JIT_CC forces
+    it): host twin == oracle mirror bit for bit, and == the exact permanent."""
+    monkeypatch.setenv("SUP_JIT_CC", str(cc))
+    a = _rand(n, d, seed, ints=False)
+    assert sup.plan_info(a, "seg")["cached"] == cc
+    got = sup.perman_cpu(a, "seg", threads=4)
+    assert got == orc.engine_perman_as(sup, a, "seg", threads=4)
+    assert rel(got, float(orc.exact_perman(a))) < 1e-12
 
 
 def test_cpu_seg_corpus_vs_sparse(sup, orc):
@@ -44,10 +58,12 @@ def test_planner_choice(sup):
     b = sup.skip_order(b)[0]
     assert sup.plan_info(b, "sparse", jit=0)["kind"] == "seg"  # 2^43 steps: worth compiling
     assert sup.plan_info(b, "skip", jit=1)["kind"] == "skip"   # SkipPer is never replaced
-    # all-nonzero matrix: one segment holds every row; the segmented step is the
-    # plain step without its final multiply (2n ops instead of 2n + 1)
+    # all-nonzero matrix: every step touches every row; the paired step and the
+    # cached walk bits (held in both states, their steps only accumulate) keep
+    # it below the plain walk's 2n + 1 ops
     _, st = sup.perman_cpu(np.ones((12, 12)), "seg", threads=2, return_stats=True)
-    assert 22 <= st["est_ops_per_step"] <= 24  # ~2n per step (truncated at the 2^-m walk tail)
+    assert 8 <= st["est_ops_per_step"] < 2 * 12
+    assert sup.plan_info(np.ones((12, 12)), "seg")["cached"] >= 1
 
 
 def test_seg_cost_model_reported(sup):
