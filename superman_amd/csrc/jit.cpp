@@ -11,10 +11,8 @@
 //   * adds the flipped column only to the rows it touches (values packed
 //     contiguously, one s_load_dwordx16 per 8 of them, SGPR operands of
 //     v_add_f64), and
-//   * re-multiplies only the segments that contain a touched row, then the
-//     suffix chain U_i = S_i * U_{i+1} down to U_0, the term.
-// Segments are the first-touch groups of the walk columns (rows walk bit k
-// touched first), so a step of walk bit k never goes deeper than segment k.
+//   * re-forms only the product-tree nodes above those rows (make_tree: rows
+//     that change on the same steps share a node).
 //
 // Paired form.  Gray steps 2j and 2j+1 differ in walk bit 0 only.  Segment 0
 // (the rows walk bit 0 touches) is held twice, x (bit 0 clear) and
@@ -29,13 +27,19 @@
 // column, zeros included) — a switch over per-bit steps would make LLVM
 // carry copies of x across its arms (measured: 120 -> 242 VGPRs).
 //
-// Measured on MI355X (profiles/r1): n=40 d=0.5 bench matrix 29.4 VALU
-// instructions per Gray step (cost model 32.7; the prefix-blocked AOT walk
-// executes 46.6, the plain dense walk 81), VALU 99% busy, 1.26e12 steps/s.
-// Everything else (chunk start, lane layout, wave-chunk queue, reduction
-// order) is walk_common.hpp's, shared with the ahead-of-time kernels, and
-// the arithmetic is mirrored bit for bit by engine_cpu.cpp (seg_*) and
-// oracle/oracle.c (kind 3).
+// Cached walk bits.  Walk bits 1..cc (cc <= 2, seg_best) are held in every
+// state: each value that depends on them has one copy per state of those
+// bits, so their pair steps only accumulate (the state is a compile-time
+// constant inside the unrolled block) and the other steps update every copy.
+// cc is chosen on the exact op count within a live-value budget.
+//
+// Measured on MI355X (profiles/r1): n=40 d=0.5 bench matrix 18.2 VALU
+// instructions per Gray step (cost model 18.0; the prefix-blocked AOT walk
+// executes 46.6, the plain dense walk 81), VALU 96% busy at 2 waves/SIMD,
+// 2.05e12 steps/s.  Everything else (chunk start, lane layout, wave-chunk
+// queue, reduction order) is walk_common.hpp's, shared with the ahead-of-time
+// kernels, and the arithmetic is mirrored bit for bit by engine_cpu.cpp
+// (tree_*, seg_*) and oracle/oracle.c (kind 3).
 //
 // Compiled code objects are cached in memory (per process, per device) and on
 // disk: $SUP_JIT_CACHE_DIR, else $XDG_CACHE_HOME/superman_amd, else
@@ -296,8 +300,8 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count) {
   if (m == 0) return extend({}, count);
   // descent: swap a walk position with another walk position or an unused
   // column while the cost drops (positions whose weight 2^-(k+1) is visible)
-  const int hot = std::min(m, 8);
-  for (int pass = 0; pass < 6; ++pass) {
+  const int hot = std::min(m, 12);
+  for (int pass = 0; pass < 8; ++pass) {
     bool improved = false;
     for (int a = 0; a < hot; ++a) {
       for (int c = 0; c < nb; ++c) {
