@@ -117,3 +117,30 @@ def test_seg_n40_bench_matrix(sup):
             parts = [parts[i] + parts[i + 1] for i in range(0, len(parts), 2)]
         assert parts[0] == full
     assert -2 * full == r_seg
+
+
+@pytest.mark.parametrize("cc", [0, 1, 2])
+def test_seg_cached_bits_bitexact(sup, orc, monkeypatch, cc):
+    """Each cached-walk-bit count (SUP_JIT_CC forces it) on the GPU: bit-exact
+    against the oracle's per-state mirror and the host twin."""
+    monkeypatch.setenv("SUP_JIT_CC", str(cc))
+    rng = np.random.default_rng(40 + cc)
+    for n, d in ((24, 0.5), (26, 0.3)):
+        a = np.where(rng.random((n, n)) < d, rng.random((n, n)) * 5, 0.0)
+        a[np.arange(n), rng.permutation(n)] = 1.0
+        assert sup.plan_info(a, "seg")["cached"] == cc
+        got = sup.perman(a, algo=4, kernel="seg")
+        assert got == orc.engine_perman_as(sup, a, "seg", threads=16), (n, d)
+        assert got == sup.perman_cpu(a, "seg", threads=16), (n, d)
+
+
+def test_seg_n40_d02_companion(sup):
+    """The bench's density-0.2 companion (double/40_0.20_0): segmented walk vs
+    the prefix-blocked walk, and exact under power-of-two row scaling."""
+    a, _, _ = sup.read_matrix(fixture_path("double__40_0.20_0"))
+    r_seg, st = sup.perman(a, algo=4, jit=1, return_stats=True)
+    assert st["walk_kind"] == 3
+    assert rel(r_seg, sup.perman(a, algo=4, jit=-1)) < 1e-9
+    b = a.copy()
+    b[7] *= 4.0
+    assert sup.perman(b, algo=4, jit=1) == r_seg * 4.0
