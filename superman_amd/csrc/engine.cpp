@@ -248,9 +248,10 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
 // fp64 VALU lane-ops per second of one MI355X on the walk kernels (measured:
 // 46.6 ops/step at 7.98e11 steps/s on the n=40 bench), for jit's auto mode.
 static constexpr double kLaneOpsPerSec = 3.7e13;
-// Compile + load of a specialised kernel is ~0.4 s; auto mode specialises only
-// when the predicted walk time saved is clearly larger.
-static constexpr double kJitMinSavingSec = 1.0;
+// Compile + load of a specialised kernel is 0.15-0.2 s on the MI355X box's
+// host (profiles/r1/probe_seg.log; 0 when the disk cache holds it); auto mode
+// specialises when the predicted walk time saved is clearly larger.
+static constexpr double kJitMinSavingSec = 0.3;
 
 static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit,
                              int ndev);
