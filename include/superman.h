@@ -29,6 +29,7 @@
 #ifndef SUPERMAN_H
 #define SUPERMAN_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -174,6 +175,19 @@ int sup_prepare(const void* mat, sup_dtype t, int n, sup_kernel kernel, const su
  * GPU entry points above, which fail with SUP_ENODEV without a device. */
 int sup_perman_cpu(const void* mat, sup_dtype t, int n, sup_kernel kernel, int threads,
                    double* out, sup_stats* st);
+
+/* Exact permanent of an integer matrix (int32, or float/double holding
+ * integers; |a| < 2^31, row sums of |a| < 2^31).  The reference computes int
+ * and -b (binary) inputs in fp64 (rounded beyond 2^53); here the same Ryser /
+ * Gray-code walk runs on 2A in residue arithmetic modulo primes < 2^42 and
+ * the residues are joined by CRT (walk_exact.hip, exact.cpp), with a built-in
+ * divisibility self-check.  *out receives the signed decimal integer,
+ * NUL-terminated (520 bytes always suffice).  o->gpu_num devices from
+ * o->device_id split the work statically; on_cpu = 1 runs o->threads host
+ * threads instead.  st (optional): kernel_ms (max over devices), wall_ms,
+ * devices_used, gray_steps. */
+int sup_perman_exact(const void* mat, sup_dtype t, int n, const sup_opts* o, int on_cpu, char* out,
+                     size_t out_len, sup_stats* st);
 
 /* Nijenhuis-Wilf prologue (gpu_exact_dense.cu:642-652): x0[j] = a[j][n-1] - rowsum_j/2,
  * p0 = prod x0.  Host-only helper, exported for the test harness. */

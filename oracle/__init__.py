@@ -35,6 +35,8 @@ def load() -> C.CDLL:
         lib.orc_engine_range.argtypes = [P, I, I, P, I, I, I, U, U, I, C.POINTER(U)]
         lib.orc_engine_perman.argtypes = [P, I, I, P, I, I]
         lib.orc_nw_start.argtypes = [P, I, P, P]
+        lib.orc_exact_mod.argtypes = [P, I, U, I]
+        lib.orc_exact_mod.restype = U
         lib.orc_engine_layout.argtypes = [I, C.POINTER(I), C.POINTER(I), C.POINTER(I)]
         for f in ("orc_ref_dense", "orc_ref_dense_partial", "orc_ref_sparse", "orc_ref_sparse_partial",
                   "orc_ref_skip", "orc_ref_skip_partial", "orc_engine_range", "orc_engine_perman"):
@@ -171,6 +173,55 @@ def exact_perman(a) -> Fraction:
             p *= s[r]
         total += p if (n - size) % 2 == 0 else -p
     return total
+
+
+def _is_prime(n: int) -> bool:
+    if n < 2:
+        return False
+    for q in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37):
+        if n % q == 0:
+            return n == q
+    d, s = n - 1, 0
+    while d % 2 == 0:
+        d, s = d // 2, s + 1
+    for b in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37):
+        x = pow(b, d, n)
+        if x in (1, n - 1):
+            continue
+        for _ in range(s - 1):
+            x = x * x % n
+            if x == n - 1:
+                break
+        else:
+            return False
+    return True
+
+
+def exact_perman_crt(a, threads: int = 8) -> int:
+    """Exact permanent of an integer matrix, independent of the engine's exact
+    path: plain Ryser over all 2^n column subsets modulo primes just below
+    2^55 (oracle.c orc_exact_mod), joined here by CRT with Python integers.
+    |perm| <= prod_i sum_j |a_ij| fixes how many primes are needed."""
+    a = np.ascontiguousarray(np.asarray(a), dtype=np.int64)
+    n = a.shape[0]
+    bound = 1
+    for r in np.abs(a).sum(axis=1).tolist():
+        bound *= int(r)
+    if bound == 0:
+        return 0
+    primes, M, c = [], 1, (1 << 55) - 1
+    while M <= 2 * bound:
+        if _is_prime(c):
+            primes.append(c)
+            M *= c
+        c -= 2
+    x, mod = 0, 1
+    for p in primes:
+        r = int(load().orc_exact_mod(a.ctypes.data, n, p, threads))
+        # x' = x + mod * ((r - x) / mod mod p)
+        t = (r - x) * pow(mod, -1, p) % p
+        x, mod = x + mod * t, mod * p
+    return x - M if x > M // 2 else x
 
 
 def exact_perman_brute(a) -> Fraction:

@@ -863,3 +863,50 @@ double orc_engine_perman(const double* a, int n, int kind, const int* colmap, in
   double s = orc_engine_range(a, n, kind, colmap, cc, L, m, 0, 1ULL << h, threads, 0);
   return (4 * (n & 1) - 2) * s;
 }
+
+/* ======================================================================
+ * Exact permanent, independent of the engine's exact path (test checker for
+ * sup_perman_exact): plain Ryser (not Nijenhuis-Wilf),
+ *   perm = (-1)^n sum_{S subset of columns} (-1)^|S| prod_i sum_{j in S} a_ij,
+ * over all 2^n column subsets in Gray order, integer row sums in int64 and
+ * the products modulo p with 128-bit multiplies.  The caller (oracle/
+ * __init__.py exact_perman_crt) picks its own primes and joins them by CRT.
+ * ====================================================================== */
+static uint64_t e_mulmod(uint64_t a, uint64_t b, uint64_t p) { return (uint64_t)((unsigned __int128)a * b % p); }
+
+unsigned long long orc_exact_mod(const long long* a, int n, unsigned long long p, int threads) {
+  if (n <= 0) return 1 % p;
+  int hb = n > 12 ? 8 : 0; /* 2^hb blocks of the subset space, one Gray walk each */
+  unsigned long long nblk = 1ULL << hb, per = 1ULL << (n - hb), total = 0;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1) reduction(+ : total)
+  for (long long b = 0; b < (long long)nblk; ++b) {
+    long long s[ORC_MAXN];
+    unsigned long long base = (unsigned long long)b * per, acc = 0;
+    unsigned long long g0 = base ^ (base >> 1);
+    for (int i = 0; i < n; ++i) {
+      s[i] = 0;
+      for (int j = 0; j < n; ++j)
+        if ((g0 >> j) & 1ULL) s[i] += a[i * n + j];
+    }
+    for (unsigned long long t = 0; t < per; ++t) {
+      unsigned long long idx = base + t, g = idx ^ (idx >> 1);
+      if (t > 0) {
+        unsigned long long gp = (idx - 1) ^ ((idx - 1) >> 1);
+        int k = __builtin_ctzll(g ^ gp);
+        long long sg = ((g >> k) & 1ULL) ? 1 : -1;
+        for (int i = 0; i < n; ++i) s[i] += sg * a[i * n + k];
+      }
+      unsigned long long pr = 1 % p;
+      for (int i = 0; i < n && pr; ++i) {
+        long long v = s[i] % (long long)p;
+        pr = e_mulmod(pr, (unsigned long long)(v < 0 ? v + (long long)p : v), p);
+      }
+      int odd = __builtin_popcountll(g) & 1;
+      acc = (acc + (odd ? (p - pr) % p : pr)) % p;
+    }
+    total = (total + acc) % p;
+  }
+  /* the reduction sums < nblk * p, fine below 2^63 for p < 2^55 */
+  total %= p;
+  return (n & 1) ? (p - total) % p : total;
+}

@@ -147,6 +147,22 @@ def perman_cpu(mat, kernel: str = "dense", threads: int = 16, return_stats: bool
     return (out.value, st.as_dict()) if return_stats else out.value
 
 
+def perman_exact(mat, gpu_num: int = 1, device_id: int = 0, cpu: bool = False, threads: int = 16,
+                 return_stats: bool = False):
+    """Exact permanent (Python int) of an integer matrix: the Ryser / Gray walk
+    of 2A in residue arithmetic modulo primes, joined by CRT (sup_perman_exact).
+    The reference's int / -b path is fp64; this one is exact."""
+    a, dt, n = _mat(mat)
+    lib = _lib.load()
+    o = _opts(gpu_num=gpu_num, device_id=device_id, threads=threads)
+    buf = C.create_string_buffer(1024)
+    st = SupStats()
+    _lib.check(lib.sup_perman_exact(a.ctypes.data, dt, n, C.byref(o), int(bool(cpu)), buf, len(buf), C.byref(st)),
+               "perman_exact")
+    v = int(buf.value.decode())
+    return (v, st.as_dict()) if return_stats else v
+
+
 def partial(mat, start: int, end: int, kernel: str = "dense", gpu_num: int = 1, device_id: int = 0,
             walk_log2: int = 0, return_stats: bool = False):
     """GPU partial Ryser sum over reference Gray indices [start, end) (index 0 = p0 term)."""

@@ -194,6 +194,41 @@ int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int
   return SUP_OK;
 }
 
+int sup_perman_exact(const void* mat, sup_dtype t, int n, const sup_opts* o_in, int on_cpu, char* out,
+                     size_t out_len, sup_stats* st) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!out || out_len < 2) {
+    set_error("sup_perman_exact: output buffer missing or too small");
+    return SUP_EINVAL;
+  }
+  std::vector<double> A;
+  int rc = to_double(mat, t, n, A);
+  if (rc) return rc;
+  sup_opts o;
+  if (o_in) o = *o_in;
+  else sup_opts_init(&o);
+  std::string s;
+  double kms = 0.0;
+  int used = 0;
+  if ((rc = exact_perman(A.data(), n, o, on_cpu != 0, s, &kms, &used))) return rc;
+  if (s.size() + 1 > out_len) {
+    set_error("sup_perman_exact: output buffer too small");
+    return SUP_EINVAL;
+  }
+  std::memcpy(out, s.c_str(), s.size() + 1);
+  if (st) {
+    std::memset(st, 0, sizeof(*st));
+    st->kernel_ms = kms;
+    st->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    st->gray_steps = 1ull << (n - 1);
+    st->visited_steps = st->gray_steps;
+    st->devices_used = used;
+    st->walk_kind = (int)kWalkDense;
+    st->leaves = 1;
+  }
+  return SUP_OK;
+}
+
 int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o_in, int* walk_kind,
                   int* colmap, int* L, int* m, int* cached_bits) {
   std::vector<double> A;

@@ -367,6 +367,8 @@ struct DeviceCtx {
   double* d_scratch = nullptr;
   size_t scratch_cap = 0;
   unsigned* d_visited = nullptr;
+  double* d_wave = nullptr;   // exact path: per-wave residues
+  size_t wave_cap = 0;
   size_t visited_cap = 0;
   unsigned* d_counter = nullptr;
   double* d_result = nullptr;
@@ -536,6 +538,72 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     r.visited = tot * (uint64_t)(1ull << P.lay.L);
   } else {
     r.visited = count << (P.lay.L + P.lay.m);
+  }
+  return SUP_OK;
+}
+
+// Exact residue walk (walk_exact.hip) over wave-chunks [c0, c1) of a dense
+// identity-map plan of 2A: per prime, the sum of the terms mod p (in [0, p)).
+// Residue sums are exact, so neither the wave a chunk lands on nor the order
+// of the per-wave sums changes the result.
+int run_range_exact(int dev, const Plan& P, uint64_t c0, uint64_t c1, const std::vector<double>& primes,
+                    std::vector<uint64_t>& res, double* kernel_ms) {
+  const int np = (int)primes.size();
+  res.assign(np, 0);
+  if (kernel_ms) *kernel_ms = 0.0;
+  if (c1 <= c0) return SUP_OK;
+  if (np < 1 || np > kMaxPrimes || P.kind != kWalkDense || c1 > P.lay.chunks()) {
+    set_error("run_range_exact: bad request");
+    return SUP_EINVAL;
+  }
+  DeviceCtx* c = nullptr;
+  int rc = get_ctx(dev, &c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(c->mu);
+  SUP_HIP(hipSetDevice(dev));
+  int occ = 0;
+  SUP_HIP(exact_occupancy(P.n, &occ));
+  if (occ < 1) occ = 1;
+  const uint64_t count = c1 - c0;
+  uint64_t grid = (uint64_t)c->cus * (uint64_t)occ;
+  const uint64_t need_blocks = (count + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (grid > need_blocks) grid = need_blocks;
+  if (grid < 1) grid = 1;
+  const size_t waves = (size_t)grid * kWavesPerBlock;
+  if ((rc = ensure(c->d_cols, c->cols_cap, P.cols.size()))) return rc;
+  if ((rc = ensure(c->d_wave, c->wave_cap, waves * kMaxPrimes))) return rc;
+  hipStream_t s = c->stream;
+  SUP_HIP(hipMemcpyAsync(c->d_cols, P.cols.data(), P.cols.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  SUP_HIP(hipMemcpyAsync(c->d_x0, P.x0.data(), P.x0.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
+  WalkParams p{};
+  p.cols = c->d_cols;
+  p.x0 = c->d_x0;
+  p.chunk_begin = c0;
+  p.chunk_count = count;
+  p.L = P.lay.L;
+  p.m = P.lay.m;
+  p.n = P.n;
+  p.counter = c->d_counter;
+  p.group = 1;
+  ExactParams e{};
+  for (int q = 0; q < np; ++q) e.prime[q] = primes[q], e.pinv[q] = 1.0 / primes[q];
+  e.nprimes = np;
+  e.wave_out = c->d_wave;
+  SUP_HIP(hipEventRecord(c->ev0, s));
+  SUP_HIP(launch_exact(P.n, p, e, (int)grid, s));
+  SUP_HIP(hipEventRecord(c->ev1, s));
+  std::vector<double> w(waves * kMaxPrimes);
+  SUP_HIP(hipMemcpyAsync(w.data(), c->d_wave, w.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  SUP_HIP(hipStreamSynchronize(s));
+  float ms = 0.f;
+  SUP_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  if (kernel_ms) *kernel_ms = ms;
+  for (int q = 0; q < np; ++q) {
+    const uint64_t pq = (uint64_t)primes[q];
+    uint64_t acc = 0;  // waves x p < 2^64
+    for (size_t i = 0; i < waves; ++i) acc = (acc + (uint64_t)w[i * kMaxPrimes + q]) % pq;
+    res[q] = acc;
   }
   return SUP_OK;
 }

@@ -173,4 +173,16 @@ int rccl_allreduce_partials(const std::vector<int>& devs, const std::vector<std:
 // the hybrid `-c -g` chunk queue).  Bit-identical to the dense/sparse kernels.
 double cpu_walk_range(const Plan& P, uint64_t c0, uint64_t c1, int threads);
 
+// ---- exact path (exact.cpp, walk_exact.hip) ----
+// Per prime, sum over wave-chunks [c0, c1) of the terms of the dense identity
+// plan P (of 2A) modulo that prime, in [0, p): on device `dev`, or on host
+// threads (same arithmetic).
+int run_range_exact(int dev, const Plan& P, uint64_t c0, uint64_t c1, const std::vector<double>& primes,
+                    std::vector<uint64_t>& res, double* kernel_ms);
+void cpu_exact_range(const Plan& P, uint64_t c0, uint64_t c1, const std::vector<double>& primes, int threads,
+                     std::vector<uint64_t>& res);
+// Exact permanent of integer-valued A as a decimal string (sup_perman_exact).
+int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::string& out, double* kernel_ms,
+                 int* devices_used);
+
 }  // namespace sup

@@ -357,4 +357,63 @@ double cpu_walk_range(const Plan& P, uint64_t c0, uint64_t c1, int threads) {
   return part[0];
 }
 
+// ---- exact path: walk_exact.hip's residue arithmetic on host threads ----
+namespace {
+inline double red(double t, double p, double pinv) { return std::fma(-std::rint(t * pinv), p, t); }
+inline double chain_mod(const double* x, int n, double p, double pinv) {
+  double r = x[0];
+  for (int j = 1; j < n; ++j) r = red(r * x[j], p, pinv);
+  return r;
+}
+inline uint64_t to_res(double v, uint64_t p) {  // |v| < 2^53, integer-valued
+  const int64_t i = (int64_t)v % (int64_t)p;
+  return (uint64_t)(i < 0 ? i + (int64_t)p : i);
+}
+}  // namespace
+
+void cpu_exact_range(const Plan& P, uint64_t c0, uint64_t c1, const std::vector<double>& primes, int threads,
+                     std::vector<uint64_t>& res) {
+  const int np = (int)primes.size(), n = P.n, L = P.lay.L, m = P.lay.m;
+  res.assign(np, 0);
+  if (c1 <= c0) return;
+  const uint64_t count = c1 - c0;
+  const int TH = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)std::max(threads, 1), count));
+  std::vector<std::vector<uint64_t>> part(TH, std::vector<uint64_t>(np, 0));
+  std::vector<std::thread> th;
+  for (int w = 0; w < TH; ++w)
+    th.emplace_back([&, w]() {
+      std::vector<double> pinv(np), acc(np);
+      for (int q = 0; q < np; ++q) pinv[q] = 1.0 / primes[q];
+      for (uint64_t a = w; a < count; a += (uint64_t)TH) {
+        const uint64_t ga = c0 + a;
+        for (unsigned l = 0; l < (1u << L); ++l) {
+          Lane s;
+          chunk_start(P, ga, l, s);
+          for (int q = 0; q < np; ++q) acc[q] = chain_mod(s.x, n, primes[q], pinv[q]);
+          for (uint32_t t = 1; t < (1u << m); ++t) {
+            const uint32_t k = __builtin_ctz(t);
+            const double* c = col_of(P, L + (int)k, (t >> (k + 1)) & 1u);
+            for (int j = 0; j < n; ++j) s.x[j] += c[j];
+            for (int q = 0; q < np; ++q) {
+              const double r = chain_mod(s.x, n, primes[q], pinv[q]);
+              acc[q] = (t & 1u) ? acc[q] - r : acc[q] + r;
+              if ((t & 255u) == 0u) acc[q] = red(acc[q], primes[q], pinv[q]);
+            }
+          }
+          const bool flip = (((unsigned)ga ^ (unsigned)__builtin_popcount(l)) & 1u) != 0;
+          for (int q = 0; q < np; ++q) {
+            const uint64_t pq = (uint64_t)primes[q];
+            const uint64_t v = to_res(red(acc[q], primes[q], pinv[q]), pq);
+            part[w][q] = (part[w][q] + (flip ? (pq - v) % pq : v)) % pq;
+          }
+        }
+      }
+    });
+  for (auto& t : th) t.join();
+  for (int q = 0; q < np; ++q) {
+    const uint64_t pq = (uint64_t)primes[q];
+    for (int w = 0; w < TH; ++w) res[q] = (res[q] + part[w][q]) % pq;
+  }
+}
+
 }  // namespace sup

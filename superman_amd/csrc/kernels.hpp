@@ -23,6 +23,14 @@ SUP_DECL_RANGE(skip, 17)
 SUP_DECL_RANGE(skip, 33)
 SUP_DECL_RANGE(skip, 49)
 #undef SUP_DECL_RANGE
+#define SUP_DECL_EXACT(LO)                                                                                  \
+  hipError_t launch_exact_##LO(int n, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s); \
+  hipError_t occupancy_exact_##LO(int n, int* blocks_per_cu);
+SUP_DECL_EXACT(1)
+SUP_DECL_EXACT(17)
+SUP_DECL_EXACT(33)
+SUP_DECL_EXACT(49)
+#undef SUP_DECL_EXACT
 
 // kWalkSeg: the pattern-specialised segmented walk (jit.cpp), compiled at run
 // time with hiprtc for one matrix pattern; launched through hipModule APIs.
@@ -32,6 +40,10 @@ enum WalkKind { kWalkDense = 0, kWalkSparse = 1, kWalkSkip = 2, kWalkSeg = 3 };
 hipError_t launch_walk(WalkKind kind, int n, const WalkParams& p, int grid, hipStream_t s);
 // Resident 256-thread blocks per CU for that kernel (occupancy API).
 hipError_t walk_occupancy(WalkKind kind, int n, int* blocks_per_cu);
+
+// Exact residue walk (walk_exact.hip) for matrix order n (1..64).
+hipError_t launch_exact(int n, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s);
+hipError_t exact_occupancy(int n, int* blocks_per_cu);
 
 // Fixed-order pairwise reduction of `count` doubles into *out (64-way passes,
 // zero padded; mirrored by oracle/oracle.c orc_pairwise_reduce).  `scratch`

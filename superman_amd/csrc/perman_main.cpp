@@ -11,7 +11,10 @@
 // --seed (-S) the estimators' Philox seed (-a / -i; the reference seeds with
 // time(0), so its estimates are not reproducible); --jit (-J) <-1|0|1> the
 // pattern-specialised segmented walk (sup_opts.jit: never / auto / whenever
-// its cost model wins).
+// its cost model wins); --exact (-E) the exact integer permanent of an int /
+// -b (binary) matrix (sup_perman_exact: residue walk + CRT; the reference's
+// int path is fp64): on -g with -p5/-p6 it uses -d devices, with -c alone
+// the -t host threads.
 #include <getopt.h>
 
 #include <chrono>
@@ -28,7 +31,7 @@ namespace {
 
 struct Cli {
   bool generic = true, dense = true, approximation = false, gpu = false, cpu = false, grid_graph = false;
-  bool rccl = false, verbose = false, compression = false;
+  bool rccl = false, verbose = false, compression = false, exact = false;
   int gpu_num = 2, threads = 16, perman_algo = 1, preprocessing = 0, device = 0, reps = 1;
   double scaling = -1.0;
   long number_of_times = 100000;  // main.cu:338-344 defaults
@@ -119,7 +122,7 @@ int run_approx(const Cli& c) {
 
 int main(int argc, char** argv) {
   Cli c;
-  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rvou:S:J:";
+  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rvou:S:J:E";
   const struct option long_options[] = {{"binary", 0, NULL, 'b'},       {"sparse", 0, NULL, 's'},
                                         {"preprocessing", 1, NULL, 'r'}, {"threads", 1, NULL, 't'},
                                         {"file", 1, NULL, 'f'},          {"gpu", 0, NULL, 'g'},
@@ -132,7 +135,7 @@ int main(int argc, char** argv) {
                                         {"rccl", 0, NULL, 'R'},          {"verbose", 0, NULL, 'v'},
                                         {"compression", 0, NULL, 'o'},   {"scaling", 1, NULL, 'u'},
                                         {"seed", 1, NULL, 'S'},          {"jit", 1, NULL, 'J'},
-                                        {NULL, 0, NULL, 0}};
+                                        {"exact", 0, NULL, 'E'},         {NULL, 0, NULL, 0}};
   int opt;
   auto need_arg = [&](char o) -> bool {
     if (optarg[0] == '-') {
@@ -164,6 +167,7 @@ int main(int argc, char** argv) {
       case 'l': if (!need_arg('l')) return 1; c.device = std::atoi(optarg); break;
       case 'k': if (!need_arg('k')) return 1; c.reps = std::max(1, std::atoi(optarg)); break;
       case 'R': c.rccl = true; break;
+      case 'E': c.exact = true; break;
       case 'v': c.verbose = true; break;
       case 'o': c.compression = true; break;  // revised_perman/main.cpp:1462
       case 'u':                                // main.cpp:1465 (atoi)
@@ -211,6 +215,31 @@ int main(int argc, char** argv) {
   o.use_rccl = c.rccl ? 1 : 0;
   o.verbose = c.verbose ? 1 : 0;
   o.jit = c.jit;
+
+  if (c.exact) {  // exact integer permanent (any -p: the sum does not depend on the kernel)
+    if (reduce) {
+      std::fprintf(stderr, "perman: --exact does not combine with -o / -u\n");
+      sup_free(mat);
+      return 1;
+    }
+    if (c.gpu && c.perman_algo != 5 && c.perman_algo != 6 && c.perman_algo != 8) o.gpu_num = 1;
+    char buf[1024];
+    sup_stats st;
+    int rc = SUP_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int rep = 0; rep < c.reps && rc == SUP_OK; ++rep)
+      rc = sup_perman_exact(mat, t, n, &o, c.gpu ? 0 : 1, buf, sizeof buf, &st);
+    const double sec =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / (double)c.reps;
+    sup_free(mat);
+    if (rc != SUP_OK) return fail("exact permanent");
+    std::cout << "Result: " << (c.gpu ? "gpu_perman64_exact_residue" : "cpu_perman64_exact_residue") << " " << buf
+              << " in " << sec << std::endl;
+    std::printf("Permanent: %s\n", buf);
+    if (c.verbose)
+      std::printf("Stats: devices %d kernel_ms %.3f wall_ms %.3f\n", st.devices_used, st.kernel_ms, st.wall_ms);
+    return 0;
+  }
 
   std::string name;
   sup_kernel kern = SUP_KERNEL_DENSE;

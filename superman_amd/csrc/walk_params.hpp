@@ -45,4 +45,15 @@ struct WalkParams {
   const double* jtab;
 };
 
+// Exact path (walk_exact.hip): residues of the walk's terms modulo up to
+// kMaxPrimes primes (p < 2^42, held in fp64; pinv = 1 / p rounded).
+constexpr int kMaxPrimes = 8;
+struct ExactParams {
+  double prime[kMaxPrimes];
+  double pinv[kMaxPrimes];
+  int nprimes;
+  int pad_;
+  double* wave_out;  // [grid waves][kMaxPrimes]: each wave's residue sum, in [0, p)
+};
+
 }  // namespace sup

@@ -1,0 +1,105 @@
+"""Exact integer permanent (sup_perman_exact; superman_amd/csrc/exact.cpp,
+walk_exact.hip) on host threads — no GPU needed.
+
+The reference computes int and -b (binary) inputs in fp64 (rounded beyond
+2^53); the exact path evaluates the same Ryser / Gray walk of 2A in residue
+arithmetic and joins the residues by CRT.  Checked against:
+* known answers (J_n = n!, permutation matrices, a zero row);
+* exact rational Ryser (oracle.exact_perman, independent Python) for n <= 10;
+* an independent plain-Ryser CRT oracle (oracle.c orc_exact_mod + Python
+  CRT, other primes) for n up to 20, negative entries included;
+* the reference's own __float128 results (goldens from the compiled
+  reference): the exact integer rounded to fp64 equals the reference's quad
+  result rounded to fp64, bit for bit, on every synthetic int matrix (n <= 22;
+  the reference's own fp64 results already differ from n = 16 on).
+"""
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, fixture_path
+
+
+def _rand(n, d, seed, lo=1, hi=6):
+    rng = np.random.default_rng(seed)
+    mask = rng.random((n, n)) < d
+    mask[np.arange(n), rng.permutation(n)] = True
+    return np.where(mask, rng.integers(lo, hi, (n, n)), 0).astype(np.int32)
+
+
+def test_known_answers(sup):
+    for n in range(1, 13):
+        assert sup.perman_exact(np.ones((n, n), np.int32), cpu=True, threads=4) == math.factorial(n)
+    p = np.eye(15, dtype=np.int32)[np.random.default_rng(0).permutation(15)]
+    assert sup.perman_exact(p, cpu=True, threads=4) == 1
+    z = _rand(12, 0.5, 1)
+    z[4, :] = 0
+    assert sup.perman_exact(z, cpu=True, threads=4) == 0
+    # J_20: 20! > 2^53, exact
+    assert sup.perman_exact(np.ones((20, 20), np.int32), cpu=True, threads=8) == math.factorial(20)
+
+
+@pytest.mark.parametrize("n,seed", [(5, 1), (8, 2), (10, 3)])
+def test_vs_rational_ryser(sup, orc, n, seed):
+    a = _rand(n, 0.6, seed, -4, 5)  # negative entries too
+    assert sup.perman_exact(a, cpu=True, threads=4) == orc.exact_perman(a)
+
+
+@pytest.mark.parametrize("n,d,lo,hi,seed", [(14, 0.5, 1, 6, 4), (16, 0.3, -5, 6, 5), (18, 0.5, 0, 2, 6),
+                                            (20, 0.5, 1, 6, 7)])
+def test_vs_crt_oracle(sup, orc, n, d, lo, hi, seed):
+    a = _rand(n, d, seed, lo, hi)
+    got = sup.perman_exact(a, cpu=True, threads=8)
+    assert got == orc.exact_perman_crt(a, 8)
+    # same value whatever the storage type
+    assert sup.perman_exact(a.astype(np.float64), cpu=True, threads=8) == got
+    # and within fp64 rounding of the fp64 walk
+    f = sup.perman_cpu(a.astype(np.float64), "dense", threads=8)
+    assert abs(f - got) <= 1e-10 * max(abs(got), 1)
+
+
+def test_vs_reference_quad_goldens(sup, golden):
+    names = sorted({k.split("|")[0] for k in golden if k.startswith("synth/") and "_int" in k})
+    checked = 0
+    for nm in names:
+        q = golden.get(f"{nm}|dense_q|r0|b0|t4")
+        if q is None:
+            continue
+        a = sup.read_matrix(fixture_path(nm))[0]
+        e = sup.perman_exact(a, cpu=True, threads=8)
+        assert float(e) == q, (nm, e, q)  # the reference's quad result, rounded to fp64, bit for bit
+        checked += 1
+    assert checked >= 20  # n = 1 .. 22; the reference's fp64 results are inexact from n = 16
+
+
+def test_rejects_non_integers(sup):
+    a = np.ones((6, 6))
+    a[2, 3] = 0.5
+    with pytest.raises(sup.SupError):
+        sup.perman_exact(a, cpu=True)
+    b = np.ones((6, 6))
+    b[0, 0] = 2.0 ** 40
+    with pytest.raises(sup.SupError):
+        sup.perman_exact(b, cpu=True)
+
+
+def test_cli_exact(sup, tmp_path):
+    a = _rand(14, 0.5, 9)
+    path = tmp_path / "m14"
+    nz = np.argwhere(a != 0)
+    with open(path, "w") as f:
+        f.write(f"14 {len(nz)} int\n")
+        for i, j in nz:
+            f.write(f"{i} {j} {a[i, j]}\n")
+    exe = os.path.join(ROOT, "superman_amd", "bin", "perman")
+    out = subprocess.run([exe, "-f", str(path), "-c", "-E", "-t", "4"], capture_output=True, text=True, check=True)
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("Permanent:")][0]
+    assert int(line.split()[1]) == sup.perman_exact(a, cpu=True, threads=4)
+    # -b: every listed entry is 1 (util.h:343-358)
+    out = subprocess.run([exe, "-f", str(path), "-c", "-E", "-b", "-t", "4"], capture_output=True, text=True,
+                         check=True)
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("Permanent:")][0]
+    assert int(line.split()[1]) == sup.perman_exact((a != 0).astype(np.int32), cpu=True, threads=4)

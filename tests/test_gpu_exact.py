@@ -1,0 +1,75 @@
+"""GPU exact integer permanent (walk_exact.hip through sup_perman_exact): the
+residues and hence the exact integer equal the host threads' and the
+independent plain-Ryser CRT oracle's; at the corpus sizes (n = 30, 36) the
+exact value sits within fp64 rounding of the reference's goldens and of the
+fp64 walks, and rounds to the reference's __float128 result."""
+import numpy as np
+import pytest
+
+from conftest import fixture_path, rel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu(sup):
+    if sup.device_count() < 1:
+        pytest.fail("no HIP device visible: -m gpu tests must run on the MI355X box")
+
+
+def _rand(n, d, seed, lo=1, hi=6):
+    rng = np.random.default_rng(seed)
+    mask = rng.random((n, n)) < d
+    mask[np.arange(n), rng.permutation(n)] = True
+    return np.where(mask, rng.integers(lo, hi, (n, n)), 0).astype(np.int32)
+
+
+@pytest.mark.parametrize("n,d,lo,hi,seed", [(7, 1.0, 1, 2, 1), (12, 0.5, -3, 4, 2), (20, 0.5, 1, 6, 3),
+                                            (22, 0.4, 0, 2, 4), (24, 0.5, -5, 6, 5)])
+def test_gpu_exact_vs_cpu_and_oracle(sup, orc, n, d, lo, hi, seed):
+    a = _rand(n, d, seed, lo, hi)
+    got, st = sup.perman_exact(a, return_stats=True)
+    assert st["devices_used"] == 1 and st["kernel_ms"] > 0
+    assert got == sup.perman_exact(a, cpu=True, threads=16)
+    assert got == orc.exact_perman_crt(a, 16)
+
+
+def test_gpu_exact_known(sup):
+    import math
+    for n in (10, 21, 26):
+        assert sup.perman_exact(np.ones((n, n), np.int32)) == math.factorial(n)
+
+
+def test_gpu_exact_synth_goldens(sup, golden):
+    names = sorted({k.split("|")[0] for k in golden if k.startswith("synth/") and "_int" in k})
+    for nm in names:
+        q = golden.get(f"{nm}|dense_q|r0|b0|t4")
+        if q is None:
+            continue
+        a = sup.read_matrix(fixture_path(nm))[0]
+        assert float(sup.perman_exact(a)) == q, nm
+
+
+@pytest.mark.parametrize("name", ["int__30_0.20_0", "int__30_0.50_0"])
+def test_gpu_exact_corpus_n30(sup, golden, name):
+    a, _, _ = sup.read_matrix(fixture_path(name))
+    e = sup.perman_exact(a)
+    q = golden.get(f"{name}|dense_q|r0|b0|t8")
+    f = golden[f"{name}|dense|r0|b0|t8"]
+    assert rel(float(e), q) < 1e-15  # the reference's __float128 result
+    assert rel(float(e), f) < 1e-9   # the reference's fp64 result
+    assert rel(float(e), sup.perman(a, algo=4, jit=1)) < 1e-9
+    # -b (binary): every listed entry is 1 (util.h:343-358); reference fp64 golden
+    b, _, _ = sup.read_matrix(fixture_path(name), binary=True)
+    eb = sup.perman_exact(b)
+    fb = golden.get(f"{name}|dense|r0|b1|t8")
+    if fb is not None:
+        assert rel(float(eb), fb) < 1e-9
+    assert rel(float(eb), sup.perman(b, algo=4)) < 1e-9
+
+
+def test_gpu_exact_n36(sup):
+    a, _, _ = sup.read_matrix(fixture_path("int__36_0.20_0"))
+    e, st = sup.perman_exact(a, return_stats=True)
+    assert rel(float(e), sup.perman(a, algo=4, jit=1)) < 1e-9
+    assert st["kernel_ms"] > 0
