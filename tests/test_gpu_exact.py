@@ -73,3 +73,22 @@ def test_gpu_exact_n36(sup):
     e, st = sup.perman_exact(a, return_stats=True)
     assert rel(float(e), sup.perman(a, algo=4, jit=1)) < 1e-9
     assert st["kernel_ms"] > 0
+
+
+def test_gpu_exact_decimal_ground_truth_n30(sup, golden):
+    """double/30_0.50_0 holds 6-digit decimals, so perm(A) = perm(round(1e6 A)) / 1e6^n
+    exactly: the true permanent.  The reference's __float128 result agrees to the
+    binary64 rounding of the entries; our fp64 walk is within 1e-11 and never
+    further from the truth than the reference's own fp64 result."""
+    from fractions import Fraction
+    a, _, _ = sup.read_matrix(fixture_path("double__30_0.50_0"))
+    ai = np.rint(a * 1e6)
+    e = sup.perman_exact(ai)
+    exact = Fraction(e, 10 ** (6 * a.shape[0]))
+    q = golden["double__30_0.50_0|dense_q|r0|b0|t8"]
+    f = golden["double__30_0.50_0|dense|r0|b0|t8"]
+    assert rel(float(exact), q) < 1e-14
+    ours = sup.perman(a, algo=4, jit=1)
+    err = lambda v: float(abs(Fraction(v) - exact) / exact)  # noqa: E731
+    assert err(ours) < 1e-11
+    assert err(ours) <= err(f)
