@@ -546,7 +546,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
 // identity-map plan of 2A: per prime, the sum of the terms mod p (in [0, p)).
 // Residue sums are exact, so neither the wave a chunk lands on nor the order
 // of the per-wave sums changes the result.
-int run_range_exact(int dev, const Plan& P, uint64_t c0, uint64_t c1, const std::vector<double>& primes,
+int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1, const std::vector<double>& primes,
                     std::vector<uint64_t>& res, double* kernel_ms) {
   const int np = (int)primes.size();
   res.assign(np, 0);
@@ -562,7 +562,7 @@ int run_range_exact(int dev, const Plan& P, uint64_t c0, uint64_t c1, const std:
   std::lock_guard<std::mutex> g(c->mu);
   SUP_HIP(hipSetDevice(dev));
   int occ = 0;
-  SUP_HIP(exact_occupancy(P.n, &occ));
+  SUP_HIP(exact_occupancy(P.n, group, &occ));
   if (occ < 1) occ = 1;
   const uint64_t count = c1 - c0;
   uint64_t grid = (uint64_t)c->cus * (uint64_t)occ;
@@ -591,7 +591,7 @@ int run_range_exact(int dev, const Plan& P, uint64_t c0, uint64_t c1, const std:
   e.nprimes = np;
   e.wave_out = c->d_wave;
   SUP_HIP(hipEventRecord(c->ev0, s));
-  SUP_HIP(launch_exact(P.n, p, e, (int)grid, s));
+  SUP_HIP(launch_exact(P.n, group, p, e, (int)grid, s));
   SUP_HIP(hipEventRecord(c->ev1, s));
   std::vector<double> w(waves * kMaxPrimes);
   SUP_HIP(hipMemcpyAsync(w.data(), c->d_wave, w.size() * sizeof(double), hipMemcpyDeviceToHost, s));

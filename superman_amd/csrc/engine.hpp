@@ -175,9 +175,10 @@ double cpu_walk_range(const Plan& P, uint64_t c0, uint64_t c1, int threads);
 
 // ---- exact path (exact.cpp, walk_exact.hip) ----
 // Per prime, sum over wave-chunks [c0, c1) of the terms of the dense identity
-// plan P (of 2A) modulo that prime, in [0, p): on device `dev`, or on host
-// threads (same arithmetic).
-int run_range_exact(int dev, const Plan& P, uint64_t c0, uint64_t c1, const std::vector<double>& primes,
+// plan P (of 2A) modulo that prime, in [0, p): on device `dev` (rows
+// multiplied in exact groups of `group` = 1, 2 or 4 first), or on host
+// threads (same residues: every operation is exact).
+int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1, const std::vector<double>& primes,
                     std::vector<uint64_t>& res, double* kernel_ms);
 void cpu_exact_range(const Plan& P, uint64_t c0, uint64_t c1, const std::vector<double>& primes, int threads,
                      std::vector<uint64_t>& res);

@@ -361,7 +361,7 @@ double cpu_walk_range(const Plan& P, uint64_t c0, uint64_t c1, int threads) {
 namespace {
 inline double red(double t, double p, double pinv) { return std::fma(-std::rint(t * pinv), p, t); }
 inline double chain_mod(const double* x, int n, double p, double pinv) {
-  double r = x[0];
+  double r = red(x[0], p, pinv);  // |r| < 1.5 p before the first product
   for (int j = 1; j < n; ++j) r = red(r * x[j], p, pinv);
   return r;
 }

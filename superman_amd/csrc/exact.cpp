@@ -153,11 +153,23 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
     maxrow = std::max(maxrow, ra);
     logT += std::log2(ra);
   }
-  // |X_j| <= maxrow; red() keeps |r| < 1.5 p, so 1.5 p maxrow < 2^53 keeps every
-  // product exact; p < 2^42 also bounds the 256-step accumulation (< 2^51)
+  // |X_j| <= maxrow.  The GPU multiplies rows in exact groups of G (|y| <=
+  // maxrow^G < 2^(G xbits)) before the residue chain, whose |r| < 1.5 p, so
+  // 1.5 p 2^(G xbits) < 2^53 keeps every product exact; p < 2^42 also bounds
+  // the 256-step accumulation (< 2^51).  G trades shared group products
+  // (n (1 - 1/G) per step) against chain length (4 n / G per prime) and
+  // smaller primes (more of them).
   const int xbits = (int)std::ceil(std::log2(maxrow + 1.0));
-  const int pbits = std::min(42, 51 - xbits);
-  if (pbits < 20) {
+  int group = 0, pbits = 0;
+  double best = 1e300;
+  for (int G : {1, 2, 4}) {
+    const int pb = std::min(42, 52 - G * xbits - 1);
+    if (pb < 20) continue;
+    const double primes_needed = std::ceil((logT + 3.0) / (pb - 0.5));
+    const double ops = n * (1.0 - 1.0 / G) + primes_needed * (4.0 * std::ceil((double)n / G) + 3.0);
+    if (ops < best) best = ops, group = G, pbits = pb;
+  }
+  if (group == 0) {
     set_error("sup_perman_exact: row sums of |a| must stay below 2^31 for the residue walk");
     return SUP_EUNSUPPORTED;
   }
@@ -201,7 +213,7 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
           const std::vector<double> pr(primes.begin() + q0, primes.begin() + std::min(np, q0 + kMaxPrimes));
           std::vector<uint64_t> r;
           double ms = 0.0;
-          drc[g] = run_range_exact(o.device_id + g, P, c0, c1, pr, r, &ms);
+          drc[g] = run_range_exact(o.device_id + g, P, group, c0, c1, pr, r, &ms);
           if (drc[g]) derr[g] = last_error();
           for (size_t i = 0; i < r.size(); ++i) dres[g][q0 + i] = r[i];
           dms[g] += ms;

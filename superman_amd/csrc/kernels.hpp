@@ -24,8 +24,9 @@ SUP_DECL_RANGE(skip, 33)
 SUP_DECL_RANGE(skip, 49)
 #undef SUP_DECL_RANGE
 #define SUP_DECL_EXACT(LO)                                                                                  \
-  hipError_t launch_exact_##LO(int n, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s); \
-  hipError_t occupancy_exact_##LO(int n, int* blocks_per_cu);
+  hipError_t launch_exact_##LO(int n, int g, const WalkParams& p, const ExactParams& e, int grid,        \
+                               hipStream_t s);                                                        \
+  hipError_t occupancy_exact_##LO(int n, int g, int* blocks_per_cu);
 SUP_DECL_EXACT(1)
 SUP_DECL_EXACT(17)
 SUP_DECL_EXACT(33)
@@ -41,9 +42,10 @@ hipError_t launch_walk(WalkKind kind, int n, const WalkParams& p, int grid, hipS
 // Resident 256-thread blocks per CU for that kernel (occupancy API).
 hipError_t walk_occupancy(WalkKind kind, int n, int* blocks_per_cu);
 
-// Exact residue walk (walk_exact.hip) for matrix order n (1..64).
-hipError_t launch_exact(int n, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s);
-hipError_t exact_occupancy(int n, int* blocks_per_cu);
+// Exact residue walk (walk_exact.hip) for matrix order n (1..64), rows
+// multiplied in exact groups of g (1, 2 or 4) before the residue chain.
+hipError_t launch_exact(int n, int g, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s);
+hipError_t exact_occupancy(int n, int g, int* blocks_per_cu);
 
 // Fixed-order pairwise reduction of `count` doubles into *out (64-way passes,
 // zero padded; mirrored by oracle/oracle.c orc_pairwise_reduce).  `scratch`

@@ -79,14 +79,14 @@ hipError_t walk_occupancy(WalkKind kind, int n, int* blocks_per_cu) {
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_exact(int n, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s) {
+hipError_t launch_exact(int n, int g, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s) {
   if (n < 1 || n > 64) return hipErrorInvalidValue;
-  SUP_DISPATCH(exact, launch, n, p, e, grid, s)
+  SUP_DISPATCH(exact, launch, n, g, p, e, grid, s)
 }
 
-hipError_t exact_occupancy(int n, int* blocks_per_cu) {
+hipError_t exact_occupancy(int n, int g, int* blocks_per_cu) {
   if (n < 1 || n > 64) return hipErrorInvalidValue;
-  SUP_DISPATCH(exact, occupancy, n, blocks_per_cu)
+  SUP_DISPATCH(exact, occupancy, n, g, blocks_per_cu)
 }
 
 }  // namespace sup

@@ -7,7 +7,8 @@
 //   X_j(S) = 2 x_j(S) = sum_c (+-) a_jc,   |X_j| <= rowabs_j = sum_c |a_jc|,
 // held exactly in fp64.  Only the products leave the integers' range; each
 // term prod_j X_j is formed modulo up to kMaxPrimes primes p < 2^42 (exact
-// fp64 residue arithmetic, red() below), summed with its Gray sign, and the
+// fp64 residue arithmetic, red() below; rows multiplied in exact groups of
+// G = 1, 2 or 4 first), summed with its Gray sign, and the
 // host joins the residues by CRT into the exact integer
 //   T = sum_i (-1)^i prod_j X_j(gray(i)) = 2^(n-1) perm / (2 - 4(n&1)).
 // The reference computes the same sum in fp64 (its -b / int path); this path
@@ -24,18 +25,38 @@ __device__ __forceinline__ double red(double t, double p, double pinv) {
   return __builtin_fma(-__builtin_rint(t * pinv), p, t);
 }
 
-// prod_j X_j mod p as a chain r <- red(r * X_j): |r| < 1.5 p and |X_j| <=
-// maxX with 1.5 p maxX < 2^53 (host picks p), so every product is exact.
-template <int N>
-__device__ __forceinline__ double chain_mod(const double (&x)[N], double p, double pinv) {
-  double r = x[0];
+// Rows in groups of G: y_k = prod of X over group k, exact (|y_k| <= maxX^G,
+// the host keeps G log2(maxX) + log2(1.5 p) < 53), formed once per step and
+// shared by every prime.
+template <int N, int G>
+struct Groups {
+  static constexpr int K = (N + G - 1) / G;
+};
+template <int N, int G>
+__device__ __forceinline__ void group_products(const double (&x)[N], double (&y)[Groups<N, G>::K]) {
 #pragma unroll
-  for (int j = 1; j < N; ++j) r = red(r * x[j], p, pinv);
+  for (int k = 0; k < Groups<N, G>::K; ++k) {
+    double v = x[k * G];
+#pragma unroll
+    for (int i = 1; i < G; ++i)
+      if (k * G + i < N) v *= x[(k * G + i < N) ? k * G + i : 0];
+    y[k] = v;
+  }
+}
+
+// prod_k y_k mod p as a chain r <- red(r * y_k), starting from red(y_0):
+// |r| < 1.5 p, so every product is exact.
+template <int K>
+__device__ __forceinline__ double chain_mod(const double (&y)[K], double p, double pinv) {
+  double r = red(y[0], p, pinv);
+#pragma unroll
+  for (int k = 1; k < K; ++k) r = red(r * y[k], p, pinv);
   return r;
 }
 
-template <int N>
+template <int N, int G>
 __global__ __launch_bounds__(kBlock) void walk_exact(WalkParams p, ExactParams e) {
+  constexpr int K = Groups<N, G>::K;
   constexpr int NP = pad8(N);
   const uint32_t lane = threadIdx.x & 63u;
   const bool lane_valid = lane < (1u << p.L);
@@ -51,19 +72,21 @@ __global__ __launch_bounds__(kBlock) void walk_exact(WalkParams p, ExactParams e
     const uint64_t ga = p.chunk_begin + g;
     double x[N];
     chunk_start<N>(x, p, ga, lane);
-    double acc[kMaxPrimes];
+    double acc[kMaxPrimes], y[K];
+    group_products<N, G>(x, y);
 #pragma unroll
     for (int q = 0; q < kMaxPrimes; ++q)
-      if (q < e.nprimes) acc[q] = chain_mod<N>(x, e.prime[q], e.pinv[q]);
+      if (q < e.nprimes) acc[q] = chain_mod<K>(y, e.prime[q], e.pinv[q]);
     for (uint32_t t = 1; t < T; ++t) {
       const uint32_t k = (uint32_t)__builtin_ctz(t);
       const uint32_t neg = (t >> (k + 1)) & 1u;
       add_col<N>(x, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u));
       const bool odd = t & 1u;
+      group_products<N, G>(x, y);
 #pragma unroll
       for (int q = 0; q < kMaxPrimes; ++q)
         if (q < e.nprimes) {
-          const double r = chain_mod<N>(x, e.prime[q], e.pinv[q]);
+          const double r = chain_mod<K>(y, e.prime[q], e.pinv[q]);
           acc[q] = odd ? acc[q] - r : acc[q] + r;
           // |acc| grows by < 1.5 p per step: fold it every 256 steps
           if ((t & 255u) == 0u) acc[q] = red(acc[q], e.prime[q], e.pinv[q]);
@@ -96,31 +119,37 @@ __global__ __launch_bounds__(kBlock) void walk_exact(WalkParams p, ExactParams e
 }
 
 template <int N, int HI>
-static hipError_t launch_rec(int n, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s) {
+static hipError_t launch_rec(int n, int g, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s) {
   if (n == N) {
-    hipLaunchKernelGGL(walk_exact<N>, dim3(grid), dim3(kBlock), 0, s, p, e);
+    if (g == 4) hipLaunchKernelGGL((walk_exact<N, 4>), dim3(grid), dim3(kBlock), 0, s, p, e);
+    else if (g == 2) hipLaunchKernelGGL((walk_exact<N, 2>), dim3(grid), dim3(kBlock), 0, s, p, e);
+    else hipLaunchKernelGGL((walk_exact<N, 1>), dim3(grid), dim3(kBlock), 0, s, p, e);
     return hipGetLastError();
   }
-  if constexpr (N < HI) return launch_rec<N + 1, HI>(n, p, e, grid, s);
+  if constexpr (N < HI) return launch_rec<N + 1, HI>(n, g, p, e, grid, s);
   return hipErrorInvalidValue;
 }
 
 template <int N, int HI>
-static hipError_t occ_rec(int n, int* blocks_per_cu) {
-  if (n == N) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact<N>, kBlock, 0);
-  if constexpr (N < HI) return occ_rec<N + 1, HI>(n, blocks_per_cu);
+static hipError_t occ_rec(int n, int g, int* blocks_per_cu) {
+  if (n == N) {
+    if (g == 4) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact<N, 4>, kBlock, 0);
+    if (g == 2) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact<N, 2>, kBlock, 0);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact<N, 1>, kBlock, 0);
+  }
+  if constexpr (N < HI) return occ_rec<N + 1, HI>(n, g, blocks_per_cu);
   return hipErrorInvalidValue;
 }
 
 #define SUP_CAT2(a, b) a##b
 #define SUP_CAT(a, b) SUP_CAT2(a, b)
 
-hipError_t SUP_CAT(launch_exact_, SUP_N_LO)(int n, const WalkParams& p, const ExactParams& e, int grid,
+hipError_t SUP_CAT(launch_exact_, SUP_N_LO)(int n, int g, const WalkParams& p, const ExactParams& e, int grid,
                                             hipStream_t s) {
-  return launch_rec<SUP_N_LO, SUP_N_HI>(n, p, e, grid, s);
+  return launch_rec<SUP_N_LO, SUP_N_HI>(n, g, p, e, grid, s);
 }
-hipError_t SUP_CAT(occupancy_exact_, SUP_N_LO)(int n, int* blocks_per_cu) {
-  return occ_rec<SUP_N_LO, SUP_N_HI>(n, blocks_per_cu);
+hipError_t SUP_CAT(occupancy_exact_, SUP_N_LO)(int n, int g, int* blocks_per_cu) {
+  return occ_rec<SUP_N_LO, SUP_N_HI>(n, g, blocks_per_cu);
 }
 
 }  // namespace sup

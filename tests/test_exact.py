@@ -103,3 +103,15 @@ def test_cli_exact(sup, tmp_path):
                          check=True)
     line = [ln for ln in out.stdout.splitlines() if ln.startswith("Permanent:")][0]
     assert int(line.split()[1]) == sup.perman_exact((a != 0).astype(np.int32), cpu=True, threads=4)
+
+
+def test_large_entries_vs_crt_oracle(sup, orc):
+    """6-digit decimals scaled to integers (the corpus ground-truth use): row
+    sums near 2^28, so the residue chain runs with small primes and must reduce
+    before its first product."""
+    rng = np.random.default_rng(11)
+    for n in (9, 13):
+        a = np.where(rng.random((n, n)) < 0.6, rng.integers(1, 5_000_000, (n, n)), 0).astype(np.int64)
+        a[np.arange(n), rng.permutation(n)] = 4_999_999
+        got = sup.perman_exact(a.astype(np.float64), cpu=True, threads=8)
+        assert got == orc.exact_perman_crt(a, 8)
