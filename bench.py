@@ -114,6 +114,37 @@ def cpu_baseline(a, n: int, budget_s: float, gpu_sup, kernel: str):
                       f"({dt:.1f} s, oracle/oracle.c orc_ref_dense_partial = cpu_perman64 restated)"}, err
 
 
+def cpu_reference_config1(S, threads: int):
+    """The reference's own CPU code (parallel_perman64, rev/cpu_algos.hpp:761,
+    compiled unmodified from the reference sources into oracle/_ref/ref_v2 by
+    oracle/Makefile) on BASELINE config 1 (double/30_0.50_0, all 2^29 Gray
+    steps), next to the oracle port on the same input: shows the port that
+    `cpu_baseline` times at n = 40 runs at the reference's speed."""
+    import subprocess
+    import oracle
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_v2")
+    mat = os.path.join(ROOT, "tests", "fixtures", "double__30_0.50_0")
+    if not os.path.exists(exe):
+        return None
+    try:
+        out = subprocess.run([exe, mat, "dense", str(threads)], capture_output=True, text=True, timeout=120,
+                             check=True).stdout.split()
+        ref_perm, ref_s = float(out[0]), float(out[1])
+    except (subprocess.SubprocessError, OSError, ValueError, IndexError):
+        return None
+    a = S.read_matrix(mat)[0]
+    t = time.perf_counter()
+    port_perm = oracle.ref_dense(a, threads)
+    port_s = time.perf_counter() - t
+    steps = 1 << 29
+    return {"value": steps / ref_s, "unit": "gray-steps/s", "cores": threads, "kind": "reference",
+            "sample": "oracle/_ref/ref_v2 (reference parallel_perman64<double,double>, compiled from the reference "
+                      f"sources) on double/30_0.50_0, all 2^29 steps, {ref_s:.2f} s (its own timer)",
+            "port_value": steps / port_s,
+            # the reference adds its thread partials in omp-critical completion order
+            "port_rel_diff": abs(port_perm - ref_perm) / abs(ref_perm)}
+
+
 def main():
     global args
     args = parse()
@@ -274,6 +305,7 @@ def main():
                                    "seg" if st["walk_kind"] == 3 else args.kernel)
         rec["cpu_baseline"] = cb_rec
         rec["rel_err_vs_cpu"] = err
+        rec["cpu_baseline_reference_config1"] = cpu_reference_config1(S, cb_rec["cores"])
     else:
         rec["cpu_baseline"] = None
     if rank == 0:
