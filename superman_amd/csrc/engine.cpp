@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -305,7 +306,25 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
   // candidates in preference order; the cheapest by walk_cost wins
   std::vector<WalkKind> kinds;
   switch (kernel) {
-    case SUP_KERNEL_SKIPPER: return make_plan(A, n, kWalkSkip, false, lay, P);
+    case SUP_KERNEL_SKIPPER: {
+      // SkipPer only gains where some x_j(S) is exactly zero.  With a
+      // non-integer entry that is a measure-zero coincidence, so SkipPer
+      // would evaluate every state: the segmented walk (same sum) runs
+      // instead when cheaper.  Integer matrices keep SkipPer (their exact
+      // zeros are common: config 5 int visits 22 % of the states).
+      int rc = make_plan(A, n, kWalkSkip, false, lay, P);
+      if (rc || jit < 0 || n < 10 || lay.m < 3) return rc;
+      bool integral = true;
+      for (size_t i = 0; i < (size_t)n * n && integral; ++i) integral = A[i] == std::floor(A[i]);
+      if (integral) return SUP_OK;
+      Plan s;
+      if (make_plan(A, n, kWalkSeg, false, lay, s) == SUP_OK && walk_cost(s) < walk_cost(P)) {
+        const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
+        const double saved = steps * (walk_cost(P) - walk_cost(s)) / kLaneOpsPerSec;
+        if (jit >= 1 || saved >= kJitMinSavingSec) P = std::move(s);
+      }
+      return SUP_OK;
+    }
     case SUP_KERNEL_DENSE_PLAIN: return make_plan(A, n, kWalkDense, false, lay, P);
     case SUP_KERNEL_SEGMENTED:
       if (n < 10 || lay.m < 3) {

@@ -238,10 +238,16 @@ def test_config5_n44(sup, orc, typ):
             mir, _ = orc.engine_range(b, kind, s >> (L + ml), e >> (L + ml), L, ml, None, 8)
             assert got == mir, (kind, k)
     r_sp = sup.perman(b, algo=4, sparse=True)
-    r_sk, st = sup.perman(b, algo=8, sparse=True, return_stats=True)
+    r_sk, st = sup.perman(b, algo=8, sparse=True, return_stats=True, jit=-1)  # the SkipPer kernel itself
+    assert st["walk_kind"] == 2
     assert np.isfinite(r_sp) and r_sp > 0 and rel(r_sk, r_sp) < 1e-9
     if typ == "int":
         assert st["visited_steps"] < 0.5 * 2.0 ** 43  # SkipPer jumps over exact-zero rows
+    # default SkipPer request: integer input keeps SkipPer; non-integer input
+    # (no exact zeros to skip) runs the cheaper segmented walk, same sum
+    r_def, st_def = sup.perman(b, algo=8, sparse=True, return_stats=True)
+    assert st_def["walk_kind"] == (2 if typ == "int" else 3)
+    assert rel(r_def, r_sp) < 1e-9
     c = b.astype(np.float64)
     c[5] *= 2.0
     assert sup.perman(c, algo=4, sparse=True) == 2.0 * r_sp  # power-of-two row scaling is exact
