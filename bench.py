@@ -19,6 +19,8 @@ outside the timed region, like the plan), then every timed step walks all
 The north star also asks for density 0.2: the reference corpus matrix
 double/40_0.20_0 (--also) is timed the same way (same shards, all-reduce and
 clock) and reported under "densities"; `value` stays the d = 0.5 metric.
+BASELINE configs 2, 3 and 5 are timed the same way under "configs"
+(--configs 0 skips them).
 
 Prints ONE JSON line on rank 0 (driver contract), including the roofline of
 the walk kernel (hipEvents on its own stream, measured inside the library)
@@ -58,6 +60,7 @@ def parse():
     ap.add_argument("--rehearse", action="store_true",
                     help="all ranks on device 0 over gloo: rehearse the N-rank path on a one-GPU box")
     ap.add_argument("--prep", type=int, default=0, choices=[0, 1, 2], help="-r: 1 SortOrder, 2 SkipOrder")
+    ap.add_argument("--configs", type=int, default=1, help="also time BASELINE configs 2, 3 and 5 (0 = skip)")
     ap.add_argument("--also", default=os.path.join(ROOT, "tests", "fixtures", "double__40_0.20_0"),
                     help="comma-separated companion matrices timed the same way (north star: densities "
                          "0.2 and 0.5 at every N); '' = none")
@@ -165,11 +168,12 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     import superman_amd as S
 
-    def load(path):
+    def load(path, prep=None):
         a = S.read_matrix(path)[0]
-        if args.prep == 1:
+        prep = args.prep if prep is None else prep
+        if prep == 1:
             a = S.sort_order(a)[0]
-        elif args.prep == 2:
+        elif prep == 2:
             a = S.skip_order(a)[0]
         return a
 
@@ -178,17 +182,19 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    def timed(a):
+    def timed(a, kernel=None, jit=None):
         """W untimed + K timed steps of one whole permanent of `a`; returns
         (elapsed max over ranks, permanent, mean walk-kernel ms, stats, compile ms)."""
         n = a.shape[0]
+        kernel = args.kernel if kernel is None else kernel
+        jit = args.jit if jit is None else jit
         # plan + (segmented walk) hiprtc compile, once, before the timed region;
         # gpu_num = world so that --jit 0 decides as the N-rank plan would
-        prep = S.prepare(a, args.kernel, jit=args.jit, gpu_num=world)
+        prep = S.prepare(a, kernel, jit=jit, gpu_num=world)
 
         def step():
-            part, st = S.perman_shard(a, rank, world, kernel=args.kernel, device_id=dev, return_stats=True,
-                                      jit=args.jit)
+            part, st = S.perman_shard(a, rank, world, kernel=kernel, device_id=dev, return_stats=True,
+                                      jit=jit)
             if world > 1:
                 t = torch.tensor([part], dtype=torch.float64, device=tdev)
                 dist.all_reduce(t)  # RCCL over xGMI: the single data-path collective
@@ -231,6 +237,31 @@ def main():
                      "ms_per_step": e2 / args.steps * 1e3, "kernel_ms_avg": kms2,
                      "walk": walk_names[st2["walk_kind"]],
                      "est_fp64_ops_per_step": st2["est_ops_per_step"], "permanent": perm2})
+
+    # the other BASELINE configs (2, 3, 5), same shards / all-reduce / clock.
+    # Configs 2 and 3 with --jit 1 (the compile is outside the timed steps, as
+    # for the headline; the CLI's auto mode keeps the AOT walk there because a
+    # single run would not repay the 0.2 s compile); SkipPer (-p8) keeps its
+    # kernel on integer input
+    configs = []
+    if args.configs:
+        fx = os.path.join(ROOT, "tests", "fixtures")
+        for label, fname, prep, kernel, jit in (
+                ("config 2: -p4 --jit 1 (dense n=32 d=0.5)", "double__32_0.50_0", 0, "dense", 1),
+                ("config 3: -p4 -s -r1 --jit 1 (SpaRyser + SortOrder, n=36 d=0.2)", "double__36_0.20_0", 1,
+                 "sparse", 1),
+                ("config 5: -p8 -s -r2 (SkipPer + SkipOrder, n=44 d=0.15 int)", "synth44_0.15_int", 2, "skip", 0),
+                ("config 5 via -p4 -s -r2 (SpaRyser walk, same input)", "synth44_0.15_int", 2, "sparse", 0)):
+            b = load(os.path.join(fx, fname), prep)
+            nb = b.shape[0]
+            e2, perm2, kms2, st2, _ = timed(b, kernel, jit)
+            configs.append({"config": label, "matrix": fname.replace("__", "/"), "n": nb,
+                            "value": args.steps * (1 << (nb - 1)) / e2, "unit": "gray-steps/s (nominal)",
+                            "ms_per_step": e2 / args.steps * 1e3, "kernel_ms_avg": kms2,
+                            "walk": walk_names[st2["walk_kind"]],
+                            # products evaluated / Gray steps of this rank's shard (SkipPer skips < 1)
+                            "visited_frac": st2["visited_steps"] * world / float(1 << (nb - 1)),
+                            "permanent": perm2})
 
     total_steps = args.steps * (1 << (n - 1))
     value = total_steps / elapsed
@@ -277,6 +308,7 @@ def main():
                      "issue_frac": st["est_ops_per_step"] * my_steps / (k_ms * 1e-3) / (FP64_PEAK_TFLOPS * 1e12 / 2)},
         "permanent": perm,
         "densities": also,
+        "configs": configs,
     }
     if pmc:  # rocprofv3 evidence for the dominant kernel (committed profile of this kernel at this n)
         sq = pmc.get("sq", {})
