@@ -92,3 +92,15 @@ def test_gpu_exact_decimal_ground_truth_n30(sup, golden):
     err = lambda v: float(abs(Fraction(v) - exact) / exact)  # noqa: E731
     assert err(ours) < 1e-11
     assert err(ours) <= err(f)
+
+
+def test_cli_exact_gpu(sup):
+    import subprocess
+    exe = sup._lib.PERMAN_BIN
+    f = fixture_path("int__30_0.20_0")
+    r = subprocess.run([exe, "-f", f, "-g", "-p4", "-E"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("Result: gpu_perman64_exact_residue ")
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("Permanent:")][0]
+    a, _, _ = sup.read_matrix(f)
+    assert int(line.split()[1]) == sup.perman_exact(a) == 4472440649521736776293900
