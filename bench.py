@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--matrix", default=os.path.join(ROOT, "tests", "fixtures", "double__40_0.50_0"))
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
-    ap.add_argument("--kernel", default="dense", choices=["dense", "dense_plain", "sparse", "skip", "seg"],
+    ap.add_argument("--kernel", default="dense", choices=["dense", "dense_plain", "dense_lds", "sparse", "skip", "seg"],
                     help="dense = -p4/-p6 (engine picks the cheapest walk); sparse/skip = -s paths")
     ap.add_argument("--jit", type=int, default=1, choices=[-1, 0, 1],
                     help="segmented walk specialised for the pattern: 1 when cheaper, 0 auto, -1 never")
@@ -223,7 +223,8 @@ def main():
     c0, c1 = shard_chunks(n, rank, world)
     my_steps = (c1 - c0) << (L + m)
     elapsed, perm, k_ms, st, compile_ms = timed(a)
-    walk_names = {0: "dense", 1: "prefix-blocked", 2: "skipper", 3: "segmented (pattern-specialised)"}
+    walk_names = {0: "dense", 1: "prefix-blocked", 2: "skipper", 3: "segmented (pattern-specialised)",
+                  4: "dense, X in LDS"}
 
     # companion densities (north star: 0.2 and 0.5), same shards / all-reduce / clock
     also = []
@@ -268,7 +269,7 @@ def main():
     flops = 2.0 * n * my_steps  # n fp64 adds + n fp64 muls per Gray step
     achieved = flops / (k_ms * 1e-3) / 1e12
     walk = {0: f"sup::walk_dense<{n}>", 1: f"sup::walk_sparse<{n}>", 2: f"sup::walk_skip<{n}>",
-            3: "sup_walk_seg"}[st["walk_kind"]]
+            3: "sup_walk_seg", 4: f"sup::walk_lds<{n}>"}[st["walk_kind"]]
     pmc = pmc_record(n, walk)
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     fname = os.path.basename(args.matrix).replace("__", "/")

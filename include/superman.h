@@ -68,9 +68,12 @@ typedef enum {
   SUP_KERNEL_SPARYSER = 1,    /* kernel_xshared_coalescing_mshared_sparse   gpu_exact_sparse.cu:455-552 */
   SUP_KERNEL_SKIPPER = 2,     /* kernel_xshared_coalescing_mshared_skipper  gpu_exact_sparse.cu:555-670 */
   SUP_KERNEL_DENSE_PLAIN = 3, /* always the plain dense walk (2n fp64 ops per Gray step)                */
-  SUP_KERNEL_SEGMENTED = 4    /* always the segmented walk specialised for the matrix pattern (n >= 10;
+  SUP_KERNEL_SEGMENTED = 4,   /* always the segmented walk specialised for the matrix pattern (n >= 10;
                                  the GPU entry points compile it with hiprtc, sup_perman_cpu runs the
                                  same operations on host threads)                                       */
+  SUP_KERNEL_DENSE_LDS = 5    /* the plain dense walk with X and the walk columns staged in LDS, as the
+                                 reference kernel (gpu_exact_dense.cu:329-399); bit-identical to
+                                 SUP_KERNEL_DENSE_PLAIN, kept to measure the layout    */
 } sup_kernel;
 
 /* ---- multi-device scheduling policy -------------------------------------- */
@@ -111,7 +114,8 @@ typedef struct {
   int      chunks_done_cpu; /* queue items taken by the CPU worker                              */
   double   partials[16];    /* per-device partial sums (before the final combine)              */
   int      walk_kind;       /* walk actually run: 0 dense, 1 prefix-blocked (SpaRyser), 2 SkipPer,
-                               3 segmented (pattern-specialised, sup_opts.jit)                   */
+                               3 segmented (pattern-specialised, sup_opts.jit), 4 dense with X
+                               in LDS (SUP_KERNEL_DENSE_LDS)                                     */
   int      leaves;          /* permanents computed: 1, or the leaf count of sup_perman_reduced   */
   double   est_ops_per_step;/* cost model: fp64 VALU ops per Gray step and lane                 */
   double   jit_ms;          /* hiprtc compile time spent by this call (0 when cached / unused)   */

@@ -102,7 +102,7 @@ def engine_layout(n: int) -> tuple[int, int, int]:
     return L.value, m.value, h.value
 
 
-KINDS = {"dense": 0, "sparse": 1, "skip": 2, "seg": 3, 0: 0, 1: 1, 2: 2, 3: 3}
+KINDS = {"dense": 0, "sparse": 1, "skip": 2, "seg": 3, "lds": 0, 0: 0, 1: 1, 2: 2, 3: 3}  # lds: dense, X in LDS
 
 
 def _colmap(colmap):

@@ -62,8 +62,9 @@ ALGOS_SPARSE = {
 }
 _KERNELS = {"dense": KERNEL_DENSE, "sparse": KERNEL_SPARYSER, "spa": KERNEL_SPARYSER,
             "skipper": KERNEL_SKIPPER, "skip": KERNEL_SKIPPER, "dense_plain": _lib.KERNEL_DENSE_PLAIN,
-            "seg": _lib.KERNEL_SEGMENTED, "segmented": _lib.KERNEL_SEGMENTED}
-WALK_NAMES = {0: "dense", 1: "sparse", 2: "skip", 3: "seg"}
+            "seg": _lib.KERNEL_SEGMENTED, "segmented": _lib.KERNEL_SEGMENTED,
+            "dense_lds": _lib.KERNEL_DENSE_LDS}
+WALK_NAMES = {0: "dense", 1: "sparse", 2: "skip", 3: "seg", 4: "lds"}
 
 
 def _mat(a, max_n: int = 64) -> tuple[np.ndarray, int, int]:

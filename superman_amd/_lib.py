@@ -27,7 +27,7 @@ ERRORS = {
     -7: "SUP_EUNSUPPORTED",
 }
 SUP_INT32, SUP_FLOAT32, SUP_FLOAT64 = 0, 1, 2
-KERNEL_DENSE, KERNEL_SPARYSER, KERNEL_SKIPPER, KERNEL_DENSE_PLAIN, KERNEL_SEGMENTED = 0, 1, 2, 3, 4
+KERNEL_DENSE, KERNEL_SPARYSER, KERNEL_SKIPPER, KERNEL_DENSE_PLAIN, KERNEL_SEGMENTED, KERNEL_DENSE_LDS = 0, 1, 2, 3, 4, 5
 SCHED_SINGLE, SCHED_STATIC, SCHED_CHUNKS = 0, 1, 2
 
 # Every symbol include/superman.h declares (checked by tests/test_capi.py).

@@ -42,7 +42,7 @@ void fill_stats(sup_stats* st, const Plan& P, const SchedResult& r, double wall_
   st->grid = r.grid;
   st->chunks_done_cpu = r.cpu_items;
   for (size_t i = 0; i < r.dev_partials.size() && i < 16; ++i) st->partials[i] = r.dev_partials[i];
-  st->walk_kind = (int)P.kind;
+  st->walk_kind = P.lds ? 4 : (int)P.kind;
   st->leaves = 1;
   st->est_ops_per_step = walk_cost(P);
   st->jit_ms = r.compile_ms;
@@ -140,6 +140,7 @@ int sup_partial(const void* mat, sup_dtype t, int n, sup_kernel kernel, uint64_t
   if ((rc = to_double(mat, t, n, A))) return rc;
   Plan P;
   if ((rc = make_plan(A.data(), n, kind_of(kernel), true, lay, P))) return rc;
+  P.lds = kernel == SUP_KERNEL_DENSE_LDS;
   const int cb = lay.L + lay.m;
   SchedResult r;
   if ((rc = schedule(P, o.gpu_num > 1 ? SUP_SCHED_STATIC : SUP_SCHED_SINGLE, o, start >> cb, end >> cb, r)))
@@ -239,7 +240,7 @@ int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const 
   else sup_opts_init(&o);
   Plan P;
   if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num))) return rc;
-  if (walk_kind) *walk_kind = (int)P.kind;
+  if (walk_kind) *walk_kind = P.lds ? 4 : (int)P.kind;
   if (cached_bits) *cached_bits = P.kind == kWalkSeg ? P.seg_cc : 0;
   if (colmap)
     for (int e = 0; e < n - 1; ++e) colmap[e] = P.colmap[e];
@@ -258,7 +259,7 @@ int sup_prepare(const void* mat, sup_dtype t, int n, sup_kernel kernel, const su
   else sup_opts_init(&o);
   Plan P;
   if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num))) return rc;
-  if (walk_kind) *walk_kind = (int)P.kind;
+  if (walk_kind) *walk_kind = P.lds ? 4 : (int)P.kind;
   if (compile_ms) *compile_ms = 0.0;
   if (P.kind == kWalkSeg) return jit_compile_only(P, compile_ms);
   return SUP_OK;

@@ -326,6 +326,11 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
       return SUP_OK;
     }
     case SUP_KERNEL_DENSE_PLAIN: return make_plan(A, n, kWalkDense, false, lay, P);
+    case SUP_KERNEL_DENSE_LDS: {
+      int rc = make_plan(A, n, kWalkDense, false, lay, P);
+      P.lds = true;
+      return rc;
+    }
     case SUP_KERNEL_SEGMENTED:
       if (n < 10 || lay.m < 3) {
         set_error("the segmented walk needs n >= 10 (>= 3 walk bits)");
@@ -490,20 +495,25 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
                          hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
 
-  int occ_seg = 0;
+  int occ_seg = 0, occ_lds = 0;
   if (seg && (rc = jit_occupancy(dev, P, &occ_seg, &r.compile_ms))) return rc;
-  int& occ = seg ? occ_seg : c->occ[P.kind][P.n];
+  if (P.lds) {  // LDS-staged dense walk: one wave per block, LDS-limited residency
+    SUP_HIP(lds_occupancy(P.n, P.lay.m, &occ_lds));
+    if (occ_lds < 1) occ_lds = 1;
+  }
+  int& occ = seg ? occ_seg : (P.lds ? occ_lds : c->occ[P.kind][P.n]);
   if (occ == 0) {
     int b = 0;
     SUP_HIP(walk_occupancy(P.kind, P.n, &b));
     occ = b > 0 ? b : 1;
   }
+  const uint64_t wpb = P.lds ? 1 : kWavesPerBlock;  // waves per block
   const uint64_t resident = (uint64_t)c->cus * (uint64_t)occ;  // resident blocks
-  const uint64_t res_waves = resident * kWavesPerBlock;
+  const uint64_t res_waves = resident * wpb;
   unsigned group = 8;
   while (group > 1 && count / ((uint64_t)group * res_waves) < 32) group >>= 1;
   const uint64_t waves_needed = (count + group - 1) / group;  // one chunk group per wave at a time
-  uint64_t grid = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
+  uint64_t grid = (waves_needed + wpb - 1) / wpb;
   if (grid > resident) grid = resident;
   if (grid < 1) grid = 1;
 
@@ -533,6 +543,8 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   SUP_HIP(hipEventRecord(c->ev0, s));
   if (seg) {
     if ((rc = jit_launch(dev, P, p, (int)grid, s))) return rc;
+  } else if (P.lds) {
+    SUP_HIP(launch_lds(P.n, p, (int)grid, s));
   } else {
     SUP_HIP(launch_walk(P.kind, P.n, p, (int)grid, s));
   }

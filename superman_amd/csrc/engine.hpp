@@ -80,6 +80,7 @@ struct Plan {
   std::vector<int> dyn_rows;       // rows touched by walk bits > seg_b (their shared step)
   ProdTree outer_tree;             // rows outside segment 0 (over x)
   ProdTree inner_tree;             // segment 0's rows (once over x, once over y)
+  bool lds = false;                // kWalkDense run by the LDS-staged kernel (walk_lds.hip; same bits)
   int seg_cc = 0;                  // cached step classes: walk bits 1..seg_cc held in every state
   double seg_ops = 0.0;            // fp64 VALU ops per Gray step of the generated kernel
   int seg_regs = 0;                // values live across steps (doubles), estimate

@@ -32,6 +32,14 @@ SUP_DECL_EXACT(17)
 SUP_DECL_EXACT(33)
 SUP_DECL_EXACT(49)
 #undef SUP_DECL_EXACT
+#define SUP_DECL_LDS(LO)                                                                   \
+  hipError_t launch_lds_##LO(int n, const WalkParams& p, int grid, hipStream_t s);        \
+  hipError_t occupancy_lds_##LO(int n, int m, int* blocks_per_cu);
+SUP_DECL_LDS(1)
+SUP_DECL_LDS(17)
+SUP_DECL_LDS(33)
+SUP_DECL_LDS(49)
+#undef SUP_DECL_LDS
 
 // kWalkSeg: the pattern-specialised segmented walk (jit.cpp), compiled at run
 // time with hiprtc for one matrix pattern; launched through hipModule APIs.
@@ -41,6 +49,10 @@ enum WalkKind { kWalkDense = 0, kWalkSparse = 1, kWalkSkip = 2, kWalkSeg = 3 };
 hipError_t launch_walk(WalkKind kind, int n, const WalkParams& p, int grid, hipStream_t s);
 // Resident 256-thread blocks per CU for that kernel (occupancy API).
 hipError_t walk_occupancy(WalkKind kind, int n, int* blocks_per_cu);
+
+// LDS-staged dense walk (walk_lds.hip; 64-thread blocks, X in LDS).
+hipError_t launch_lds(int n, const WalkParams& p, int grid, hipStream_t s);
+hipError_t lds_occupancy(int n, int m, int* blocks_per_cu);
 
 // Exact residue walk (walk_exact.hip) for matrix order n (1..64), rows
 // multiplied in exact groups of g (1, 2 or 4) before the residue chain.

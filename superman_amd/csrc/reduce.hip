@@ -79,6 +79,16 @@ hipError_t walk_occupancy(WalkKind kind, int n, int* blocks_per_cu) {
   return hipErrorInvalidValue;
 }
 
+hipError_t launch_lds(int n, const WalkParams& p, int grid, hipStream_t s) {
+  if (n < 1 || n > 64) return hipErrorInvalidValue;
+  SUP_DISPATCH(lds, launch, n, p, grid, s)
+}
+
+hipError_t lds_occupancy(int n, int m, int* blocks_per_cu) {
+  if (n < 1 || n > 64) return hipErrorInvalidValue;
+  SUP_DISPATCH(lds, occupancy, n, m, blocks_per_cu)
+}
+
 hipError_t launch_exact(int n, int g, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s) {
   if (n < 1 || n > 64) return hipErrorInvalidValue;
   SUP_DISPATCH(exact, launch, n, g, p, e, grid, s)

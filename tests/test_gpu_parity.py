@@ -310,3 +310,19 @@ def test_chesapeake(sup):
     assert r == pytest.approx(13173497329080.0, rel=2e-5)
     assert abs(r - round(r)) < 1e-3 * abs(r) ** 0.5  # an integer, up to fp64 rounding of the sum
     assert rel(sup.perman(a, algo=4, sparse=True), r) < 1e-12
+
+
+def test_dense_lds_bitexact(sup, orc):
+    """The north star's LDS-staged dense kernel (walk_lds.hip) does walk_dense's
+    arithmetic with X in LDS: bit-identical results, full and partial."""
+    rng = np.random.default_rng(17)
+    for n in (3, 9, 16, 23, 30):
+        a = rng.random((n, n)) * 5
+        got, st = sup.perman(a, algo=4, kernel="dense_lds", return_stats=True)
+        assert st["walk_kind"] == 4
+        assert got == sup.perman(a, algo=4, kernel="dense_plain"), n
+        assert got == orc.engine_perman_as(sup, a, "dense_lds", threads=16), n
+    a, _, _ = sup.read_matrix(fixture_path("double__32_0.50_0"))
+    assert sup.perman(a, algo=4, kernel="dense_lds") == sup.perman(a, algo=4, kernel="dense_plain")
+    s, e = 1 << 24, 1 << 25
+    assert sup.partial(a, s, e, kernel="dense_lds") == sup.partial(a, s, e, kernel="dense_plain")

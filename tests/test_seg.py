@@ -96,3 +96,13 @@ def test_generated_kernel_compiles(sup, case, tmp_path, monkeypatch):
     assert len(list(tmp_path.glob("seg_*.co"))) == 1  # disk cache written
     again = sup.prepare(a, "seg")
     assert again["compile_ms"] == 0.0  # in-memory cache
+
+
+def test_dense_lds_plan_and_cpu(sup, orc):
+    """SUP_KERNEL_DENSE_LDS: the plain dense walk with X staged in LDS on the
+    GPU; the plan (and so the host twin and the oracle mirror) is the dense one."""
+    a = _rand(14, 0.5, 21, ints=False)
+    assert sup.plan_info(a, "dense_lds")["kind"] == "lds"
+    got = sup.perman_cpu(a, "dense_lds", threads=4)
+    assert got == sup.perman_cpu(a, "dense_plain", threads=4)
+    assert got == orc.engine_perman_as(sup, a, "dense_lds", threads=4)

@@ -18,7 +18,7 @@ run() {  # name seconds cmd...
   if [ $rc -eq 124 ] || [ $rc -ge 128 ]; then echo "STOP: $name exit $rc"; exit $rc; fi
   return 0
 }
-BENCH1="python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 --also="
+BENCH1="python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 --also= --configs 0 ${BENCH_EXTRA:-}"
 prof_pmc() {  # name counters...
   local name=$1; shift
   run "$name" 600 rocprofv3 --pmc "$@" --kernel-trace -d "$OUT/$name" -o run --output-format csv -- $BENCH1
@@ -30,7 +30,7 @@ for step in "$@"; do
     test)  run pytest_gpu 1200 python3 -m pytest tests -m gpu -q -x -p no:cacheprovider;;
     testall) run pytest_gpu 1200 python3 -m pytest tests -m gpu -q -p no:cacheprovider;;
     bench) run bench 600 python3 bench.py --steps 3 --warmup 1;;
-    prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --also=;;
+    prof)  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --also= --configs 0 ${BENCH_EXTRA:-};;
     list)  run counters 120 rocprofv3 -L;;
     pmc)   prof_pmc pmc_fetch FETCH_SIZE
            prof_pmc pmc_write WRITE_SIZE
