@@ -232,11 +232,18 @@ def main():
         b = load(path)
         nb = b.shape[0]
         e2, perm2, kms2, st2, _ = timed(b)
+        Lb, mb, _ = S.layout(nb)
+        b0, b1 = shard_chunks(nb, rank, world)
+        ach = 2.0 * nb * ((b1 - b0) << (Lb + mb)) / (kms2 * 1e-3) / 1e12  # same definition as the headline
         also.append({"matrix": os.path.basename(path).replace("__", "/"), "n": nb,
                      "density": round(float((b != 0).sum()) / (nb * nb), 4),
                      "value": args.steps * (1 << (nb - 1)) / e2, "unit": "gray-steps/s",
                      "ms_per_step": e2 / args.steps * 1e3, "kernel_ms_avg": kms2,
                      "walk": walk_names[st2["walk_kind"]],
+                     "roofline": {"achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": ach / FP64_PEAK_TFLOPS,
+                                  "issue_frac": st2["est_ops_per_step"] * ((b1 - b0) << (Lb + mb)) /
+                                  (kms2 * 1e-3) / (FP64_PEAK_TFLOPS * 1e12 / 2)},
                      "est_fp64_ops_per_step": st2["est_ops_per_step"], "permanent": perm2})
 
     # the other BASELINE configs (2, 3, 5), same shards / all-reduce / clock.
