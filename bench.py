@@ -271,6 +271,14 @@ def main():
                             "visited_frac": st2["visited_steps"] * world / float(1 << (nb - 1)),
                             "permanent": perm2})
 
+    # every rank's walk-kernel time (strong-scaling diagnosis: the slowest rank sets the step)
+    rank_kms = [k_ms]
+    if world > 1:
+        t = torch.tensor([k_ms], dtype=torch.float64, device=tdev)
+        lst = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(lst, t)
+        rank_kms = [float(x.item()) for x in lst]
+
     total_steps = args.steps * (1 << (n - 1))
     value = total_steps / elapsed
     flops = 2.0 * n * my_steps  # n fp64 adds + n fp64 muls per Gray step
@@ -315,6 +323,7 @@ def main():
                      "executed_fp64_ops_per_s": st["est_ops_per_step"] * my_steps / (k_ms * 1e-3),
                      "issue_frac": st["est_ops_per_step"] * my_steps / (k_ms * 1e-3) / (FP64_PEAK_TFLOPS * 1e12 / 2)},
         "permanent": perm,
+        "kernel_ms_per_rank": rank_kms,
         "densities": also,
         "configs": configs,
     }
