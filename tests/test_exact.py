@@ -115,3 +115,9 @@ def test_large_entries_vs_crt_oracle(sup, orc):
         a[np.arange(n), rng.permutation(n)] = 4_999_999
         got = sup.perman_exact(a.astype(np.float64), cpu=True, threads=8)
         assert got == orc.exact_perman_crt(a, 8)
+
+
+def test_tiny_and_degenerate(sup, orc):
+    for a in (np.array([[5]]), np.array([[-7]]), np.array([[1, 2], [3, 4]]), np.zeros((2, 2)),
+              np.array([[1, -1, 2], [0, 3, -4], [5, 6, -7]]), np.zeros((5, 5))):
+        assert sup.perman_exact(a.astype(np.int32), cpu=True, threads=2) == orc.exact_perman(a)

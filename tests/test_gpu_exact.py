@@ -104,3 +104,10 @@ def test_cli_exact_gpu(sup):
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("Permanent:")][0]
     a, _, _ = sup.read_matrix(f)
     assert int(line.split()[1]) == sup.perman_exact(a) == 4472440649521736776293900
+
+
+def test_gpu_exact_tiny(sup, orc):
+    rng = np.random.default_rng(8)
+    for n in range(1, 9):
+        a = rng.integers(-3, 4, (n, n)).astype(np.int32)
+        assert sup.perman_exact(a) == orc.exact_perman(a), n
