@@ -249,8 +249,8 @@ def main():
     # the other BASELINE configs (2, 3, 5), same shards / all-reduce / clock.
     # Configs 2 and 3 with --jit 1 (the compile is outside the timed steps, as
     # for the headline; the CLI's auto mode keeps the AOT walk there because a
-    # single run would not repay the 0.2 s compile); SkipPer (-p8) keeps its
-    # kernel on integer input
+    # single run would not repay the 0.2 s compile); config 5 both as the
+    # SkipPer kernel itself and as the engine's choice for the -p8 request
     configs = []
     if args.configs:
         fx = os.path.join(ROOT, "tests", "fixtures")
@@ -258,8 +258,10 @@ def main():
                 ("config 2: -p4 --jit 1 (dense n=32 d=0.5)", "double__32_0.50_0", 0, "dense", 1),
                 ("config 3: -p4 -s -r1 --jit 1 (SpaRyser + SortOrder, n=36 d=0.2)", "double__36_0.20_0", 1,
                  "sparse", 1),
-                ("config 5: -p8 -s -r2 (SkipPer + SkipOrder, n=44 d=0.15 int)", "synth44_0.15_int", 2, "skip", 0),
-                ("config 5 via -p4 -s -r2 (SpaRyser walk, same input)", "synth44_0.15_int", 2, "sparse", 0)):
+                ("config 5: -p8 -s -r2 --jit -1 (the SkipPer kernel + SkipOrder, n=44 d=0.15 int)",
+                 "synth44_0.15_int", 2, "skip", -1),
+                ("config 5: -p8 -s -r2 (engine's choice after sampling SkipPer's visited fraction)",
+                 "synth44_0.15_int", 2, "skip", 0)):
             b = load(os.path.join(fx, fname), prep)
             nb = b.shape[0]
             e2, perm2, kms2, st2, _ = timed(b, kernel, jit)

@@ -169,7 +169,9 @@ int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const 
 
 /* Build the plan sup_perman would run and, if it is the segmented walk,
  * compile its kernel now (hiprtc; no device needed) into the in-memory and
- * disk caches, so a later sup_perman does not pay the compile.  *walk_kind =
+ * disk caches, so a later sup_perman does not pay the compile.  (A SkipPer
+ * request on an integer matrix measures SkipPer's visited fraction on a
+ * sample of its chunks when a device is visible, here and in sup_plan_info.)  *walk_kind =
  * the plan's walk kind; *compile_ms = hiprtc time spent (0 when cached). */
 int sup_prepare(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o, int* walk_kind,
                 double* compile_ms);

@@ -97,7 +97,9 @@ int sup_perman(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched
     lay.m = std::min(o.walk_log2, rest);
     lay.h = rest - lay.m;
   }
-  if ((rc = plan_for(A.data(), n, kernel, lay, P, o.jit, sched == SUP_SCHED_SINGLE ? 1 : o.gpu_num))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, lay, P, o.jit, sched == SUP_SCHED_SINGLE ? 1 : o.gpu_num,
+                     o.device_id)))
+    return rc;
   SchedResult r;
   if ((rc = schedule(P, sched, o, 0, P.lay.chunks(), r))) return rc;
   *out = (double)(4 * (n & 1) - 2) * r.total;  // gpu_exact_dense.cu:698
@@ -184,7 +186,7 @@ int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int
   std::vector<double> A;
   if ((rc = to_double(mat, t, n, A))) return rc;
   Plan P;
-  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, nshards))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, nshards, o.device_id))) return rc;
   const uint64_t C = P.lay.chunks();
   const uint64_t c0 = C * (uint64_t)shard / (uint64_t)nshards, c1 = C * (uint64_t)(shard + 1) / (uint64_t)nshards;
   SchedResult r;
@@ -239,7 +241,7 @@ int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const 
   if (o_in) o = *o_in;
   else sup_opts_init(&o);
   Plan P;
-  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num, o.device_id))) return rc;
   if (walk_kind) *walk_kind = P.lds ? 4 : (int)P.kind;
   if (cached_bits) *cached_bits = P.kind == kWalkSeg ? P.seg_cc : 0;
   if (colmap)
@@ -258,7 +260,7 @@ int sup_prepare(const void* mat, sup_dtype t, int n, sup_kernel kernel, const su
   if (o_in) o = *o_in;
   else sup_opts_init(&o);
   Plan P;
-  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num, o.device_id))) return rc;
   if (walk_kind) *walk_kind = P.lds ? 4 : (int)P.kind;
   if (compile_ms) *compile_ms = 0.0;
   if (P.kind == kWalkSeg) return jit_compile_only(P, compile_ms);

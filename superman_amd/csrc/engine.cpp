@@ -255,7 +255,7 @@ static constexpr double kLaneOpsPerSec = 3.7e13;
 static constexpr double kJitMinSavingSec = 0.3;
 
 static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit,
-                             int ndev);
+                             int ndev, int dev);
 
 // Plans are pure functions of (matrix, request, layout): repeated calls on the
 // same matrix (the bench's steps, a shard per rank, -p6 items, reductions
@@ -274,7 +274,7 @@ std::map<PlanKey, std::pair<std::vector<double>, Plan>> g_plans;
 constexpr size_t kPlanCacheMax = 32;
 }  // namespace
 
-int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit, int ndev) {
+int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit, int ndev, int dev) {
   const size_t nn = (size_t)n * n;
   uint64_t h = 1469598103934665603ull;
   for (size_t i = 0; i < nn; ++i) {
@@ -284,7 +284,7 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
   }
   // ndev only feeds auto mode's compile-or-not decision
   const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0};
-  if (std::getenv("SUP_JIT_CC")) return plan_for_uncached(A, n, kernel, lay, P, jit, ndev);  // experiments
+  if (std::getenv("SUP_JIT_CC")) return plan_for_uncached(A, n, kernel, lay, P, jit, ndev, dev);  // experiments
   {
     std::lock_guard<std::mutex> g(g_plan_mu);
     auto it = g_plans.find(key);
@@ -293,7 +293,7 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
       return SUP_OK;
     }
   }
-  const int rc = plan_for_uncached(A, n, kernel, lay, P, jit, ndev);
+  const int rc = plan_for_uncached(A, n, kernel, lay, P, jit, ndev, dev);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(g_plan_mu);
   if (g_plans.size() >= kPlanCacheMax) g_plans.clear();
@@ -301,28 +301,62 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
   return SUP_OK;
 }
 
+// SkipPer evaluates only the states without an exactly-zero row; its jumps
+// and divergence cost it efficiency per evaluated state: measured on config 5
+// int, 25.5 modelled ops per visited state at 1.38e13 ops/s against the plain
+// walks' 3.7e13 (profiles/r1/probe_seg.log).
+static constexpr double kSkipEfficiency = 0.37;
+
+// Fraction of the states the SkipPer plan P evaluates, measured on a fixed
+// sample of its wave-chunks (8 evenly spaced ranges, ~1/64 of the walk) on
+// device `dev`; -1 without a device.  Deterministic: visited counts depend only
+// on the matrix and the chunks, not on timing.
+static double skip_visited_fraction(const Plan& P, int dev) {
+  int nd = 0;
+  if (device_count(&nd) != SUP_OK || nd < 1) return -1.0;
+  if (dev < 0 || dev >= nd) dev = 0;
+  const uint64_t C = P.lay.chunks(), len = std::max<uint64_t>(1, C / 512);
+  uint64_t vis = 0, tot = 0;
+  for (uint64_t i = 0; i < 8; ++i) {
+    uint64_t c0 = (2 * i + 1) * C / 16;
+    if (c0 + len > C) c0 = C - len;
+    RangeResult r;
+    if (run_range(dev, P, c0, c0 + len, true, r) != SUP_OK) return -1.0;
+    vis += r.visited;
+    tot += len << (P.lay.L + P.lay.m);
+  }
+  return tot ? (double)vis / (double)tot : 1.0;
+}
+
 static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit,
-                             int ndev) {
+                             int ndev, int dev) {
   // candidates in preference order; the cheapest by walk_cost wins
   std::vector<WalkKind> kinds;
   switch (kernel) {
     case SUP_KERNEL_SKIPPER: {
       // SkipPer only gains where some x_j(S) is exactly zero.  With a
       // non-integer entry that is a measure-zero coincidence, so SkipPer
-      // would evaluate every state: the segmented walk (same sum) runs
-      // instead when cheaper.  Integer matrices keep SkipPer (their exact
-      // zeros are common: config 5 int visits 22 % of the states).
+      // evaluates every state; with integer entries the fraction it
+      // evaluates is measured on a sample of its chunks (GPU; without a
+      // device the request keeps SkipPer).  The segmented walk (same sum,
+      // every state) runs instead when that is cheaper.
       int rc = make_plan(A, n, kWalkSkip, false, lay, P);
       if (rc || jit < 0 || n < 10 || lay.m < 3) return rc;
       bool integral = true;
       for (size_t i = 0; i < (size_t)n * n && integral; ++i) integral = A[i] == std::floor(A[i]);
-      if (integral) return SUP_OK;
       Plan s;
-      if (make_plan(A, n, kWalkSeg, false, lay, s) == SUP_OK && walk_cost(s) < walk_cost(P)) {
-        const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
-        const double saved = steps * (walk_cost(P) - walk_cost(s)) / kLaneOpsPerSec;
-        if (jit >= 1 || saved >= kJitMinSavingSec) P = std::move(s);
+      if (make_plan(A, n, kWalkSeg, false, lay, s) != SUP_OK) return SUP_OK;
+      const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
+      double skip_cost = walk_cost(P) / (integral ? kSkipEfficiency : 1.0);  // f <= 1
+      if (walk_cost(s) >= skip_cost) return SUP_OK;
+      if (jit < 1 && steps * (skip_cost - walk_cost(s)) / kLaneOpsPerSec < kJitMinSavingSec) return SUP_OK;
+      if (integral) {
+        const double f = skip_visited_fraction(P, dev);
+        if (f < 0.0) return SUP_OK;
+        skip_cost *= f;
       }
+      const double saved = steps * (skip_cost - walk_cost(s)) / kLaneOpsPerSec;
+      if (walk_cost(s) < skip_cost && (jit >= 1 || saved >= kJitMinSavingSec)) P = std::move(s);
       return SUP_OK;
     }
     case SUP_KERNEL_DENSE_PLAIN: return make_plan(A, n, kWalkDense, false, lay, P);

@@ -133,7 +133,10 @@ double walk_cost(const Plan& P);
 // forces the plain dense walk.
 // jit: sup_opts.jit (-1 never, 0 auto, 1 whenever the segmented walk's cost
 // model wins); ndev: devices the walk is spread over (auto mode's estimate).
-int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit = -1, int ndev = 1);
+// dev: the device a SkipPer request on an integer matrix samples its visited
+// fraction on (the decision itself does not depend on it).
+int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit = -1, int ndev = 1,
+             int dev = 0);
 
 struct RangeResult {
   double partial = 0.0;     // pairwise sum over the range's wave-chunks
