@@ -305,6 +305,15 @@ int sup_decompose(const void* mat, sup_dtype t, int n, const sup_reduce_opts* r,
 int sup_perman_reduced(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched sched, const sup_opts* o,
                        int on_cpu, const sup_reduce_opts* r, double* out, sup_stats* st);
 
+/* sup_perman_exact after the -o reductions (d1/d2/d34, as sup_perman_reduced
+ * with r->compress; scaling is refused: not exact).  The tree folds every
+ * coefficient into its leaves, so the permanent is the exact sum of the exact
+ * leaf permanents (a big integer; up to 4096 x 4096 input, leaves <= 64).
+ * st (optional): kernel_ms summed over leaves, leaves, wall_ms. */
+int sup_perman_reduced_exact(const void* mat, sup_dtype t, int n, const sup_opts* o, int on_cpu,
+                             const sup_reduce_opts* r, char* out, size_t out_len, sup_stats* st);
+
+
 /* ------------------------------------------------------------------------ *
  * Randomized estimators (reference -a, main.cu:77-103,
  * 156-183, 193-243).  Both estimate the permanent of the 0/1 nonzero pattern,

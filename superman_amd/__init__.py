@@ -374,6 +374,23 @@ def perman_reduced(mat, algo: int = 4, sparse: bool = False, compress: bool = Tr
     return (out.value, st.as_dict()) if return_stats else out.value
 
 
+def perman_reduced_exact(mat, cpu: bool = False, threads: int = 16, device_id: int = 0, gpu_num: int = 1,
+                         min_n: int = 30, max_deg: int = 5, return_stats: bool = False):
+    """-o with exact leaves (sup_perman_reduced_exact): the d1/d2/d34 tree folds
+    every coefficient into its integer leaves, so the permanent is the exact
+    sum of their exact permanents (Python int)."""
+    a, dt, n = _mat(mat, 4096)
+    lib = _lib.load()
+    o = _opts(gpu_num, device_id, threads)
+    r = _reduce_opts(True, None, min_n, max_deg)
+    buf = C.create_string_buffer(1 << 16)
+    st = SupStats()
+    _lib.check(lib.sup_perman_reduced_exact(a.ctypes.data, dt, n, C.byref(o), int(bool(cpu)), C.byref(r), buf,
+                                            len(buf), C.byref(st)), "perman_reduced_exact")
+    v = int(buf.value.decode())
+    return (v, st.as_dict()) if return_stats else v
+
+
 def read_mtx(path: str, binary: bool = False) -> tuple[np.ndarray, str, int]:
     """MatrixMarket coordinate file -> (matrix, type name, nz lines) (read_matrix.hpp:11-157)."""
     lib = _lib.load()

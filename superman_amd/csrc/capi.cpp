@@ -232,6 +232,43 @@ int sup_perman_exact(const void* mat, sup_dtype t, int n, const sup_opts* o_in, 
   return SUP_OK;
 }
 
+int sup_perman_reduced_exact(const void* mat, sup_dtype t, int n, const sup_opts* o_in, int on_cpu,
+                             const sup_reduce_opts* r_in, char* out, size_t out_len, sup_stats* st) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!mat || !out || out_len < 2 || n < 1 || n > SUP_MAX_READ_N) {
+    set_error("sup_perman_reduced_exact: bad argument");
+    return SUP_EINVAL;
+  }
+  const size_t nn = (size_t)n * n;
+  std::vector<double> A(nn);
+  for (size_t i = 0; i < nn; ++i)
+    A[i] = t == SUP_INT32 ? (double)((const int32_t*)mat)[i]
+           : t == SUP_FLOAT32 ? (double)((const float*)mat)[i] : ((const double*)mat)[i];
+  sup_opts o;
+  if (o_in) o = *o_in;
+  else sup_opts_init(&o);
+  sup_reduce_opts r;
+  if (r_in) r = *r_in;
+  else sup_reduce_opts_init(&r);
+  std::string s;
+  double kms = 0.0;
+  int leaves = 0, rc;
+  if ((rc = exact_perman_reduced(A.data(), n, o, on_cpu != 0, r, s, &kms, &leaves))) return rc;
+  if (s.size() + 1 > out_len) {
+    set_error("sup_perman_reduced_exact: output buffer too small");
+    return SUP_EINVAL;
+  }
+  std::memcpy(out, s.c_str(), s.size() + 1);
+  if (st) {
+    std::memset(st, 0, sizeof(*st));
+    st->kernel_ms = kms;
+    st->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    st->leaves = leaves;
+    st->walk_kind = (int)kWalkDense;
+  }
+  return SUP_OK;
+}
+
 int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o_in, int* walk_kind,
                   int* colmap, int* L, int* m, int* cached_bits) {
   std::vector<double> A;

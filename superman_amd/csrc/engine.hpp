@@ -189,5 +189,8 @@ void cpu_exact_range(const Plan& P, uint64_t c0, uint64_t c1, const std::vector<
 // Exact permanent of integer-valued A as a decimal string (sup_perman_exact).
 int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::string& out, double* kernel_ms,
                  int* devices_used);
+// The same after the -o reductions (sup_perman_reduced_exact): exact leaves, big-integer sum.
+int exact_perman_reduced(const double* A, int n, const sup_opts& o, bool on_cpu, const sup_reduce_opts& r,
+                         std::string& out, double* kernel_ms, int* leaves);
 
 }  // namespace sup

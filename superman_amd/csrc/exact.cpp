@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -71,6 +72,23 @@ struct Big {
     }
     while (carry) d.push_back((uint32_t)carry), carry >>= 32;
     trim();
+  }
+  void add(const Big& o) {  // *this += o
+    u128 carry = 0;
+    if (d.size() < o.d.size()) d.resize(o.d.size(), 0u);
+    for (size_t i = 0; i < d.size(); ++i) {
+      const u128 v = (u128)d[i] + (i < o.d.size() ? o.d[i] : 0u) + carry;
+      d[i] = (uint32_t)v;
+      carry = v >> 32;
+    }
+    if (carry) d.push_back((uint32_t)carry);
+    trim();
+  }
+  static Big from_dec(const std::string& s) {
+    Big b;
+    for (char c : s)
+      if (c >= '0' && c <= '9') b.mul_add(10, (uint64_t)(c - '0'));
+    return b;
   }
   int cmp(const Big& o) const {
     if (d.size() != o.d.size()) return d.size() < o.d.size() ? -1 : 1;
@@ -269,6 +287,67 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
   out = (neg && !T.zero() ? "-" : "") + T.dec();
   if (kernel_ms) *kernel_ms = kms;
   if (devices_used) *devices_used = used;
+  return SUP_OK;
+}
+
+// -o reductions with exact leaves: without scaling the d1/d2/d34 tree folds
+// every coefficient into its leaf matrices (integers stay integers), so
+// perm(A) = sum of the leaf permanents; each leaf is computed exactly and the
+// sum is a big integer (the fp64 combine of the same tree loses every digit on
+// chesapeake).
+namespace {
+struct ReducedExact {
+  const sup_opts* o;
+  bool on_cpu;
+  Big pos, neg;
+  double kms = 0.0;
+  std::string err;
+};
+int reduced_leaf(const double* a, int n, void* user, double* out) {
+  ReducedExact* R = (ReducedExact*)user;
+  std::string s;
+  double kms = 0.0;
+  int used = 0;
+  const int rc = exact_perman(a, n, *R->o, R->on_cpu, s, &kms, &used);
+  if (rc) {
+    R->err = last_error();
+    return rc;
+  }
+  R->kms += kms;
+  const bool negative = !s.empty() && s[0] == '-';
+  (negative ? R->neg : R->pos).add(Big::from_dec(s));
+  *out = std::strtod(s.c_str(), nullptr);
+  return SUP_OK;
+}
+}  // namespace
+
+int exact_perman_reduced(const double* A, int n, const sup_opts& o, bool on_cpu, const sup_reduce_opts& r,
+                         std::string& out, double* kernel_ms, int* leaves) {
+  if (r.scale_threshold > 0.0) {
+    set_error("sup_perman_reduced_exact: scaling (-u) is not exact");
+    return SUP_EUNSUPPORTED;
+  }
+  ReducedExact R;
+  R.o = &o;
+  R.on_cpu = on_cpu;
+  sup_reduce_opts rr = r;
+  rr.compress = 1;
+  double approx = 0.0;
+  int nl = 0;
+  const int rc = sup_decompose(A, SUP_FLOAT64, n, &rr, reduced_leaf, &R, &approx, &nl);
+  if (rc) {
+    if (!R.err.empty()) set_error(R.err);
+    return rc;
+  }
+  if (R.pos.cmp(R.neg) >= 0) {
+    R.pos.sub(R.neg);
+    out = R.pos.dec();
+  } else {
+    R.neg.sub(R.pos);
+    out = "-" + R.neg.dec();
+  }
+  if (kernel_ms) *kernel_ms = R.kms;
+  if (leaves) *leaves = nl;
   return SUP_OK;
 }
 

@@ -217,18 +217,19 @@ int main(int argc, char** argv) {
   o.jit = c.jit;
 
   if (c.exact) {  // exact integer permanent (any -p: the sum does not depend on the kernel)
-    if (reduce) {
-      std::fprintf(stderr, "perman: --exact does not combine with -o / -u\n");
+    if (c.scaling > 0.0) {
+      std::fprintf(stderr, "perman: --exact does not combine with -u (scaling is not exact)\n");
       sup_free(mat);
       return 1;
     }
     if (c.gpu && c.perman_algo != 5 && c.perman_algo != 6 && c.perman_algo != 8) o.gpu_num = 1;
-    char buf[1024];
+    static char buf[1 << 16];
     sup_stats st;
     int rc = SUP_OK;
     const auto t0 = std::chrono::steady_clock::now();
     for (int rep = 0; rep < c.reps && rc == SUP_OK; ++rep)
-      rc = sup_perman_exact(mat, t, n, &o, c.gpu ? 0 : 1, buf, sizeof buf, &st);
+      rc = reduce ? sup_perman_reduced_exact(mat, t, n, &o, c.gpu ? 0 : 1, &ro, buf, sizeof buf, &st)
+                  : sup_perman_exact(mat, t, n, &o, c.gpu ? 0 : 1, buf, sizeof buf, &st);
     const double sec =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / (double)c.reps;
     sup_free(mat);

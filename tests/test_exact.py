@@ -121,3 +121,29 @@ def test_tiny_and_degenerate(sup, orc):
     for a in (np.array([[5]]), np.array([[-7]]), np.array([[1, 2], [3, 4]]), np.zeros((2, 2)),
               np.array([[1, -1, 2], [0, 3, -4], [5, 6, -7]]), np.zeros((5, 5))):
         assert sup.perman_exact(a.astype(np.int32), cpu=True, threads=2) == orc.exact_perman(a)
+
+
+def test_reduced_exact_vs_direct(sup, orc, tmp_path):
+    """-o with exact leaves: the d1/d2/d34 tree folds its coefficients into the
+    integer leaves, so the exact leaf permanents add up to the exact permanent."""
+    rng = np.random.default_rng(3)
+    n = 26
+    a = np.where(rng.random((n, n)) < 0.12, rng.integers(1, 4, (n, n)), 0).astype(np.int32)
+    a[np.arange(n), rng.permutation(n)] = 1
+    r, st = sup.perman_reduced_exact(a, cpu=True, threads=8, min_n=12, return_stats=True)
+    assert st["leaves"] > 10
+    assert r == sup.perman_exact(a, cpu=True, threads=8) == orc.exact_perman_crt(a, 8)
+    # CLI -o -E (singleton compression, then one leaf at this size)
+    path = tmp_path / "m26"
+    nz = np.argwhere(a != 0)
+    with open(path, "w") as f:
+        f.write(f"{n} {len(nz)} int\n")
+        for i, j in nz:
+            f.write(f"{i} {j} {a[i, j]}\n")
+    exe = os.path.join(ROOT, "superman_amd", "bin", "perman")
+    out = subprocess.run([exe, "-f", str(path), "-c", "-E", "-o", "-t", "8"], capture_output=True, text=True,
+                         check=True)
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("Permanent:")][0]
+    assert int(line.split()[1]) == r
+    with pytest.raises(sup.SupError):
+        sup.perman_reduced_exact(a.astype(np.float64) + 0.5, cpu=True)

@@ -111,3 +111,21 @@ def test_gpu_exact_tiny(sup, orc):
     for n in range(1, 9):
         a = rng.integers(-3, 4, (n, n)).astype(np.int32)
         assert sup.perman_exact(a) == orc.exact_perman(a), n
+
+
+def test_gpu_chesapeake_exact_two_ways(sup):
+    """chesapeake (n = 39, the matrix whose fp64 -o reduction has no correct digit
+    in the reference or here): the exact permanent from the -o tree
+    (231 exact leaves, big-integer sum) equals the exact direct walk.  The matrix
+    cancels badly: the fp64 direct walk is within the north star's 1e-6, closer
+    than the best of the reference's five published runs
+    (revised_perman/sparyser/RealResults/chesapeake.mtx.a*.out: 13173497329080 at
+    best, 1.2e-6 off)."""
+    a, _, _ = sup.read_mtx(fixture_path("mtx/chesapeake.mtx"))
+    r, st = sup.perman_reduced_exact(a, return_stats=True)
+    assert st["leaves"] == 231
+    d = sup.perman_exact(a)
+    assert r == d == 13173481190272
+    published_best = 13173497329080
+    err = rel(float(d), sup.perman(a, algo=4, jit=1))
+    assert err < 1e-6 and err < rel(float(d), float(published_best))
