@@ -210,6 +210,18 @@ double chunk_partial(const Plan& P, uint64_t ga) {
   const uint32_t T = 1u << m;
   double lane_val[64];
   if (P.kind == kWalkSeg) {
+    // the kernel's chunk skip: the outer tree's tail (rows no walk bit touches)
+    // is an exact zero in every valid lane -> the chunk's part is +0
+    const ProdTree& ot = P.outer_tree;
+    if (ot.tail_hi > ot.tail_lo) {
+      bool live = false;
+      for (unsigned l = 0; l < (1u << L) && !live; ++l) {
+        Lane s;
+        chunk_start(P, ga, l, s);
+        live = seg_tree(s.x, ot.tail_lo, ot.tail_hi) != 0.0;
+      }
+      if (!live) return 0.0;
+    }
     for (unsigned l = 0; l < 64; ++l) {
       if (l >= (1u << L)) {
         lane_val[l] = 0.0;

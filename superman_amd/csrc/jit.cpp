@@ -558,12 +558,20 @@ struct Gen {
             << ";\n";
       }
     tree_init(outer, "      ");
+    // Rows no walk bit touches (the outer tree's tail, Ro) are constant over the
+    // chunk: when Ro is an exact zero in every valid lane (integer matrices),
+    // every product of the chunk is zero and the walk is skipped (part = +0).
+    o << "      double acc = 0.0;\n";
+    if (P.outer_tree.tail_hi > P.outer_tree.tail_lo)
+      o << "      if (__builtin_amdgcn_ballot_w64(lane_valid && " << outer.T << " != 0.0) != 0) {\n";
+    else
+      o << "      {\n";
     tree_init(inx, "      ");
     tree_init(iny, "      ");
     set_d("      ", true);
     {
       const std::string U = outer.top(0);
-      o << "      double acc = " << (U.empty() ? dname(0) : dname(0) + " * " + U) << ";\n";
+      o << "      acc = " << (U.empty() ? dname(0) : dname(0) + " * " + U) << ";\n";
     }
     o << "      for (uint32_t q = 0; q < " << Q << "u; ++q) {\n";
     const char* ind = "        ";
@@ -600,6 +608,7 @@ struct Gen {
     }
     o << "      }\n";
     o << "      if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;\n";
+    o << "      }\n";
     o << "      const double part = wave_sum(lane_valid ? acc : 0.0);\n";
     o << "      keep = (lane == j) ? part : keep;\n";
     o << "    }\n";
@@ -693,6 +702,8 @@ int build_seg(Plan& P) {
     P.seg_cc = f.cc;
     P.seg_ops = f.ops;
     P.seg_regs = f.regs;
+    if (std::getenv("SUP_JIT_VERBOSE"))
+      std::fprintf(stderr, "seg plan n=%d m=%d ops/step=%.4f regs=%d cc=%d\n", n, m, f.ops, f.regs, f.cc);
   }
   P.jofs.assign(m, 0);
   P.jtab.clear();

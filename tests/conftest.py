@@ -2,6 +2,7 @@ import json
 import os
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -45,3 +46,29 @@ def rel(a: float, b: float) -> float:
     if a == b:
         return 0.0
     return abs(a - b) / max(abs(a), abs(b), 1e-300)
+
+
+def seg_skip_fraction(sup, a, kernel="sparse"):
+    """Fraction of wave-chunks whose rows untouched by the walk bits (the
+    segmented walk's outer-tree tail) hold an exact zero in every lane, i.e. the
+    chunks the generated kernel skips; restated from the plan's column map in
+    numpy (x0 = a[:, n-1] - rowsum / 2, chunk-start Gray state of the lane and
+    chunk bits)."""
+    n = a.shape[0]
+    info = sup.plan_info(a, kernel, jit=1)
+    cm, L, m = [int(c) for c in info["colmap"]], info["L"], info["m"]
+    x0 = a[:, n - 1] - a.sum(1) / 2
+    rest = [j for j in range(n) if not a[j, cm[L:L + m]].any()]
+    if not rest:
+        return 0.0
+    cols = cm[:L] + cm[L + m:]
+    h = len(cols) - L
+    allz = np.ones(1 << h, bool)
+    for lane in range(1 << L):
+        p = (np.arange(1 << h, dtype=np.int64) << L) | lane
+        g = p ^ (p >> 1)
+        x = np.tile(x0[rest], (1 << h, 1))
+        for k, c in enumerate(cols):
+            x += ((g >> k) & 1)[:, None] * a[rest][:, c][None, :]
+        allz &= (x == 0).any(1)
+    return float(allz.mean())

@@ -144,3 +144,18 @@ def test_seg_n40_d02_companion(sup):
     b = a.copy()
     b[7] *= 4.0
     assert sup.perman(b, algo=4, jit=1) == r_seg * 4.0
+
+
+@pytest.mark.parametrize("n,d,seed", [(20, 0.2, 1), (24, 0.15, 3)])
+def test_seg_chunk_skip_gpu(sup, orc, n, d, seed):
+    """Wave-chunks whose walk-untouched rows are exactly zero in every lane are
+    skipped by the generated kernel: GPU == host twin (same skip) == oracle
+    mirror (walks them) bit for bit, and the exact permanent."""
+    from conftest import seg_skip_fraction
+    from test_seg import _skip_case
+    a = _skip_case(sup, n, d, seed)
+    assert seg_skip_fraction(sup, a) >= 0.25
+    got, st = sup.perman(a, algo=4, kernel="seg", return_stats=True)
+    assert st["walk_kind"] == 3
+    assert got == sup.perman_cpu(a, "seg", threads=8) == orc.engine_perman_as(sup, a, "seg", threads=8)
+    assert rel(got, float(orc.exact_perman_crt(a))) < 1e-13

@@ -106,3 +106,25 @@ def test_dense_lds_plan_and_cpu(sup, orc):
     got = sup.perman_cpu(a, "dense_lds", threads=4)
     assert got == sup.perman_cpu(a, "dense_plain", threads=4)
     assert got == orc.engine_perman_as(sup, a, "dense_lds", threads=4)
+
+
+def _skip_case(sup, n, d, seed):
+    rng = np.random.default_rng(seed)
+    mask = rng.random((n, n)) < d
+    mask[np.arange(n), rng.permutation(n)] = True
+    a = np.where(mask, rng.integers(1, 6, (n, n)), 0).astype(np.float64)
+    return sup.skip_order(a)[0]
+
+
+@pytest.mark.parametrize("n,d,seed", [(20, 0.2, 1), (24, 0.15, 3)])
+def test_cpu_seg_chunk_skip(sup, orc, n, d, seed):
+    """Integer matrices whose rows untouched by the walk are exactly zero in
+    whole wave-chunks: the walk skips those chunks (25 % and 56 % here); the
+    host twin (which skips the same chunks) == the oracle mirror (which walks
+    them and gets +-0) == the exact permanent."""
+    from conftest import seg_skip_fraction
+    a = _skip_case(sup, n, d, seed)
+    assert seg_skip_fraction(sup, a) >= 0.25
+    got = sup.perman_cpu(a, "seg", threads=8)
+    assert got == orc.engine_perman_as(sup, a, "seg", threads=8)
+    assert rel(got, float(orc.exact_perman_crt(a))) < 1e-13
