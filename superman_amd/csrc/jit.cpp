@@ -41,9 +41,16 @@
 // kernels, and the arithmetic is mirrored bit for bit by engine_cpu.cpp
 // (tree_*, seg_*) and oracle/oracle.c (kind 3).
 //
+// Chunk skip.  Rows no walk bit touches (the outer tree's tail) are constant
+// over a wave-chunk; when their product is an exact zero in every valid lane
+// the chunk's walk is skipped (integer matrices; config 5: 60% of chunks).
+//
 // Compiled code objects are cached in memory (per process, per device) and on
 // disk: $SUP_JIT_CACHE_DIR, else $XDG_CACHE_HOME/superman_amd, else
 // ~/.cache/superman_amd (SUP_JIT_CACHE_DIR="" disables the disk cache).
+// Debugging / experiment knobs: SUP_JIT_DUMP=<dir> keeps the generated source,
+// SUP_JIT_VERBOSE prints the plan's op count, live values and cached bits,
+// SUP_JIT_CC / SUP_JIT_WAVES / SUP_JIT_LDS force cached bits, occupancy, LDS.
 #include <hip/hiprtc.h>
 #include <sys/stat.h>
 #include <unistd.h>
