@@ -33,3 +33,30 @@ for name in [k for k in exact if not k.startswith("_")]:
         row.append(f"{label} {err:.2e} ({st['kernel_ms']:.0f} ms)")
     os.environ.pop("SUP_JIT_CC", None)
     print(f"{name} n={a.shape[0]}: " + " | ".join(row), flush=True)
+
+# random integer matrices (values 1..5, a permutation's diagonal forced nonzero):
+# the exact integer path gives the ground truth
+import numpy as np  # noqa: E402
+
+geo = {label: [] for label, *_ in runs}
+for n, d, seeds in ((36, 0.5, range(6)), (38, 0.3, range(6, 10))):
+    for seed in seeds:
+        rng = np.random.default_rng(1000 + seed)
+        mask = rng.random((n, n)) < d
+        mask[np.arange(n), rng.permutation(n)] = True
+        a = np.where(mask, rng.integers(1, 6, (n, n)), 0).astype(np.float64)
+        e = S.perman_exact(a)
+        row = []
+        for label, kernel, jit, cc in runs:
+            if cc is None:
+                os.environ.pop("SUP_JIT_CC", None)
+            else:
+                os.environ["SUP_JIT_CC"] = cc
+            v = S.perman(a, kernel=kernel, jit=jit)
+            err = float(abs(Fraction(v) - e) / e)
+            geo[label].append(max(err, 1e-18))
+            row.append(f"{label} {err:.1e}")
+        os.environ.pop("SUP_JIT_CC", None)
+        print(f"random int n={n} d={d} seed={seed}: " + " | ".join(row), flush=True)
+print("geometric mean rel.err over the random matrices: " +
+      " | ".join(f"{k} {float(np.exp(np.mean(np.log(v)))):.1e}" for k, v in geo.items()), flush=True)
