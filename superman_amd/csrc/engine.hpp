@@ -88,6 +88,8 @@ struct Plan {
   std::vector<double> jtab;        // packed touched values: + block, - block (each padded to 8)
   std::string jit_src;             // generated HIP source of the specialised kernel
   uint64_t jit_key = 0;            // hash of jit_src + compile options
+  uint64_t uid = 0;                // plan-cache identity (0: uncached); a device that holds
+                                   // this plan's tables skips their upload (run_range)
 };
 
 // Build a plan.  identity_map keeps engine bit e = column e (needed when a
