@@ -392,12 +392,17 @@ typedef struct {
   char dyn[ORC_MAXN];             /* rows some walk bit > segb touches */
 } eplan;
 
-/* Layout: L = min(6, n-1); m = max(min(rest, 10), rest - 20); h = rest - m. */
+/* Layout: L = min(6, n-1); m = max(min(rest, 10), rest - 20), shortened for small n (rest - m < 13)
+   to max(min(rest, 6), rest - 13) so that there are 2^13 wave-chunks; h = rest - m. */
 void orc_engine_layout(int n, int* L, int* m, int* h) {
   int nb = n - 1;
   int l = nb < 6 ? nb : 6;
   int rest = nb - l;
   int mm = rest < 10 ? rest : 10;
+  if (rest - mm < 13) {  /* small n: shorter walks, 2^13 wave-chunks */
+    int lo = rest < 6 ? rest : 6;
+    mm = rest - 13 > lo ? rest - 13 : lo;
+  }
   if (rest - 20 > mm) mm = rest - 20;
   if (mm > 31) mm = 31;
   *L = l;

@@ -104,7 +104,10 @@ def layout(n: int) -> tuple[int, int, int]:
     nb = n - 1
     L = min(6, nb)
     rest = nb - L
-    m = min(max(min(rest, 10), rest - 20), 31)
+    m = min(rest, 10)
+    if rest - m < 13:  # small n: shorter walks, 2^13 wave-chunks (engine.cpp default_layout)
+        m = max(min(rest, 6), rest - 13)
+    m = min(max(m, rest - 20), 31)
     return L, m, rest - m
 
 

@@ -79,7 +79,10 @@ Layout default_layout(int n) {
   // >= 2^10 walk steps per wave-chunk when possible, and at most 2^20
   // wave-chunks (8 MiB of partials) — fine-grained enough that the dynamic
   // chunk queue balances a whole MI355X (~5k resident waves) to < 1 %.
+  // Small n (rest < 23): the walk shortens (down to 2^6 steps) until there are
+  // 2^13 wave-chunks, so the whole chip walks instead of a few waves.
   int m = rest < 10 ? rest : 10;
+  if (rest - m < 13) m = std::max(std::min(rest, 6), rest - 13);
   if (rest - 20 > m) m = rest - 20;
   if (m > 31) m = 31;  // 32-bit walk index in the kernels (n > 58 only)
   l.m = m;
