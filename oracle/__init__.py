@@ -138,7 +138,15 @@ def engine_perman_as(sup_module, a, kernel="dense", threads: int = 8, jit: int =
     """Mirror of exactly the plan the product runs for `kernel` (walk kind,
     column map and cached walk bits queried through the C ABI's sup_plan_info)."""
     info = sup_module.plan_info(a, kernel, jit=jit)
-    return engine_perman(a, info["kind"], info["colmap"], threads, info.get("cached", 0))
+    n = _d(a).shape[0]
+    L, m, _ = engine_layout(n)
+    if (info["L"], info["m"]) == (L, m):
+        return engine_perman(a, info["kind"], info["colmap"], threads, info.get("cached", 0))
+    # the plan's own layout (the segmented walk lengthens its wave-chunks)
+    h = n - 1 - info["L"] - info["m"]
+    s, _ = engine_range(a, info["kind"], 0, 1 << h, info["L"], info["m"], info["colmap"], threads,
+                        info.get("cached", 0))
+    return (4 * (n & 1) - 2) * s
 
 
 def exact_perman(a) -> Fraction:

@@ -725,6 +725,7 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
           D[S] = e_tree_top(&inner, xs[S], &vx[S]) - e_tree_top(&inner, ys[S], &vy[S]);
         }
         acc = D[0] * e_tree_top(&outer, xs[0], &vo[0]);
+        double tot = 0.0; /* two-level lane sum: acc folds into tot after pair j = 2^segb (q + 1) */
         /* pair j = Gray steps 2j, 2j+1: contributes (-1)^j D U1, in the
          * state of its Gray bits 1..cc */
         for (unsigned j = 1; j < T / 2; ++j) {
@@ -734,7 +735,9 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
             e_seg_step(P, &outer, &inner, xs[S2], ys[S2], &vo[S2], &vx[S2], &vy[S2], &D[S2], (int)pb + 1, (int)neg);
           for (int i = 0; i < P->cc; ++i) S |= (int)(((j >> i) ^ (j >> (i + 1))) & 1u) << i;
           acc = fma((j & 1u) ? -D[S] : D[S], e_tree_top(&outer, xs[S], &vo[S]), acc);
+          if ((j & ((1u << P->segb) - 1u)) == 0u) tot += acc, acc = 0.0;
         }
+        acc = tot + acc;
       } else if (P->kind == 0) {
         acc = e_prod4(x, n);
         for (unsigned t = 1; t < T; ++t) {

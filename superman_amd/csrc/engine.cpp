@@ -337,6 +337,7 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
                              int ndev, int dev) {
   // candidates in preference order; the cheapest by walk_cost wins
   std::vector<WalkKind> kinds;
+  auto make_seg = [&](Plan& s) { return make_plan(A, n, kWalkSeg, false, lay, s); };
   switch (kernel) {
     case SUP_KERNEL_SKIPPER: {
       // SkipPer only gains where some x_j(S) is exactly zero.  With a
@@ -350,7 +351,7 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
       bool integral = true;
       for (size_t i = 0; i < (size_t)n * n && integral; ++i) integral = A[i] == std::floor(A[i]);
       Plan s;
-      if (make_plan(A, n, kWalkSeg, false, lay, s) != SUP_OK) return SUP_OK;
+      if (make_seg(s) != SUP_OK) return SUP_OK;
       const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
       double skip_cost = walk_cost(P) / (integral ? kSkipEfficiency : 1.0);  // f <= 1
       if (walk_cost(s) >= skip_cost) return SUP_OK;
@@ -375,7 +376,7 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
         set_error("the segmented walk needs n >= 10 (>= 3 walk bits)");
         return SUP_EUNSUPPORTED;
       }
-      return make_plan(A, n, kWalkSeg, false, lay, P);
+      return make_seg(P);
     case SUP_KERNEL_SPARYSER: kinds = {kWalkSparse}; break;
     case SUP_KERNEL_DENSE: kinds = {kWalkDense}; if (n >= 8) kinds.push_back(kWalkSparse); break;
     default: set_error("unknown sup_kernel"); return SUP_EINVAL;
@@ -389,7 +390,7 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
   }
   if (jit >= 0 && n >= 8 && lay.m >= 3) {
     Plan s;
-    if (make_plan(A, n, kWalkSeg, false, lay, s) == SUP_OK && walk_cost(s) < walk_cost(best)) {
+    if (make_seg(s) == SUP_OK && walk_cost(s) < walk_cost(best)) {
       const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
       const double saved = steps * (walk_cost(best) - walk_cost(s)) / kLaneOpsPerSec;
       if (jit >= 1 || saved >= kJitMinSavingSec) best = std::move(s);

@@ -232,12 +232,19 @@ double chunk_partial(const Plan& P, uint64_t ga) {
       static thread_local SegLane g;
       seg_init(s, g, P);
       double acc = g.D[0] * tree_top(P.outer_tree, g.x[0], g.o[0]);
+      // two-level lane sum (the kernel's): acc folds into tot after each shared
+      // dyn step's pair j = 2^seg_b (q + 1), so no sequential sum runs longer
+      // than 2^seg_b pairs
+      double tot = 0.0;
+      const uint32_t qmask = (1u << P.seg_b) - 1u;
       for (uint32_t j = 1; j < T / 2; ++j) {  // pair steps: walk bit ctz(j) + 1
         const uint32_t pb = __builtin_ctz(j);
         seg_step(g, P, (int)pb + 1, (j >> (pb + 1)) & 1u);
         const int S = seg_state(j, P.seg_cc);
         acc = std::fma((j & 1u) ? -g.D[S] : g.D[S], tree_top(P.outer_tree, g.x[S], g.o[S]), acc);
+        if ((j & qmask) == 0u) tot += acc, acc = 0.0;
       }
+      acc = tot + acc;
       const unsigned par = (unsigned)__builtin_popcount(l) & 1u;
       if ((((unsigned)ga) ^ par) & 1u) acc = -acc;
       lane_val[l] = acc;

@@ -580,6 +580,9 @@ struct Gen {
       const std::string U = outer.top(0);
       o << "      acc = " << (U.empty() ? dname(0) : dname(0) + " * " + U) << ";\n";
     }
+    // two-level lane sum: acc folds into tot after each shared dyn step, so
+    // no sequential sum runs longer than 2^b pairs (error growth)
+    o << "      double tot = 0.0;\n";
     o << "      for (uint32_t q = 0; q < " << Q << "u; ++q) {\n";
     const char* ind = "        ";
     // pair index j = B*q + s, s = 1 .. B-1: pair bit p = ctz(s) (walk bit p+1);
@@ -611,9 +614,11 @@ struct Gen {
       adds(P.dyn_rows, true, ind);
       products(P.seg_b, ind);
       accumulate(false, 0u, "          ");
+      o << ind << "  tot += acc;\n" << ind << "  acc = 0.0;\n";
       o << ind << "}\n";
     }
     o << "      }\n";
+    o << "      acc = tot + acc;\n";
     o << "      if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;\n";
     o << "      }\n";
     o << "      const double part = wave_sum(lane_valid ? acc : 0.0);\n";

@@ -128,3 +128,4 @@ def test_cpu_seg_chunk_skip(sup, orc, n, d, seed):
     got = sup.perman_cpu(a, "seg", threads=8)
     assert got == orc.engine_perman_as(sup, a, "seg", threads=8)
     assert rel(got, float(orc.exact_perman_crt(a))) < 1e-13
+
