@@ -159,3 +159,17 @@ def test_seg_chunk_skip_gpu(sup, orc, n, d, seed):
     assert st["walk_kind"] == 3
     assert got == sup.perman_cpu(a, "seg", threads=8) == orc.engine_perman_as(sup, a, "seg", threads=8)
     assert rel(got, float(orc.exact_perman_crt(a))) < 1e-13
+
+
+def test_seg_shared_steps_and_lane_fold_gpu(sup, orc):
+    """The n = 28 case of test_seg.py (shared steps, two-level lane sum) on the
+    GPU: == host twin == oracle mirror bit for bit."""
+    rng = np.random.default_rng(28)
+    n = 28
+    mask = rng.random((n, n)) < 0.15
+    mask[np.arange(n), rng.permutation(n)] = True
+    a = np.where(mask, rng.random((n, n)) * 3, 0).astype(np.float64)
+    a = sup.sort_order(a)[0]
+    got, st = sup.perman(a, algo=4, kernel="seg", return_stats=True)
+    assert st["walk_kind"] == 3
+    assert got == sup.perman_cpu(a, "seg", threads=8) == orc.engine_perman_as(sup, a, "seg", threads=8)

@@ -129,3 +129,21 @@ def test_cpu_seg_chunk_skip(sup, orc, n, d, seed):
     assert got == orc.engine_perman_as(sup, a, "seg", threads=8)
     assert rel(got, float(orc.exact_perman_crt(a))) < 1e-13
 
+
+
+def test_cpu_seg_shared_steps_and_lane_fold(sup, orc):
+    """n = 28 (8 walk bits, 5 specialised pair bits): the shared step of the
+    walk bits above them and the two-level lane sum (acc folds into the running
+    total after each shared step) run on the CPU too; host twin == oracle
+    mirror bit for bit, and the prefix walk to 1e-11."""
+    rng = np.random.default_rng(28)
+    n = 28
+    mask = rng.random((n, n)) < 0.15
+    mask[np.arange(n), rng.permutation(n)] = True
+    a = np.where(mask, rng.random((n, n)) * 3, 0).astype(np.float64)
+    a = sup.sort_order(a)[0]
+    info = sup.plan_info(a, "seg")
+    assert info["m"] - 1 > 5  # more pair bits than specialised ones: shared steps + folds
+    got = sup.perman_cpu(a, "seg", threads=8)
+    assert got == orc.engine_perman_as(sup, a, "seg", threads=8)
+    assert rel(got, sup.perman_cpu(a, "sparse", threads=8)) < 1e-11
