@@ -190,7 +190,7 @@ def main():
         jit = args.jit if jit is None else jit
         # plan + (segmented walk) hiprtc compile, once, before the timed region;
         # gpu_num = world so that --jit 0 decides as the N-rank plan would
-        prep = S.prepare(a, kernel, jit=jit, gpu_num=world)
+        prep = S.prepare(a, kernel, jit=jit, gpu_num=world, device_id=dev)
 
         def step():
             part, st = S.perman_shard(a, rank, world, kernel=kernel, device_id=dev, return_stats=True,
@@ -234,16 +234,16 @@ def main():
         e2, perm2, kms2, st2, _ = timed(b)
         Lb, mb, _ = S.layout(nb)
         b0, b1 = shard_chunks(nb, rank, world)
-        ach = 2.0 * nb * ((b1 - b0) << (Lb + mb)) / (kms2 * 1e-3) / 1e12  # same definition as the headline
+        ach = st2["est_ops_per_step"] * ((b1 - b0) << (Lb + mb)) / (kms2 * 1e-3) / 1e12  # as the headline
         also.append({"matrix": os.path.basename(path).replace("__", "/"), "n": nb,
                      "density": round(float((b != 0).sum()) / (nb * nb), 4),
                      "value": args.steps * (1 << (nb - 1)) / e2, "unit": "gray-steps/s",
                      "ms_per_step": e2 / args.steps * 1e3, "kernel_ms_avg": kms2,
                      "walk": walk_names[st2["walk_kind"]],
                      "roofline": {"achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                  "frac": ach / FP64_PEAK_TFLOPS,
-                                  "issue_frac": st2["est_ops_per_step"] * ((b1 - b0) << (Lb + mb)) /
-                                  (kms2 * 1e-3) / (FP64_PEAK_TFLOPS * 1e12 / 2)},
+                                  "frac": ach / FP64_PEAK_TFLOPS, "issue_frac": ach / (FP64_PEAK_TFLOPS / 2),
+                                  "gray_step_equiv_frac": 2.0 * nb * ((b1 - b0) << (Lb + mb)) /
+                                  (kms2 * 1e-3) / 1e12 / FP64_PEAK_TFLOPS},
                      "est_fp64_ops_per_step": st2["est_ops_per_step"], "permanent": perm2})
 
     # the other BASELINE configs (2, 3, 5), same shards / all-reduce / clock.
@@ -283,8 +283,19 @@ def main():
 
     total_steps = args.steps * (1 << (n - 1))
     value = total_steps / elapsed
-    flops = 2.0 * n * my_steps  # n fp64 adds + n fp64 muls per Gray step
+    # Roofline of the walk kernel.  Algorithmic work per Gray step = the fp64
+    # operations of the walk that runs (its cost model: est_ops_per_step, 18.0
+    # for the bench matrix's segmented walk), so `frac` is a true
+    # fraction of the fp64 peak.  Every one of those ops is an add, a mul or an
+    # fma issued as one VALU instruction; counting each as one flop (an fma as
+    # one too) makes `achieved` a lower bound.  Without FMA the issue ceiling
+    # is peak / 2, hence `issue_frac` = achieved / (peak / 2).  SURVEY §8(d)'s
+    # nominal 2n flops per Gray step (the plain walk's n adds + n muls) is kept
+    # as gray_step_equiv_*: the rate the plain algorithm would need.
+    ops_step = st["est_ops_per_step"]
+    flops = ops_step * my_steps
     achieved = flops / (k_ms * 1e-3) / 1e12
+    nominal = 2.0 * n * my_steps / (k_ms * 1e-3) / 1e12
     walk = {0: f"sup::walk_dense<{n}>", 1: f"sup::walk_sparse<{n}>", 2: f"sup::walk_skip<{n}>",
             3: "sup_walk_seg", 4: f"sup::walk_lds<{n}>"}[st["walk_kind"]]
     pmc = pmc_record(n, walk)
@@ -315,15 +326,15 @@ def main():
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": walk, "kernel_ms_avg": k_ms,
                      "algorithmic_flops_per_launch": flops,
-                     "flops_definition": "2n fp64 flops per Gray step (n adds + n muls, SURVEY 8(d)); the "
-                                         f"{walk} walk skips the operations structural zeros make redundant, "
-                                         f"so it executes ~{st['est_ops_per_step']:.1f} fp64 VALU ops per step "
-                                         f"(cost model) instead of {2 * n + 1}; fp64 issue ceiling without FMA "
-                                         "= 0.5 of peak",
-                     # executed (cost-model) fp64 VALU ops / s and their share of the
-                     # non-FMA issue rate (peak / 2): the kernel's issue efficiency
-                     "executed_fp64_ops_per_s": st["est_ops_per_step"] * my_steps / (k_ms * 1e-3),
-                     "issue_frac": st["est_ops_per_step"] * my_steps / (k_ms * 1e-3) / (FP64_PEAK_TFLOPS * 1e12 / 2)},
+                     "flops_definition": f"{ops_step:.2f} fp64 ops per Gray step: the {walk} walk's cost model "
+                                         "(adds, muls, fmas it issues per step, each counted as 1 flop); "
+                                         "fp64 issue ceiling without FMA = 0.5 of peak",
+                     "issue_frac": achieved / (FP64_PEAK_TFLOPS / 2),
+                     "gray_step_equiv_tflops": nominal,
+                     "gray_step_equiv_frac": nominal / FP64_PEAK_TFLOPS,
+                     "gray_step_equiv_definition": f"2n = {2 * n} fp64 flops per Gray step (SURVEY 8(d), the "
+                                                   "plain walk's n adds + n muls); above 1 because the walk "
+                                                   "skips the operations structural zeros make redundant"},
         "permanent": perm,
         "kernel_ms_per_rank": rank_kms,
         "densities": also,

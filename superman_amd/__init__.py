@@ -192,28 +192,30 @@ def perman_shard(mat, shard: int, nshards: int, kernel: str = "dense", device_id
     return (out.value, st.as_dict()) if return_stats else out.value
 
 
-def plan_info(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1) -> dict:
+def plan_info(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_id: int = 0) -> dict:
     """The plan the engine runs for `kernel` (and options jit / gpu_num): walk
-    kind, column map, layout, cached walk bits of the segmented walk."""
+    kind, column map, layout, cached walk bits of the segmented walk.  A SkipPer
+    plan may sample its visited fraction on device `device_id`."""
     a, dt, n = _mat(mat)
     lib = _lib.load()
     kind, L, m, cc = C.c_int(), C.c_int(), C.c_int(), C.c_int()
     cm = np.zeros(max(n - 1, 1), np.int32)
-    o = _opts(gpu_num=gpu_num, jit=jit)
+    o = _opts(gpu_num=gpu_num, device_id=device_id, jit=jit)
     _lib.check(lib.sup_plan_info(a.ctypes.data, dt, n, _KERNELS[kernel], C.byref(o), C.byref(kind), cm.ctypes.data,
                                  C.byref(L), C.byref(m), C.byref(cc)), "plan_info")
     return {"kind": WALK_NAMES[kind.value], "colmap": cm[: n - 1].copy(), "L": L.value, "m": m.value,
             "cached": cc.value}
 
 
-def prepare(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1) -> dict:
+def prepare(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_id: int = 0) -> dict:
     """Plan `mat` as perman / perman_shard would and compile the segmented
     walk's specialised kernel now if the plan uses it (hiprtc, no device
-    needed): {"kind": walk name, "compile_ms": hiprtc time (0 when cached)}."""
+    needed): {"kind": walk name, "compile_ms": hiprtc time (0 when cached)}.
+    Planning work that needs a device (SkipPer's sample) runs on `device_id`."""
     a, dt, n = _mat(mat)
     lib = _lib.load()
     kind, ms = C.c_int(), C.c_double(0.0)
-    o = _opts(gpu_num=gpu_num, jit=jit)
+    o = _opts(gpu_num=gpu_num, device_id=device_id, jit=jit)
     _lib.check(lib.sup_prepare(a.ctypes.data, dt, n, _KERNELS[kernel], C.byref(o), C.byref(kind), C.byref(ms)),
                "prepare")
     return {"kind": WALK_NAMES[kind.value], "compile_ms": ms.value}

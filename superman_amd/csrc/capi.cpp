@@ -20,6 +20,21 @@ int check_common(const void* mat, int n, double* out) {
   return SUP_OK;
 }
 
+// The kernels index the walk with 32 bits (T = 1u << m) and pack the walk
+// bits' block counts into two 64-bit words (k < 32), as default_layout
+// assumes; an item of the chunk queue is 2^chunk_log2 wave-chunks (< 2^64).
+int check_walk_opts(const sup_opts& o) {
+  if (o.walk_log2 < 0 || o.walk_log2 > 31) {
+    set_error("walk_log2 = " + std::to_string(o.walk_log2) + " outside [0, 31] (0 = default layout)");
+    return SUP_EINVAL;
+  }
+  if (o.chunk_log2 < 0 || o.chunk_log2 > 62) {
+    set_error("chunk_log2 = " + std::to_string(o.chunk_log2) + " outside [0, 62] (0 = automatic item size)");
+    return SUP_EINVAL;
+  }
+  return SUP_OK;
+}
+
 WalkKind kind_of(sup_kernel k) {
   switch (k) {
     case SUP_KERNEL_SPARYSER: return kWalkSparse;
@@ -91,6 +106,7 @@ int sup_perman(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched
   std::vector<double> A;
   if ((rc = to_double(mat, t, n, A))) return rc;
   Plan P;
+  if ((rc = check_walk_opts(o))) return rc;
   Layout lay = default_layout(n);
   if (o.walk_log2 > 0) {
     const int rest = n - 1 - lay.L;
@@ -121,6 +137,7 @@ int sup_partial(const void* mat, sup_dtype t, int n, sup_kernel kernel, uint64_t
   sup_opts o;
   if (o_in) o = *o_in;
   else sup_opts_init(&o);
+  if ((rc = check_walk_opts(o))) return rc;
   // Largest layout whose wave-chunk (2^(L+m) Gray indices) divides both ends.
   Layout lay = default_layout(n);
   const int nb = n - 1;

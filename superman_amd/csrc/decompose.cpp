@@ -333,6 +333,15 @@ int sup_decompose(const void* mat, sup_dtype t, int n, const sup_reduce_opts* r_
   Decomposer d;
   if (r_in) d.r = *r_in;
   else sup_reduce_opts_init(&d.r);
+  // d34 splits a row of degree 3 or 4 (main.cpp:1007 hard-codes minDeg < 5), and
+  // needs a zero column and two surviving merges (order >= 5): larger max_deg
+  // would split a degree-5+ row on its first four nonzeros, a smaller min_n
+  // would recurse into n = 0 leaves
+  if (d.r.max_deg < 1 || d.r.max_deg > 5 || d.r.min_n < 4) {
+    set_error("sup_decompose: need 1 <= max_deg <= 5 and min_n >= 4 (got max_deg " + std::to_string(d.r.max_deg) +
+              ", min_n " + std::to_string(d.r.min_n) + ")");
+    return SUP_EINVAL;
+  }
   d.fn = fn;
   d.user = user;
   Mat m;

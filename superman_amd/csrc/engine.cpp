@@ -778,11 +778,13 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     // single device, or a static contiguous split (-p5)
     std::vector<RangeResult> rr(G);
     std::vector<int> rcs(G, SUP_OK);
+    std::vector<std::string> errs(G);  // g_err is thread_local: carry worker messages back
     auto work = [&](int g) {
       const uint64_t a = c0 + total * (uint64_t)g / (uint64_t)G;
       const uint64_t b = c0 + total * (uint64_t)(g + 1) / (uint64_t)G;
       auto t0 = std::chrono::steady_clock::now();
       rcs[g] = run_range(devs[g], P, a, b, want_visited, rr[g]);
+      if (rcs[g]) errs[g] = last_error();
       if (o.verbose) {
         double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         std::printf("kernel%d in %f\n", devs[g], s);
@@ -796,7 +798,10 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
       for (auto& t : th) t.join();
     }
     for (int g = 0; g < G; ++g)
-      if (rcs[g]) return rcs[g];
+      if (rcs[g]) {
+        set_error(errs[g]);
+        return rcs[g];
+      }
     out.dev_partials.resize(G);
     for (int g = 0; g < G; ++g) {
       out.dev_partials[g] = rr[g].partial;
@@ -836,6 +841,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   std::vector<uint64_t> dev_vis(G + 1, 0);
   std::vector<int> dev_grid(G + 1, 0);
   std::vector<int> rcs(G + 1, SUP_OK);
+  std::vector<std::string> errs(G + 1);  // worker-thread messages (g_err is thread_local)
   std::vector<double> dev_sum(G, 0.0);
   std::atomic<uint64_t> next{0};
   std::atomic<int> cpu_items{0};
@@ -852,6 +858,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
       int e = run_range(devs[g], P, a, b, want_visited, r);
       if (e) {
         rcs[g] = e;
+        errs[g] = last_error();
         failed.store(true);
         return;
       }
@@ -889,7 +896,10 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   if (o.cpu_worker) th.emplace_back(cpu_worker);
   for (auto& t : th) t.join();
   for (int g = 0; g <= G; ++g)
-    if (rcs[g]) return rcs[g];
+    if (rcs[g]) {
+      set_error(errs[g]);
+      return rcs[g];
+    }
   out.devices = G;
   out.cpu_items = cpu_items.load();
   for (int g = 0; g <= G; ++g) {

@@ -90,11 +90,11 @@ inline int copies(uint32_t sig, int cc) { return 1 << __builtin_popcount(sig & (
 // re-form anything; class c < b flips on 2^-(c+1) of the pair steps, the
 // shared class on ~2^-b.
 struct ClassWeights {
-  uint64_t w[64];
+  uint64_t w[256];
   ClassWeights(int b, int cc) {
-    for (uint32_t s = 0; s < 64; ++s) {
+    for (uint32_t s = 0; s < 256; ++s) {
       uint64_t v = 0;
-      for (int c = cc; c <= b && c < 6; ++c)
+      for (int c = cc; c <= b && c < 8; ++c)
         if ((s >> c) & 1u) v += c < b ? (1ull << (b - 1 - c)) : 1ull;
       w[s] = v * (uint64_t)copies(s, cc);
     }
@@ -121,7 +121,7 @@ ProdTree make_tree(const std::vector<int>& rows, const std::vector<uint32_t>& rs
     uint64_t bw = UINT64_MAX;
     for (size_t i = 0; i < id.size(); ++i)
       for (size_t j = i + 1; j < id.size(); ++j) {
-        const uint64_t w = W.w[(sg[i] | sg[j]) & 63u];
+        const uint64_t w = W.w[(sg[i] | sg[j]) & 255u];
         if (w < bw) bw = w, bi = i, bj = j;
       }
     const uint32_t ns = sg[bi] | sg[bj];
@@ -154,7 +154,7 @@ struct SegRows {
 };
 
 void seg_rows_finish(SegRows& R) {
-  R.b = std::min(R.m - 1, 5);  // seg_static_bits
+  R.b = seg_static_bits(R.m);
   R.rsig.assign(R.n, 0u);
   std::vector<char> dyn(R.n, 0);
   for (int k = 1; k < R.m; ++k)
@@ -260,7 +260,12 @@ SegRows seg_rows_of(const double* A, int n, const std::vector<int>& walk) {
 
 }  // namespace
 
-int seg_static_bits(int m) { return std::min(m - 1, 5); }
+// SUP_JIT_B (experiments): specialised pair bits, 3..7
+int seg_static_bits(int m) {
+  int b = 5;
+  if (const char* e = std::getenv("SUP_JIT_B")) b = std::max(3, std::min(7, std::atoi(e)));
+  return std::min(m - 1, b);
+}
 
 double seg_walk_cost(const Plan& P) { return P.seg_ops; }
 

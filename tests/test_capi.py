@@ -57,6 +57,20 @@ def test_error_codes(sup):
         sup.perman(np.ones((3, 3)), algo=9)
 
 
+def test_walk_option_bounds(sup):
+    # the kernels index the walk in 32 bits and pack walk-bit data for k < 32:
+    # walk_log2 > 31 and chunk_log2 >= 63 are refused before any planning or
+    # device work (so the check holds on a CPU-only host too)
+    a = np.ones((44, 44))
+    for kw in ({"walk_log2": 32}, {"walk_log2": 40}, {"walk_log2": -1}, {"chunk_log2": 63}, {"chunk_log2": -2}):
+        with pytest.raises(sup.SupError) as e:
+            sup.perman(a, **kw)
+        assert e.value.code == -1 and ("walk_log2" in str(e.value) or "chunk_log2" in str(e.value)), kw
+    with pytest.raises(sup.SupError) as e:
+        sup.partial(a, 0, 1 << 20, walk_log2=32)
+    assert e.value.code == -1
+
+
 def test_partial_range_validation(sup):
     if sup.device_count() > 0:
         pytest.skip("GPU present: covered by the gpu tests")

@@ -150,3 +150,25 @@ def test_cli_compression(sup):
     r = subprocess.run([exe, "-f", f, "-c", "-o", "-u", "4", "-t", "4"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and float(r.stdout.splitlines()[1].split()[1]) == pytest.approx(56892084785.0,
                                                                                             rel=1e-12)
+
+
+def test_reduction_option_bounds(sup, orc):
+    # d34 splits rows of degree 3 or 4 only (main.cpp:1007 hard-codes minDeg < 5):
+    # max_deg > 5 would split a degree-5+ row on its first four nonzeros, and
+    # min_n < 4 recurses into n = 0 leaves.  Both are refused up front.
+    rng = np.random.default_rng(11)
+    a = (rng.random((8, 8)) < 0.8) * rng.integers(1, 6, (8, 8))
+    a[np.arange(8), rng.permutation(8)] = 1
+    a = a.astype(np.int32)
+    for kw in ({"max_deg": 6}, {"max_deg": 7}, {"max_deg": 0}, {"min_n": 3}, {"min_n": 0}):
+        with pytest.raises(sup.SupError) as e:
+            sup.decompose(a, lambda m: float(orc.exact_perman(m.astype(np.int64))), compress=True,
+                          **{"min_n": 4, "max_deg": 5, **kw})
+        assert e.value.code == -1 and ("max_deg" in str(e.value) or "min_n" in str(e.value))
+    with pytest.raises(sup.SupError):
+        sup.perman_reduced(a, cpu=True, compress=True, min_n=2)
+    # the widest accepted options still give the exact permanent
+    want = float(orc.exact_perman(a.astype(np.int64)))
+    got, _ = sup.decompose(a, lambda m: float(orc.exact_perman(m.astype(np.int64))), compress=True, min_n=4,
+                           max_deg=5)
+    assert got == want
