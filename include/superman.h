@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SUP_ABI_VERSION 2
+#define SUP_ABI_VERSION 3
 
 /* ---- error codes ------------------------------------------------------ */
 #define SUP_OK            0
@@ -161,11 +161,14 @@ int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int
 /* The plan sup_perman would run with options `o` (NULL = defaults; o->jit and
  * o->gpu_num matter): walk kind (0 dense, 1 prefix/SpaRyser, 2 SkipPer,
  * 3 segmented), engine-bit -> column map (n-1 entries), lane and walk bits,
- * and (segmented walk) the walk bits held in every state (*cached_bits, 0-2;
- * any pointer may be NULL).  For the test harness's bit-exact mirror of the
- * enumeration. */
+ * and (segmented walk) the walk bits held in every state (*cached_bits, 0-2)
+ * and the pair bits with a specialised step (*pair_bits, 3-8; the walk loop is
+ * unrolled by 2^pair_bits pair steps); *est_ops_per_step = the walk's cost
+ * model (sup_stats.est_ops_per_step); any pointer may be NULL.  For the test
+ * harness's bit-exact mirror of the enumeration. */
 int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o, int* walk_kind,
-                  int* colmap, int* lane_bits, int* walk_bits, int* cached_bits);
+                  int* colmap, int* lane_bits, int* walk_bits, int* cached_bits, int* pair_bits,
+                  double* est_ops_per_step);
 
 /* Build the plan sup_perman would run and, if it is the segmented walk,
  * compile its kernel now (hiprtc; no device needed) into the in-memory and

@@ -32,8 +32,8 @@ def load() -> C.CDLL:
         lib.orc_ref_sparse_partial.argtypes = [P, I, LL, LL, I]
         lib.orc_ref_skip.argtypes = [P, I, I, C.POINTER(U)]
         lib.orc_ref_skip_partial.argtypes = [P, I, LL, LL, I]
-        lib.orc_engine_range.argtypes = [P, I, I, P, I, I, I, U, U, I, C.POINTER(U)]
-        lib.orc_engine_perman.argtypes = [P, I, I, P, I, I]
+        lib.orc_engine_range.argtypes = [P, I, I, P, I, I, I, I, U, U, I, C.POINTER(U)]
+        lib.orc_engine_perman.argtypes = [P, I, I, P, I, I, I]
         lib.orc_nw_start.argtypes = [P, I, P, P]
         lib.orc_exact_mod.argtypes = [P, I, U, I]
         lib.orc_exact_mod.restype = U
@@ -113,25 +113,27 @@ def _colmap(colmap):
 
 
 def engine_range(a, kind, c0: int, c1: int, L: int, m: int, colmap=None, threads: int = 8,
-                 cached: int = 0) -> tuple[float, int]:
+                 cached: int = 0, pair_bits: int = 0) -> tuple[float, int]:
     """Engine-schedule mirror over wave-chunks [c0, c1): (partial, visited).
-    colmap: engine bit -> matrix column (None = identity); cached: the
-    segmented walk's cached walk bits (plan_info()["cached"])."""
+    colmap: engine bit -> matrix column (None = identity); cached, pair_bits:
+    the segmented walk's cached walk bits and specialised pair bits
+    (plan_info()["cached"], ["pair_bits"]; pair_bits 0 = the default 5)."""
     a = _d(a)
     v = C.c_ulonglong(0)
     keep, ptr = _colmap(colmap)
-    r = load().orc_engine_range(a.ctypes.data, a.shape[0], KINDS[kind], ptr, int(cached), L, m, c0, c1, threads,
-                                C.byref(v))
+    r = load().orc_engine_range(a.ctypes.data, a.shape[0], KINDS[kind], ptr, int(cached), int(pair_bits), L, m, c0,
+                                c1, threads, C.byref(v))
     return r, v.value
 
 
-def engine_perman(a, kind="dense", colmap=None, threads: int = 8, cached: int = 0) -> float:
+def engine_perman(a, kind="dense", colmap=None, threads: int = 8, cached: int = 0, pair_bits: int = 0) -> float:
     """Full permanent enumerated exactly as the gfx950 kernels do (bit-exact
     mirror), for walk `kind`, engine column map `colmap` and (segmented walk)
-    `cached` walk bits."""
+    `cached` walk bits and `pair_bits` specialised pair bits."""
     a = _d(a)
     keep, ptr = _colmap(colmap)
-    return load().orc_engine_perman(a.ctypes.data, a.shape[0], KINDS[kind], ptr, int(cached), threads)
+    return load().orc_engine_perman(a.ctypes.data, a.shape[0], KINDS[kind], ptr, int(cached), int(pair_bits),
+                                    threads)
 
 
 def engine_perman_as(sup_module, a, kernel="dense", threads: int = 8, jit: int = 0) -> float:
@@ -141,11 +143,12 @@ def engine_perman_as(sup_module, a, kernel="dense", threads: int = 8, jit: int =
     n = _d(a).shape[0]
     L, m, _ = engine_layout(n)
     if (info["L"], info["m"]) == (L, m):
-        return engine_perman(a, info["kind"], info["colmap"], threads, info.get("cached", 0))
+        return engine_perman(a, info["kind"], info["colmap"], threads, info.get("cached", 0),
+                             info.get("pair_bits", 0))
     # the plan's own layout (the segmented walk lengthens its wave-chunks)
     h = n - 1 - info["L"] - info["m"]
     s, _ = engine_range(a, info["kind"], 0, 1 << h, info["L"], info["m"], info["colmap"], threads,
-                        info.get("cached", 0))
+                        info.get("cached", 0), info.get("pair_bits", 0))
     return (4 * (n & 1) - 2) * s
 
 

@@ -410,7 +410,8 @@ void orc_engine_layout(int n, int* L, int* m, int* h) {
   *h = rest - mm;
 }
 
-static void engine_plan(const double* a, int n, int kind, const int* colmap, int L, int m, int cc, eplan* P) {
+static void engine_plan(const double* a, int n, int kind, const int* colmap, int L, int m, int cc, int segb,
+                        eplan* P) {
   memset(P, 0, sizeof(*P));
   P->cc = cc;
   P->n = n;
@@ -500,10 +501,12 @@ static void engine_plan(const double* a, int n, int kind, const int* colmap, int
         if (P->col[2 * (L + k)][j] != 0.0 && !got[j]) got[j] = 1, ++c;
       if (c > P->sub[P->nsub]) P->sub[++P->nsub] = c;
     }
-    /* pair steps flip walk bits k >= 1; bits k <= segb = min(m-1, 5) get
-     * their own step (touched rows), bits > segb share one step over the
-     * union of their rows (jit.cpp) */
-    P->segb = m - 1 < 5 ? m - 1 : 5;
+    /* pair steps flip walk bits k >= 1; bits k <= segb (the plan's choice,
+     * sup_plan_info pair_bits; 0 = the default min(m-1, 5)) get their own
+     * step (touched rows), bits > segb share one step over the union of
+     * their rows (jit.cpp) */
+    P->segb = segb > 0 ? segb : 5;
+    if (P->segb > m - 1) P->segb = m - 1;
     for (int k = P->segb + 1; k < m; ++k)
       for (int j = 0; j < n; ++j)
         if (P->col[2 * (L + k)][j] != 0.0) P->dyn[j] = 1;
@@ -647,27 +650,57 @@ static void e_seg_trees(const eplan* P, etree* outer, etree* inner) {
   e_tree_build(inner, rsig, 0, P->sub[P->nsub], P->len0, P->segb, P->cc);
 }
 
-/* one pair step flipping walk bit k >= 1 in one cached state: its rows (x,
- * and y on segment 0), the outer tree, and segment 0's trees over x and y with
- * D = top_x - top_y */
-static void e_seg_step(const eplan* P, const etree* outer, const etree* inner, double* x, double* y, etv* vo,
-                       etv* vx, etv* vy, double* D, int k, int neg) {
+/* Row copies of the segmented walk: only x0 (walk bits 0..cc clear) is
+ * walked; the value of row r in cached state S is x0_r + cx_r(S & rs_r)
+ * (x0_r when S & rs_r = 0) and its walk-bit-0 twin x0_r + cy_r(S & rs_r),
+ * rs_r = the cached walk bits 1..cc touching row r (bit k-1 for walk bit k),
+ * cx_r(S) = a_k(r) (+ cx_r(S minus its lowest bit)) for the lowest set bit of
+ * S (walk bit k), cy_r(S) = a_0(r) (+ cx_r(S) when S != 0), a_k = the +
+ * column of walk bit k (jit.cpp seg_cx / seg_cy). */
+static double e_cx(const eplan* P, int r, unsigned S) {
+  unsigned low = S & (0u - S), rest = S ^ low;
+  double a = P->col[2 * (P->L + __builtin_ctz(low) + 1)][r];
+  return rest ? e_cx(P, r, rest) + a : a;
+}
+static unsigned e_rs(const eplan* P, int r) {
+  unsigned s = 0;
+  for (int k = 1; k <= P->cc && k < P->m; ++k)
+    if (P->col[2 * (P->L + k)][r] != 0.0) s |= 1u << (k - 1);
+  return s;
+}
+/* every state's copies of row r from x0 */
+static void e_derive(const eplan* P, const double* x0, double xs[][ORC_MAXN], double ys[][ORC_MAXN], int r) {
+  unsigned rs = e_rs(P, r);
+  for (int S = 0; S < (1 << P->cc); ++S) {
+    unsigned s = (unsigned)S & rs;
+    xs[S][r] = s ? x0[r] + e_cx(P, r, s) : x0[r];
+    if (r < P->len0) ys[S][r] = x0[r] + (s ? P->col[2 * P->L][r] + e_cx(P, r, s) : P->col[2 * P->L][r]);
+  }
+}
+
+/* one pair step flipping walk bit k >= 1: its rows of x0 (and their copies in
+ * every cached state), then in every state the outer tree and segment 0's
+ * trees over x and y with D = top_x - top_y */
+static void e_seg_step(const eplan* P, const etree* outer, const etree* inner, double* x0, double xs[][ORC_MAXN],
+                       double ys[][ORC_MAXN], etv* vo, etv* vx, etv* vy, double* D, int k, int neg) {
   const double* c = P->col[2 * (P->L + k) + neg];
   int any = 0;
   int cl = k <= P->segb ? k - 1 : P->segb;
   if (cl < P->cc) return; /* cached walk bit: every state already held */
   for (int j = 0; j < P->n; ++j)
     if (k <= P->segb ? c[j] != 0.0 : P->dyn[j]) {
-      x[j] += c[j];
-      if (j < P->len0) y[j] += c[j];
+      x0[j] += c[j];
+      e_derive(P, x0, xs, ys, j);
       any = 1;
     }
   if (!any) return;
-  e_tree_update(outer, x, vo, cl);
-  if ((e_root_sig(inner) >> cl) & 1u) {
-    e_tree_update(inner, x, vx, cl);
-    e_tree_update(inner, y, vy, cl);
-    *D = e_tree_top(inner, x, vx) - e_tree_top(inner, y, vy);
+  for (int S = 0; S < (1 << P->cc); ++S) {
+    e_tree_update(outer, xs[S], &vo[S], cl);
+    if ((e_root_sig(inner) >> cl) & 1u) {
+      e_tree_update(inner, xs[S], &vx[S], cl);
+      e_tree_update(inner, ys[S], &vy[S], cl);
+      D[S] = e_tree_top(inner, xs[S], &vx[S]) - e_tree_top(inner, ys[S], &vy[S]);
+    }
   }
 }
 
@@ -696,28 +729,15 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
       double x[ORC_MAXN], U[ORC_MAXN / 8 + 2], acc;
       e_start(P, ga, l, x);
       if (P->kind == 3) {
-        /* cached walk bits 1..cc: one full state per assignment S of them;
-         * state S = state S^low + the + column of walk bit ctz(low)+1 on the
-         * rows it touches (low = lowest set bit of S) */
-        static __thread etv vo[4], vx[4], vy[4];
+        /* cached walk bits 1..cc: one full state per assignment S of them,
+         * its rows derived from x0 (e_derive) */
+        static __thread etv vo[8], vx[8], vy[8];
         static __thread etree outer, inner;
-        static __thread double xs[4][ORC_MAXN], ys[4][ORC_MAXN];
-        double D[4];
+        static __thread double xs[8][ORC_MAXN], ys[8][ORC_MAXN];
+        double D[8];
         int NS = 1 << P->cc;
         e_seg_trees(P, &outer, &inner);
-        memcpy(xs[0], x, sizeof(double) * n);
-        for (int r = 0; r < P->len0; ++r) ys[0][r] = xs[0][r] + P->col[2 * L][r];
-        for (int S = 1; S < NS; ++S) {
-          int low = S & -S, k = __builtin_ctz(low) + 1;
-          const double* cp = P->col[2 * (L + k)];
-          memcpy(xs[S], xs[S ^ low], sizeof(double) * n);
-          memcpy(ys[S], ys[S ^ low], sizeof(double) * P->len0);
-          for (int r = 0; r < n; ++r)
-            if (cp[r] != 0.0) {
-              xs[S][r] = xs[S ^ low][r] + cp[r];
-              if (r < P->len0) ys[S][r] = ys[S ^ low][r] + cp[r];
-            }
-        }
+        for (int r = 0; r < n; ++r) e_derive(P, x, xs, ys, r);
         for (int S = 0; S < NS; ++S) {
           e_tree_init(&outer, xs[S], &vo[S]);
           e_tree_init(&inner, xs[S], &vx[S]);
@@ -731,8 +751,7 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
         for (unsigned j = 1; j < T / 2; ++j) {
           unsigned pb = __builtin_ctz(j), neg = (j >> (pb + 1)) & 1u;
           int S = 0;
-          for (int S2 = 0; S2 < NS; ++S2)
-            e_seg_step(P, &outer, &inner, xs[S2], ys[S2], &vo[S2], &vx[S2], &vy[S2], &D[S2], (int)pb + 1, (int)neg);
+          e_seg_step(P, &outer, &inner, x, xs, ys, vo, vx, vy, D, (int)pb + 1, (int)neg);
           for (int i = 0; i < P->cc; ++i) S |= (int)(((j >> i) ^ (j >> (i + 1))) & 1u) << i;
           acc = fma((j & 1u) ? -D[S] : D[S], e_tree_top(&outer, xs[S], &vo[S]), acc);
           if ((j & ((1u << P->segb) - 1u)) == 0u) tot += acc, acc = 0.0;
@@ -827,11 +846,12 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
  * kind: 0 dense, 1 SpaRyser (prefix blocks), 2 SkipPer, 3 segmented walk
  * (jit.cpp's generated kernel).  colmap: engine bit e
  * -> matrix column (n-1 entries; NULL = identity).  cc (kind 3): walk bits
- * 1..cc held in every state (the engine plan's choice, sup_plan_info). */
-double orc_engine_range(const double* a, int n, int kind, const int* colmap, int cc, int L, int m,
+ * 1..cc held in every state and segb specialised pair bits (the engine
+ * plan's choices, sup_plan_info; segb 0 = default). */
+double orc_engine_range(const double* a, int n, int kind, const int* colmap, int cc, int segb, int L, int m,
                         unsigned long long c0, unsigned long long c1, int threads, unsigned long long* visited) {
   eplan* P = (eplan*)malloc(sizeof(eplan));
-  engine_plan(a, n, kind, colmap, L, m, cc, P);
+  engine_plan(a, n, kind, colmap, L, m, cc, segb, P);
   unsigned long long count = c1 > c0 ? c1 - c0 : 0;
   if (count == 0) {
     free(P);
@@ -865,10 +885,10 @@ double orc_engine_range(const double* a, int n, int kind, const int* colmap, int
 }
 
 /* Full permanent with the engine's default layout and the given column map. */
-double orc_engine_perman(const double* a, int n, int kind, const int* colmap, int cc, int threads) {
+double orc_engine_perman(const double* a, int n, int kind, const int* colmap, int cc, int segb, int threads) {
   int L, m, h;
   orc_engine_layout(n, &L, &m, &h);
-  double s = orc_engine_range(a, n, kind, colmap, cc, L, m, 0, 1ULL << h, threads, 0);
+  double s = orc_engine_range(a, n, kind, colmap, cc, segb, L, m, 0, 1ULL << h, threads, 0);
   return (4 * (n & 1) - 2) * s;
 }
 

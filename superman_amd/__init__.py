@@ -194,17 +194,19 @@ def perman_shard(mat, shard: int, nshards: int, kernel: str = "dense", device_id
 
 def plan_info(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_id: int = 0) -> dict:
     """The plan the engine runs for `kernel` (and options jit / gpu_num): walk
-    kind, column map, layout, cached walk bits of the segmented walk.  A SkipPer
+    kind, column map, layout, cost model (fp64 ops per Gray step), cached walk
+    bits and specialised pair bits of the segmented walk.  A SkipPer
     plan may sample its visited fraction on device `device_id`."""
     a, dt, n = _mat(mat)
     lib = _lib.load()
-    kind, L, m, cc = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    kind, L, m, cc, pb = C.c_int(), C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    ops = C.c_double(0.0)
     cm = np.zeros(max(n - 1, 1), np.int32)
     o = _opts(gpu_num=gpu_num, device_id=device_id, jit=jit)
     _lib.check(lib.sup_plan_info(a.ctypes.data, dt, n, _KERNELS[kernel], C.byref(o), C.byref(kind), cm.ctypes.data,
-                                 C.byref(L), C.byref(m), C.byref(cc)), "plan_info")
+                                 C.byref(L), C.byref(m), C.byref(cc), C.byref(pb), C.byref(ops)), "plan_info")
     return {"kind": WALK_NAMES[kind.value], "colmap": cm[: n - 1].copy(), "L": L.value, "m": m.value,
-            "cached": cc.value}
+            "cached": cc.value, "pair_bits": pb.value, "est_ops_per_step": ops.value}
 
 
 def prepare(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_id: int = 0) -> dict:

@@ -126,7 +126,7 @@ def load() -> C.CDLL:
             build()
         lib = C.CDLL(LIB_PATH)
         _declare(lib)
-        if lib.sup_abi_version() != 2:
+        if lib.sup_abi_version() != 3:
             raise RuntimeError("libsuperman_hip.so ABI version mismatch")
         _lib = lib
         return lib
@@ -146,7 +146,7 @@ def _declare(lib: C.CDLL) -> None:
     lib.sup_perman_exact.argtypes = [P, I, I, C.POINTER(SupOpts), I, C.c_char_p, C.c_size_t, C.POINTER(SupStats)]
     lib.sup_perman_shard.argtypes = [P, I, I, I, I, I, C.POINTER(SupOpts), C.POINTER(D), C.POINTER(SupStats)]
     lib.sup_plan_info.argtypes = [P, I, I, I, C.POINTER(SupOpts), C.POINTER(I), P, C.POINTER(I), C.POINTER(I),
-                                  C.POINTER(I)]
+                                  C.POINTER(I), C.POINTER(I), C.POINTER(D)]
     lib.sup_prepare.argtypes = [P, I, I, I, C.POINTER(SupOpts), C.POINTER(I), C.POINTER(C.c_double)]
     lib.sup_nw_start.argtypes = [P, I, I, C.POINTER(D), C.POINTER(D)]
     lib.sup_read_matrix.argtypes = [C.c_char_p, I, C.POINTER(P), C.POINTER(I), C.POINTER(I), C.POINTER(I)]

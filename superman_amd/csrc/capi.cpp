@@ -287,7 +287,7 @@ int sup_perman_reduced_exact(const void* mat, sup_dtype t, int n, const sup_opts
 }
 
 int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o_in, int* walk_kind,
-                  int* colmap, int* L, int* m, int* cached_bits) {
+                  int* colmap, int* L, int* m, int* cached_bits, int* pair_bits, double* est_ops_per_step) {
   std::vector<double> A;
   int rc = to_double(mat, t, n, A);
   if (rc) return rc;
@@ -298,6 +298,8 @@ int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const 
   if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num, o.device_id))) return rc;
   if (walk_kind) *walk_kind = P.lds ? 4 : (int)P.kind;
   if (cached_bits) *cached_bits = P.kind == kWalkSeg ? P.seg_cc : 0;
+  if (pair_bits) *pair_bits = P.kind == kWalkSeg ? P.seg_b : 0;
+  if (est_ops_per_step) *est_ops_per_step = walk_cost(P);
   if (colmap)
     for (int e = 0; e < n - 1; ++e) colmap[e] = P.colmap[e];
   if (L) *L = P.lay.L;

@@ -174,7 +174,10 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
     // walk bits get the greedy prefix order (greedy_walk_order; the segmented
     // walk: seg_walk_order), lane bits the next L columns of that order, high
     // bits the rest in matrix order.
-    std::vector<int> order = kind == kWalkSeg ? seg_walk_order(A, n, m, m + L) : greedy_walk_order(A, n, m + L);
+    int segb = 0;
+    std::vector<int> order =
+        kind == kWalkSeg ? seg_walk_order(A, n, m, m + L, &segb) : greedy_walk_order(A, n, m + L);
+    P.seg_b = segb;
     std::vector<char> used(n, 0);
     for (int k = 0; k < m; ++k) P.colmap[L + k] = order[k], used[order[k]] = 1;
     for (int e = 0; e < L; ++e) P.colmap[e] = order[m + e], used[order[m + e]] = 1;
@@ -287,7 +290,8 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
   }
   // ndev only feeds auto mode's compile-or-not decision
   const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0};
-  if (std::getenv("SUP_JIT_CC")) return plan_for_uncached(A, n, kernel, lay, P, jit, ndev, dev);  // experiments
+  if (std::getenv("SUP_JIT_CC") || std::getenv("SUP_JIT_B"))  // experiment knobs: never cached
+    return plan_for_uncached(A, n, kernel, lay, P, jit, ndev, dev);
   {
     std::lock_guard<std::mutex> g(g_plan_mu);
     auto it = g_plans.find(key);

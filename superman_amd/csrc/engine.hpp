@@ -49,11 +49,18 @@ struct ProdTree {
   int tail_lo = 0, tail_hi = 0;
   std::vector<int> a, b;
   std::vector<uint32_t> sig;
+  // per item (segmented walk's row copies, jit.cpp seg_fit): bit 0 = the
+  // copies over x are kept live, bit 1 = the copies over y (inner tree) are;
+  // otherwise they are formed on demand when the parent node is re-formed
+  std::vector<uint8_t> item_live;
   int items() const { return (int)item_row.size(); }
   int K() const { return (int)a.size(); }
   int root() const { return K() ? items() + K() - 1 : (items() ? 0 : -1); }
   uint32_t root_sig() const { return K() ? sig.back() : (items() ? item_sig[0] : 0u); }
 };
+
+// Cached walk bits (Plan::seg_cc) at most.
+constexpr int kMaxCachedBits = 3;
 
 struct Plan {
   int n = 0;
@@ -85,7 +92,10 @@ struct Plan {
   double seg_ops = 0.0;            // fp64 VALU ops per Gray step of the generated kernel
   int seg_regs = 0;                // values live across steps (doubles), estimate
   std::vector<int> jofs;           // [m] offset (doubles) of walk bit k's + block in jtab
-  std::vector<double> jtab;        // packed touched values: + block, - block (each padded to 8)
+  std::vector<double> jtab;        // packed touched values: + block, - block (each padded to 8); then,
+                                   // from seg_cbase, the row-copy constants (jit.cpp Gen::tail)
+  size_t seg_cbase = 0;
+  int seg_kp = 4;                  // SGPR pieces (8 doubles) pinned per step region of the generated code
   std::string jit_src;             // generated HIP source of the specialised kernel
   uint64_t jit_key = 0;            // hash of jit_src + compile options
   uint64_t uid = 0;                // plan-cache identity (0: uncached); a device that holds
@@ -103,7 +113,8 @@ std::vector<int> greedy_walk_order(const double* A, int n, int count);
 // ---- segmented walk (jit.cpp) ----
 // Walk-column order for the segmented walk: greedy starts from every column,
 // then pairwise-swap descent on seg_cost (first `count` columns returned).
-std::vector<int> seg_walk_order(const double* A, int n, int m, int count);
+// *b_out = the specialised pair bits the order was chosen for (seg_b).
+std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b_out);
 // Engine row order of the segmented walk for walk columns `walk`: rows in
 // first-touch order, segment 0 (the rows of walk[0]) internally ordered by
 // first touch among walk[1..], its rows no other walk column touches last.
@@ -111,9 +122,15 @@ std::vector<int> seg_row_order(const double* A, int n, const std::vector<int>& w
 // Fill the segment structure, packed table and generated source of a plan
 // whose rows are already in first-touch order (make_plan, kind kWalkSeg).
 int build_seg(Plan& P);
-// Walk bits with a specialised step: min(m, 5) (the walk loop is unrolled by
-// 2^b Gray steps; bits >= b share one straight-line step).
+// Default specialised pair bits, min(m - 1, 5) (the walk loop is unrolled by
+// 2^b pair steps; walk bits > b share one straight-line step).  Plans choose
+// b in 5..8 by the op count (seg_walk_order / build_seg).
 int seg_static_bits(int m);
+// Row-copy constants of the segmented walk (x^S_r = x^0_r + seg_cx(P, r, S),
+// y^S_r = x^0_r + seg_cy(P, r, S); S = cached state masked to the walk bits
+// 1..seg_cc that touch row r, nonzero for seg_cx).
+double seg_cx(const Plan& P, int r, uint32_t S);
+double seg_cy(const Plan& P, int r, uint32_t S);
 // fp64 VALU ops per Gray step and lane of the segmented walk.
 double seg_walk_cost(const Plan& P);
 // Resolve (compile or fetch from cache) the specialised kernel of P for the

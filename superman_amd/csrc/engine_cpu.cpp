@@ -129,34 +129,55 @@ inline double tree_top(const ProdTree& t, const double* a, const TreeVal& v) {
 // Pair step j flips walk bit k = ctz(j) + 1; walk bits k <= seg_b use their
 // own touched rows, bits > seg_b one shared step over dyn_rows (the generated
 // kernel's straight-line step for those bits).
-// Cached walk bits 1..seg_cc: the kernel holds every value that depends on them
-// once per state of those bits and their steps only accumulate.  Restated here
-// as one full lane state per cached state S (copies of rows and nodes that do
-// not depend on a bit are equal in every state, computed from equal operands):
-// state S = state S' (S without its lowest bit, walk bit k) + the + column of
-// walk bit k on the rows it touches, then every non-cached step updates every
-// state the same way, and pair j accumulates with the state of its Gray bits.
-constexpr int kMaxCached = 2;
+// Cached walk bits 1..seg_cc: the kernel holds every node that depends on
+// them once per state of those bits and their steps only accumulate.  Only
+// x^0 (walk bits 0..cc clear) is walked; every row copy is a pure function of
+// it, x^S_r = x^0_r + seg_cx(r, S) (x^0_r when no bit of S touches r) and
+// y^S_r = x^0_r + seg_cy(r, S), whether the kernel keeps it live or forms it
+// on demand.  Restated here as one full lane state per cached state S, its
+// rows re-derived from x^0 whenever x^0_r changes; every non-cached step then
+// re-forms every state's dirty nodes, and pair j accumulates with the state
+// of its Gray bits.
+constexpr int kMaxCached = kMaxCachedBits;
 struct SegLane {
+  double x0[SUP_MAX_N];
   double x[1 << kMaxCached][SUP_MAX_N], y[1 << kMaxCached][SUP_MAX_N], D[1 << kMaxCached];
   TreeVal o[1 << kMaxCached], ix[1 << kMaxCached], iy[1 << kMaxCached];
 };
-
-void seg_init(const Lane& s, SegLane& g, const Plan& P) {
-  const int len0 = P.seg_start[1], NS = 1 << P.seg_cc;
-  std::copy(s.x, s.x + P.n, g.x[0]);
-  for (int r = 0; r < len0; ++r) g.y[0][r] = g.x[0][r] + P.jtab[P.jofs[0] + r];
-  for (int S = 1; S < NS; ++S) {
-    const int low = S & -S, k = __builtin_ctz(low) + 1;
-    std::copy(g.x[S ^ low], g.x[S ^ low] + P.n, g.x[S]);
-    std::copy(g.y[S ^ low], g.y[S ^ low] + len0, g.y[S]);
-    const std::vector<int>& t = P.touched[k];
-    for (size_t i = 0; i < t.size(); ++i) {
-      const double v = P.jtab[P.jofs[k] + i];
-      g.x[S][t[i]] = g.x[S ^ low][t[i]] + v;
-      if (t[i] < len0) g.y[S][t[i]] = g.y[S ^ low][t[i]] + v;
+// Row-copy constants of a plan: cached part of each row's classes and
+// cx[r][S], cy[r][S] (seg_cx / seg_cy) for S within it.
+struct SegConsts {
+  uint32_t rs[SUP_MAX_N];
+  double cx[SUP_MAX_N][1 << kMaxCached], cy[SUP_MAX_N][1 << kMaxCached];
+  explicit SegConsts(const Plan& P) {
+    const uint32_t ccm = (1u << P.seg_cc) - 1u;
+    for (int r = 0; r < P.n; ++r) rs[r] = 0;
+    for (int k = 1; k <= P.seg_cc && k < P.lay.m; ++k)
+      for (int r : P.touched[k]) rs[r] |= 1u << (k - 1);
+    for (int r = 0; r < P.n; ++r) {
+      rs[r] &= ccm;
+      for (uint32_t S = 0; S < (1u << P.seg_cc); ++S) {
+        if (S & ~rs[r]) continue;
+        cx[r][S] = S ? seg_cx(P, r, S) : 0.0;
+        cy[r][S] = r < P.seg_start[1] ? seg_cy(P, r, S) : 0.0;
+      }
     }
   }
+};
+
+inline void seg_derive(SegLane& g, const Plan& P, const SegConsts& K, int r) {
+  const int len0 = P.seg_start[1];
+  for (uint32_t S = 0; S < (1u << P.seg_cc); ++S) {
+    const uint32_t s = S & K.rs[r];
+    g.x[S][r] = s ? g.x0[r] + K.cx[r][s] : g.x0[r];
+    if (r < len0) g.y[S][r] = g.x0[r] + K.cy[r][s];
+  }
+}
+
+void seg_init(const Lane& s, SegLane& g, const Plan& P, const SegConsts& K) {
+  const int NS = 1 << P.seg_cc;
+  std::copy(s.x, s.x + P.n, g.x0);
+  for (int r = 0; r < P.n; ++r) seg_derive(g, P, K, r);
   for (int S = 0; S < NS; ++S) {
     tree_init(P.outer_tree, g.x[S], g.o[S]);
     tree_init(P.inner_tree, g.x[S], g.ix[S]);
@@ -165,34 +186,26 @@ void seg_init(const Lane& s, SegLane& g, const Plan& P) {
   }
 }
 
-void seg_step(SegLane& g, const Plan& P, int k, int neg) {
-  const int len0 = P.seg_start[1], c = k <= P.seg_b ? k - 1 : P.seg_b;
+void seg_step(SegLane& g, const Plan& P, const SegConsts& K, int k, int neg) {
+  const int c = k <= P.seg_b ? k - 1 : P.seg_b;
   if (c < P.seg_cc) return;  // cached walk bit: nothing changes
+  if (k > P.seg_b) {  // shared step: full signed column over dyn_rows (zeros included)
+    if (P.dyn_rows.empty()) return;
+    const double* col = col_of(P, P.lay.L + k, neg);
+    for (int r : P.dyn_rows) g.x0[r] += col[r], seg_derive(g, P, K, r);
+  } else {
+    const std::vector<int>& t = P.touched[k];
+    if (t.empty()) return;
+    const size_t blk = (t.size() + 7) & ~(size_t)7;
+    const double* v = P.jtab.data() + P.jofs[k] + (neg ? blk : 0);
+    for (size_t i = 0; i < t.size(); ++i) g.x0[t[i]] += v[i], seg_derive(g, P, K, t[i]);
+  }
   for (int S = 0; S < (1 << P.seg_cc); ++S) {
-    double* x = g.x[S];
-    double* y = g.y[S];
-    if (k > P.seg_b) {  // shared step: full signed column over dyn_rows (zeros included)
-      if (P.dyn_rows.empty()) return;
-      const double* col = col_of(P, P.lay.L + k, neg);
-      for (int r : P.dyn_rows) {
-        x[r] += col[r];
-        if (r < len0) y[r] += col[r];
-      }
-    } else {
-      const std::vector<int>& t = P.touched[k];
-      if (t.empty()) return;
-      const size_t blk = (t.size() + 7) & ~(size_t)7;
-      const double* v = P.jtab.data() + P.jofs[k] + (neg ? blk : 0);
-      for (size_t i = 0; i < t.size(); ++i) {
-        x[t[i]] += v[i];
-        if (t[i] < len0) y[t[i]] += v[i];
-      }
-    }
-    tree_update(P.outer_tree, x, g.o[S], c);
+    tree_update(P.outer_tree, g.x[S], g.o[S], c);
     if ((P.inner_tree.root_sig() >> c) & 1u) {
-      tree_update(P.inner_tree, x, g.ix[S], c);
-      tree_update(P.inner_tree, y, g.iy[S], c);
-      g.D[S] = tree_top(P.inner_tree, x, g.ix[S]) - tree_top(P.inner_tree, y, g.iy[S]);
+      tree_update(P.inner_tree, g.x[S], g.ix[S], c);
+      tree_update(P.inner_tree, g.y[S], g.iy[S], c);
+      g.D[S] = tree_top(P.inner_tree, g.x[S], g.ix[S]) - tree_top(P.inner_tree, g.y[S], g.iy[S]);
     }
   }
 }
@@ -222,6 +235,7 @@ double chunk_partial(const Plan& P, uint64_t ga) {
       }
       if (!live) return 0.0;
     }
+    const SegConsts K(P);
     for (unsigned l = 0; l < 64; ++l) {
       if (l >= (1u << L)) {
         lane_val[l] = 0.0;
@@ -230,7 +244,7 @@ double chunk_partial(const Plan& P, uint64_t ga) {
       Lane s;
       chunk_start(P, ga, l, s);
       static thread_local SegLane g;
-      seg_init(s, g, P);
+      seg_init(s, g, P, K);
       double acc = g.D[0] * tree_top(P.outer_tree, g.x[0], g.o[0]);
       // two-level lane sum (the kernel's): acc folds into tot after each shared
       // dyn step's pair j = 2^seg_b (q + 1), so no sequential sum runs longer
@@ -239,7 +253,7 @@ double chunk_partial(const Plan& P, uint64_t ga) {
       const uint32_t qmask = (1u << P.seg_b) - 1u;
       for (uint32_t j = 1; j < T / 2; ++j) {  // pair steps: walk bit ctz(j) + 1
         const uint32_t pb = __builtin_ctz(j);
-        seg_step(g, P, (int)pb + 1, (j >> (pb + 1)) & 1u);
+        seg_step(g, P, K, (int)pb + 1, (j >> (pb + 1)) & 1u);
         const int S = seg_state(j, P.seg_cc);
         acc = std::fma((j & 1u) ? -g.D[S] : g.D[S], tree_top(P.outer_tree, g.x[S], g.o[S]), acc);
         if ((j & qmask) == 0u) tot += acc, acc = 0.0;

@@ -61,12 +61,15 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <sstream>
+#include <tuple>
+#include <thread>
 
 #include "engine.hpp"
 
@@ -90,11 +93,11 @@ inline int copies(uint32_t sig, int cc) { return 1 << __builtin_popcount(sig & (
 // re-form anything; class c < b flips on 2^-(c+1) of the pair steps, the
 // shared class on ~2^-b.
 struct ClassWeights {
-  uint64_t w[256];
+  uint64_t w[512];  // classes 0..b, b <= 8
   ClassWeights(int b, int cc) {
-    for (uint32_t s = 0; s < 256; ++s) {
+    for (uint32_t s = 0; s < 512; ++s) {
       uint64_t v = 0;
-      for (int c = cc; c <= b && c < 8; ++c)
+      for (int c = cc; c <= b && c < 9; ++c)
         if ((s >> c) & 1u) v += c < b ? (1ull << (b - 1 - c)) : 1ull;
       w[s] = v * (uint64_t)copies(s, cc);
     }
@@ -121,7 +124,7 @@ ProdTree make_tree(const std::vector<int>& rows, const std::vector<uint32_t>& rs
     uint64_t bw = UINT64_MAX;
     for (size_t i = 0; i < id.size(); ++i)
       for (size_t j = i + 1; j < id.size(); ++j) {
-        const uint64_t w = W.w[(sg[i] | sg[j]) & 255u];
+        const uint64_t w = W.w[(sg[i] | sg[j]) & 511u];
         if (w < bw) bw = w, bi = i, bj = j;
       }
     const uint32_t ns = sg[bi] | sg[bj];
@@ -153,8 +156,8 @@ struct SegRows {
   std::vector<uint32_t> rsig;     // step classes of each row
 };
 
-void seg_rows_finish(SegRows& R) {
-  R.b = seg_static_bits(R.m);
+void seg_rows_finish(SegRows& R, int b) {
+  R.b = b;
   R.rsig.assign(R.n, 0u);
   std::vector<char> dyn(R.n, 0);
   for (int k = 1; k < R.m; ++k)
@@ -174,7 +177,29 @@ struct SegFit {
   ProdTree outer, inner;
 };
 
-// Trees, cost and live values with cc cached classes.
+// Pair-step frequency (x 2^b) of a value re-formed on the step classes `s`:
+// class c < b flips on 2^-(c+1) of the pair steps, the shared class b on
+// ~2^-b; cached classes (c < cc) never re-form anything.
+inline uint64_t freq(uint32_t s, int b, int cc) {
+  uint64_t v = 0;
+  for (int c = cc; c <= b && c < 9; ++c)
+    if ((s >> c) & 1u) v += c < b ? (1ull << (b - 1 - c)) : 1ull;
+  return v;
+}
+
+// Trees, cost, live values and the live/on-demand choice of every row copy
+// with cc cached classes.
+//
+// Row copies.  Only x^0 (the lane state with walk bits 0..cc clear) is walked;
+// every other value of row r is a pure function of it: the copy for cached
+// state S is x^S_r = x^0_r + cx_r[S] (x^0_r itself when no bit of S touches
+// r) and its walk-bit-0 twin y^S_r = x^0_r + cy_r[S] (seg_consts).  A copy is
+// either kept live (re-formed when x^0_r changes) or formed on demand when its
+// parent node is re-formed: the same value either way, so the choice is free
+// of numerical effect.  On demand costs nothing extra when the parent is
+// re-formed exactly as often as the row changes (the tree joins rows of equal
+// step classes first) and frees the register; it is taken whenever it costs
+// no more ops than keeping the copy.
 SegFit seg_fit(const SegRows& R, int cc) {
   SegFit f;
   f.cc = cc;
@@ -184,32 +209,50 @@ SegFit seg_fit(const SegRows& R, int cc) {
   for (int r = 0; r < R.s_end; ++r) irow.push_back(r);
   f.outer = make_tree(orow, R.rsig, R.r_end, R.n, W);
   f.inner = make_tree(irow, R.rsig, R.s_end, R.len0, W);
-  // ops per pair step of class c: the row adds (all copies, y too), the
-  // dirty nodes (all copies; segment 0's over x and over y), D, the fma
-  double c = 0.0, w = 0.5;
-  for (int p = 0; p + 1 < R.m; ++p, w *= 0.5) {
-    const int k = p + 1, cl = step_class(k, R.b);
-    double ops = 1.0;
-    if (cl >= cc) {
-      for (int r : (k <= R.b ? R.touched[k] : R.dyn_rows)) ops += copies(R.rsig[r], cc) * (r < R.len0 ? 2.0 : 1.0);
-      for (int i = 0; i < f.outer.K(); ++i)
-        if ((f.outer.sig[i] >> cl) & 1u) ops += copies(f.outer.sig[i], cc);
-      for (int i = 0; i < f.inner.K(); ++i)
-        if ((f.inner.sig[i] >> cl) & 1u) ops += 2.0 * copies(f.inner.sig[i], cc);
-      if ((f.inner.root_sig() >> cl) & 1u) ops += copies(f.inner.root_sig(), cc);
+  const uint32_t ccm = (1u << cc) - 1u;
+  uint64_t ops = 0;                        // x 2^b per pair step
+  int regs = 6 + R.n;                      // x^0, acc, tot, loop state
+  for (int r = 0; r < R.n; ++r) ops += freq(R.rsig[r], R.b, cc);  // x^0 adds
+  for (int ti = 0; ti < 2; ++ti) {
+    ProdTree& t = ti ? f.inner : f.outer;
+    const int nv = ti ? 2 : 1;             // inner: over x and over y
+    std::vector<int> par(t.items() + t.K(), -1);
+    for (int j = 0; j < t.K(); ++j) par[t.a[j]] = j, par[t.b[j]] = j;
+    for (int i = 0; i < t.K(); ++i) {
+      ops += freq(t.sig[i], R.b, cc) * (uint64_t)(copies(t.sig[i], cc) * nv);
+      const int p = par[t.items() + i];
+      if (p < 0 || t.sig[p] != t.sig[i]) regs += copies(t.sig[i], cc) * nv;
     }
-    c += w * ops;
+    t.item_live.assign(t.items(), 0);
+    for (int j = 0; j < t.items(); ++j) {
+      const int r = t.item_row[j];
+      if (r < 0) continue;
+      const uint32_t rs = R.rsig[r];
+      for (int v = 0; v < nv; ++v) {
+        const int own = copies(rs, cc), ncopy = v == 0 ? own - 1 : own;  // copies other than x^0
+        if (ncopy == 0) continue;
+        const uint64_t live = freq(rs, R.b, cc) * (uint64_t)ncopy;
+        const int p = par[j];
+        bool keep = p < 0;  // a root row stays live (read by every accumulate)
+        uint64_t dem = 0;
+        if (!keep) {
+          const uint32_t ps = t.sig[p];
+          const int pc = copies(ps, cc);
+          dem = freq(ps, R.b, cc) * (uint64_t)(v == 0 ? pc - (1 << __builtin_popcount(ps & ~rs & ccm)) : pc);
+          keep = dem > live;
+        }
+        if (keep) t.item_live[j] |= (uint8_t)(1u << v), ops += live, regs += ncopy;
+        else ops += dem;
+      }
+    }
+    if (ti == 1 && t.root() >= 0) {  // D per copy of the inner root
+      const uint32_t rs = t.root_sig();
+      ops += freq(rs, R.b, cc) * (uint64_t)copies(rs, cc);
+      regs += copies(rs, cc);
+    }
   }
-  f.ops = c / 2.0;
-  // live across steps: rows (x, y on segment 0) with their copies, the nodes
-  // whose parent is not re-formed with them, D, acc and loop state
-  int regs = 6 + copies(f.inner.root_sig(), cc);
-  for (int r = 0; r < R.n; ++r) regs += copies(R.rsig[r], cc) * (r < R.len0 ? 2 : 1);
-  for (const ProdTree* t : {&f.outer, &f.inner})
-    for (int i = 0; i < t->K(); ++i) {
-      const int ps = parent_sig(*t, i);
-      if (ps < 0 || (uint32_t)ps != t->sig[i]) regs += copies(t->sig[i], cc) * (t == &f.inner ? 2 : 1);
-    }
+  // + the accumulate fma per pair step; / 2 pair -> Gray steps
+  f.ops = ((double)ops / (double)(1u << R.b) + 1.0) / 2.0;
   f.regs = regs;
   return f;
 }
@@ -222,8 +265,9 @@ SegFit seg_fit(const SegRows& R, int cc) {
 constexpr int kRegs3 = 90, kRegsMax = 142;
 constexpr double kOcc2Penalty = 1.02;
 
-// Best number of cached classes (0 .. min(2, b-1)) within the register budget.
-SegFit seg_best(const SegRows& R, int cc_max = 2) {
+// Best number of cached classes (0 .. min(kMaxCachedBits, b-1)) within the
+// register budget.
+SegFit seg_best(const SegRows& R, int cc_max = kMaxCachedBits) {
   SegFit best = seg_fit(R, 0);
   double bscore = best.ops * (best.regs <= kRegs3 ? 1.0 : kOcc2Penalty);
   for (int cc = 1; cc <= std::min(cc_max, R.b - 1); ++cc) {
@@ -235,8 +279,9 @@ SegFit seg_best(const SegRows& R, int cc_max = 2) {
   return best;
 }
 
-// SegRows of walk columns `walk` in the engine row order make_plan uses.
-SegRows seg_rows_of(const double* A, int n, const std::vector<int>& walk) {
+// SegRows of walk columns `walk` in the engine row order make_plan uses,
+// with b specialised pair bits.
+SegRows seg_rows_of(const double* A, int n, const std::vector<int>& walk, int b) {
   SegRows R;
   R.n = n, R.m = (int)walk.size();
   const std::vector<int> order = seg_row_order(A, n, walk);
@@ -254,22 +299,52 @@ SegRows seg_rows_of(const double* A, int n, const std::vector<int>& walk) {
   while (R.s_end < R.len0 && any1[R.s_end]) ++R.s_end;
   R.r_end = R.len0;
   while (R.r_end < n && any1[R.r_end]) ++R.r_end;
-  seg_rows_finish(R);
+  seg_rows_finish(R, b);
   return R;
+}
+
+// Score of a fit: ops per Gray step, 2% more when it needs the 2-wave budget.
+double seg_score(const SegFit& f) { return f.ops * (f.regs <= kRegs3 ? 1.0 : kOcc2Penalty); }
+
+// Instruction bytes of the unrolled 2^b-pair block (the loop body), estimated
+// from the op count: 2 * ops per Gray step per pair step, 8 B per fp64 VOP3
+// instruction, +25% for the scalar loads, branches and sched barriers.  The
+// block must stay well inside the 64 KB instruction cache two CUs share.
+constexpr double kMaxBlockBytes = 40.0 * 1024.0;
+double seg_block_bytes(const SegFit& f, int b) { return 1.25 * 8.0 * 2.0 * f.ops * (double)(1u << b); }
+
+// Candidate specialised pair-bit counts for m walk bits: SUP_JIT_B forces one
+// (experiments), else 5..8 (fewer when the walk is shorter).  More pair bits
+// make the shared step of the higher walk bits rarer (it adds the full column
+// to the union of their rows) and let more rows keep a class of their own, at
+// 2x the code per bit (measured on MI355X, profiles/r2/probe_b.log: the n = 40
+// d = 0.5 bench matrix 2.06e12 Gray steps/s at b = 5, 2.14e12 at 6, 2.05e12 at
+// 7, each as its op count predicts; config 5 3.57e13 / 3.95e13 / 5.13e13).
+std::vector<int> seg_b_candidates(int m) {
+  std::vector<int> v;
+  if (const char* e = std::getenv("SUP_JIT_B")) {
+    v.push_back(std::min(m - 1, std::max(3, std::min(8, std::atoi(e)))));
+    return v;
+  }
+  for (int b = 5; b <= 8; ++b) {
+    const int bb = std::min(m - 1, b);
+    if (v.empty() || v.back() != bb) v.push_back(bb);
+  }
+  return v;
 }
 
 }  // namespace
 
-// SUP_JIT_B (experiments): specialised pair bits, 3..7
+// Default specialised pair bits when no choice was made (SUP_JIT_B forces, 3..8)
 int seg_static_bits(int m) {
   int b = 5;
-  if (const char* e = std::getenv("SUP_JIT_B")) b = std::max(3, std::min(7, std::atoi(e)));
+  if (const char* e = std::getenv("SUP_JIT_B")) b = std::max(3, std::min(8, std::atoi(e)));
   return std::min(m - 1, b);
 }
 
 double seg_walk_cost(const Plan& P) { return P.seg_ops; }
 
-std::vector<int> seg_walk_order(const double* A, int n, int m, int count) {
+std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b_out) {
   const int nb = n - 1;
   m = std::min(m, nb);
   count = std::min(std::max(count, m), nb);
@@ -300,39 +375,89 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count) {
   // the exact op count of the generated code (best cached-class count within
   // the register budget); walk bit 0 defines segment 0 (the paired rows) and
   // must touch a row
-  auto cost = [&](const std::vector<int>& o) {
+  auto cost = [&](const std::vector<int>& o, int b) {
     if (nnz[o[0]] == 0) return 1e300;
     if (m < 3) return 0.0;
-    const SegFit f = seg_best(seg_rows_of(A, n, std::vector<int>(o.begin(), o.begin() + m)));
-    return f.ops * (f.regs <= kRegs3 ? 1.0 : kOcc2Penalty);
+    const SegFit f = seg_best(seg_rows_of(A, n, std::vector<int>(o.begin(), o.begin() + m), b));
+    return seg_block_bytes(f, b) > kMaxBlockBytes ? 1e300 : seg_score(f);
   };
-  std::vector<int> best;
-  double bcost = 1e300;
-  for (int f = 0; f < nb && m > 0; ++f) {
-    std::vector<int> o = extend({f}, m);
-    const double c = cost(o);
-    if (c < bcost) bcost = c, best = o;
+  if (m == 0) {
+    if (b_out) *b_out = 0;
+    return extend({}, count);
   }
-  if (m == 0) return extend({}, count);
-  // descent: swap a walk position with another walk position or an unused
-  // column while the cost drops (positions whose weight 2^-(k+1) is visible)
-  const int hot = std::min(m, 12);
-  for (int pass = 0; pass < 8; ++pass) {
-    bool improved = false;
-    for (int a = 0; a < hot; ++a) {
-      for (int c = 0; c < nb; ++c) {
-        if (c == best[a]) continue;
-        std::vector<int> o = best;
-        auto it = std::find(o.begin(), o.end(), c);
-        if (it != o.end()) std::swap(o[a], *it);
-        else o[a] = c;
-        const double v = cost(o);
-        if (v < bcost - 1e-12) bcost = v, best = o, improved = true;
+  // one search per candidate b (the best order differs with b), each on its
+  // own host thread; the cheapest (order, b) wins, ties -> the smaller b
+  const std::vector<int> cands = seg_b_candidates(m);
+  std::vector<std::vector<int>> bests(cands.size());
+  std::vector<double> bcosts(cands.size(), 1e300);
+  auto search = [&](size_t ci) {
+    const int b = cands[ci];
+    std::vector<int> best;
+    double bcost = 1e300;
+    for (int f = 0; f < nb; ++f) {
+      std::vector<int> o = extend({f}, m);
+      const double c = cost(o, b);
+      if (c < bcost || best.empty()) bcost = c, best = o;
+    }
+    // descent: swap a walk position with another walk position or an unused
+    // column while the cost drops (positions whose weight 2^-(k+1) is visible)
+    const int hot = std::getenv("SUP_JIT_HOT") ? std::min(m, std::atoi(std::getenv("SUP_JIT_HOT"))) : std::min(m, 12);
+    for (int pass = 0; pass < 8 && bcost < 1e300; ++pass) {
+      bool improved = false;
+      for (int a = 0; a < hot; ++a) {
+        for (int c = 0; c < nb; ++c) {
+          if (c == best[a]) continue;
+          std::vector<int> o = best;
+          auto it = std::find(o.begin(), o.end(), c);
+          if (it != o.end()) std::swap(o[a], *it);
+          else o[a] = c;
+          const double v = cost(o, b);
+          if (v < bcost - 1e-12) bcost = v, best = o, improved = true;
+        }
+      }
+      if (!improved) break;
+    }
+    if (const char* e = std::getenv("SUP_JIT_ANNEAL")) {  // experiment: simulated annealing on the order
+      const int iters = std::atoi(e);
+      uint64_t rs = 0x9E3779B97F4A7C15ull ^ (uint64_t)b;
+      auto rnd = [&]() { rs ^= rs << 13; rs ^= rs >> 7; rs ^= rs << 17; return rs; };
+      std::vector<int> cur = best;
+      std::vector<char> inw(n, 0);
+      double ccost = bcost;
+      for (int it = 0; it < iters; ++it) {
+        const double T = 0.02 * bcost * (1.0 - (double)it / iters);
+        std::vector<int> o = cur;
+        const int a = (int)(rnd() % m);
+        if (rnd() & 1) {
+          const int c2 = (int)(rnd() % m);
+          std::swap(o[a], o[c2]);
+        } else {
+          std::fill(inw.begin(), inw.end(), 0);
+          for (int k = 0; k < m; ++k) inw[o[k]] = 1;
+          int c = (int)(rnd() % nb);
+          if (inw[c]) continue;
+          o[a] = c;
+        }
+        const double v = cost(o, b);
+        const double u = (double)(rnd() >> 11) * (1.0 / 9007199254740992.0);
+        if (v < ccost || (T > 0 && u < std::exp((ccost - v) / T))) cur = o, ccost = v;
+        if (ccost < bcost - 1e-12) bcost = ccost, best = cur;
       }
     }
-    if (!improved) break;
+    bests[ci] = std::move(best);
+    bcosts[ci] = bcost;
+  };
+  {
+    std::vector<std::thread> th;
+    for (size_t ci = 1; ci < cands.size(); ++ci) th.emplace_back(search, ci);
+    search(0);
+    for (auto& t : th) t.join();
   }
-  return extend(best, count);
+  size_t gi = 0;
+  for (size_t ci = 1; ci < cands.size(); ++ci)
+    if (bcosts[ci] < bcosts[gi] - 1e-12) gi = ci;
+  if (b_out) *b_out = cands[gi];
+  return extend(bests[gi], count);
 }
 
 std::vector<int> seg_row_order(const double* A, int n, const std::vector<int>& walk) {
@@ -353,6 +478,21 @@ std::vector<int> seg_row_order(const double* A, int n, const std::vector<int>& w
 }
 
 // ----------------------------------------------------------------- codegen --
+
+// Constants of the row copies (seg_fit): a_k(r) = the + column of walk bit k
+// at engine row r; cx_r[S] = a_{k(low)}(r) (+ cx_r[S \ low]) for the lowest
+// set bit low of S (walk bit k(low) = ctz(low) + 1), cy_r[S] = a_0(r) (+ cx_r[S]).
+double seg_cx(const Plan& P, int r, uint32_t S) {
+  const uint32_t low = S & (0u - S), rest = S ^ low;
+  const int k = __builtin_ctz(low) + 1;
+  const double a = P.cols[(size_t)(2 * (P.lay.L + k)) * P.NP + r];
+  return rest ? seg_cx(P, r, rest) + a : a;
+}
+double seg_cy(const Plan& P, int r, uint32_t S) {
+  const double a0 = P.cols[(size_t)(2 * P.lay.L) * P.NP + r];
+  return S ? a0 + seg_cx(P, r, S) : a0;
+}
+
 namespace {
 
 std::string tree(int lo, int hi, const char* v = "x") {
@@ -360,40 +500,6 @@ std::string tree(int lo, int hi, const char* v = "x") {
   const int mid = lo + (hi - lo + 1) / 2;
   return "(" + tree(lo, mid, v) + " * " + tree(mid, hi, v) + ")";
 }
-
-// Values in the generated code.  With cc cached classes every value exists
-// once per state of the cached walk bits it depends on (copy index = that
-// state masked to its classes): row r's copy i is x[r] (i = 0) or x<r>_<i>,
-// y likewise; node i of a tree is <N><i>_<copy>; constant items are <T>.
-struct Names {
-  uint32_t ccmask = 0;
-  std::string X(int r, uint32_t s, uint32_t rsig, const char* arr) const {
-    const uint32_t i = s & rsig & ccmask;
-    return i ? std::string(arr) + std::to_string(r) + "_" + std::to_string(i)
-             : std::string(arr) + "[" + std::to_string(r) + "]";
-  }
-};
-
-struct TreeNames {
-  const ProdTree* t;
-  const Names* nm;
-  const std::vector<uint32_t>* rsig;
-  std::string arr, N, T;
-  uint32_t csig(int id) const {
-    const uint32_t s = id < t->items() ? t->item_sig[id] : t->sig[id - t->items()];
-    return s & nm->ccmask;
-  }
-  std::string id(int i, uint32_t s) const {
-    if (i < t->items()) {
-      const int r = t->item_row[i];
-      return r < 0 ? T : nm->X(r, s, (*rsig)[r], arr.c_str());
-    }
-    return N + std::to_string(i - t->items()) + "_" + std::to_string(s & csig(i));
-  }
-  std::string top(uint32_t s) const { return t->root() < 0 ? std::string() : id(t->root(), s); }
-  std::string node(int i, uint32_t s) const { return id(t->a[i], s) + " * " + id(t->b[i], s); }
-  uint32_t root_csig() const { return t->root() < 0 ? 0u : csig(t->root()); }
-};
 
 // submasks of m in increasing order (0 included)
 std::vector<uint32_t> submasks(uint32_t m) {
@@ -403,6 +509,12 @@ std::vector<uint32_t> submasks(uint32_t m) {
   return v;
 }
 
+// A statement of a step whose operands may read constants of the step's
+// constant stream: "@<i>@" in `text` stands for the stream's i-th value.
+struct Stmt {
+  std::string text;
+};
+
 // Generated kernel (paired segmented walk).  Gray steps 2j and 2j+1 differ in
 // walk bit 0 only, so they are evaluated together: segment 0 (the rows walk
 // bit 0 touches) is held twice, x (bit 0 clear) and y = x + a_0 (bit 0 set),
@@ -410,99 +522,259 @@ std::vector<uint32_t> submasks(uint32_t m) {
 // the product of every other row.  The pair walk is a Gray walk over walk
 // bits 1..m-1 (pair bit p = walk bit p+1).  Both products are product trees
 // (make_tree): a step re-forms the nodes above the rows it touches.
-// Cached classes (walk bits 1..cc): every value that depends on them is held
+// Cached classes (walk bits 1..cc): every node that depends on them is held
 // in each of their states, so their pair steps only accumulate (the state is
 // known at compile time inside the unrolled block) and every other step
-// updates all copies.
+// updates all copies.  Only x[r] (x^0) is walked; the row copies x^S, y^S are
+// x[r] + a constant (seg_cx / seg_cy), kept live or formed on demand inside
+// the node that reads them (ProdTree::item_live).
+//
+// Names: x[r] = x^0_r; live copies x<r>_<S> (S != 0) and y[r] / y<r>_<S>;
+// node i of a tree <N><i>_<copy>, copy = state masked to the node's classes;
+// constant items (tails) <T>; D<S> = top_x - top_y of segment 0.
 struct Gen {
   const Plan& P;
   int len0;
+  uint32_t ccm;
   std::vector<uint32_t> rsig;
-  Names nm;
-  TreeNames outer, inx, iny;
   std::ostringstream o;
-  explicit Gen(const Plan& p) : P(p), len0(p.seg_start[1]), rsig(p.n, 0u) {
+  // constant directory (init): (row, S, variant) -> index into the jtab tail
+  std::map<std::tuple<int, uint32_t, int>, int> cdir;
+  std::vector<double> ctab;          // appended to P.jtab at cbase
+  size_t cbase = 0;
+  std::vector<int> kofs;             // per step class: offset (doubles, from cbase) of its stream
+  std::vector<std::vector<Stmt>> cls_stmts;
+  std::vector<std::vector<double>> cls_consts;
+  // which tree item holds row r: (tree 0 outer / 1 inner, item)
+  std::vector<std::pair<int, int>> item_of;
+
+  explicit Gen(const Plan& p) : P(p), len0(p.seg_start[1]), ccm((1u << p.seg_cc) - 1u), rsig(p.n, 0u) {
     for (int k = 1; k < p.lay.m; ++k)
       for (int r : p.touched[k]) rsig[r] |= 1u << step_class(k, p.seg_b);
-    nm.ccmask = (1u << p.seg_cc) - 1u;
-    outer = {&p.outer_tree, &nm, &rsig, "x", "o", "Ro"};
-    inx = {&p.inner_tree, &nm, &rsig, "x", "px", "Cx"};
-    iny = {&p.inner_tree, &nm, &rsig, "y", "py", "Cy"};
+    item_of.assign(p.n, {-1, -1});
+    for (int ti = 0; ti < 2; ++ti) {
+      const ProdTree& t = ti ? p.inner_tree : p.outer_tree;
+      for (int j = 0; j < t.items(); ++j)
+        if (t.item_row[j] >= 0) item_of[t.item_row[j]] = {ti, j};
+    }
+  }
+  const ProdTree& tr(int ti) const { return ti ? P.inner_tree : P.outer_tree; }
+  uint32_t rs(int r) const { return rsig[r] & ccm; }
+  bool live(int r, int v) const {  // v: 0 copies over x, 1 over y
+    const auto it = item_of[r];
+    return it.first >= 0 && (tr(it.first).item_live[it.second] >> v) & 1u;
+  }
+  double cval(int r, uint32_t S, int v) const { return v ? seg_cy(P, r, S) : seg_cx(P, r, S); }
+  // name of a row copy (S already masked to the row's cached classes)
+  std::string cname(int r, uint32_t S, int v) const {
+    if (v == 0) return S ? "x" + std::to_string(r) + "_" + std::to_string(S) : "x[" + std::to_string(r) + "]";
+    return S ? "y" + std::to_string(r) + "_" + std::to_string(S) : "y[" + std::to_string(r) + "]";
+  }
+  int dir(int r, uint32_t S, int v) {
+    auto key = std::make_tuple(r, S, v);
+    auto it = cdir.find(key);
+    if (it != cdir.end()) return it->second;
+    const int i = (int)ctab.size();
+    ctab.push_back(cval(r, S, v));
+    cdir[key] = i;
+    return i;
+  }
+  // init-time constant: one scalar load of the directory entry
+  std::string kinit(int r, uint32_t S, int v) {
+    return "opaque_c(p.jtab, " + std::to_string((cbase + dir(r, S, v)) * 8) + "u)[0]";
   }
 
-  void tree_init(const TreeNames& t, const char* ind) {
-    if (t.t->tail_hi > t.t->tail_lo)
-      o << ind << "const double " << t.T << " = " << tree(t.t->tail_lo, t.t->tail_hi, t.arr.c_str()) << ";\n";
-    for (int i = 0; i < t.t->K(); ++i)
-      for (uint32_t s : submasks(t.csig(t.t->items() + i)))
-        o << ind << "double " << t.N << i << "_" << s << " = " << t.node(i, s) << ";\n";
+  // tree operand id in state S: `step` = inside a step (on-demand copies read
+  // the stream `ks`), else init (every copy is a named variable)
+  std::string opnd(int ti, int v, int id, uint32_t S, std::vector<double>* ks) const {
+    const ProdTree& t = tr(ti);
+    if (id < t.items()) {
+      const int r = t.item_row[id];
+      if (r < 0) return ti == 0 ? "Ro" : (v ? "Cy" : "Cx");
+      const uint32_t s = S & rs(r);
+      if (v == 0 && s == 0) return "x[" + std::to_string(r) + "]";
+      if (!ks || live(r, v)) return cname(r, s, v);
+      ks->push_back(cval(r, s, v));
+      return "(x[" + std::to_string(r) + "] + @" + std::to_string(ks->size() - 1) + "@)";
+    }
+    const int i = id - t.items();
+    const char* N = ti == 0 ? "o" : (v ? "py" : "px");
+    return N + std::to_string(i) + "_" + std::to_string(S & t.sig[i] & ccm);
   }
-  // re-form the nodes of step class c (every copy); returns whether the root changed
-  bool tree_update(const TreeNames& t, int c, const char* ind) {
-    for (int i = 0; i < t.t->K(); ++i)
-      if ((t.t->sig[i] >> c) & 1u)
-        for (uint32_t s : submasks(t.csig(t.t->items() + i)))
-          o << ind << "  " << t.N << i << "_" << s << " = " << t.node(i, s) << ";\n";
-    return (t.t->root_sig() >> c) & 1u;
+  uint32_t csig(int ti, int id) const {
+    const ProdTree& t = tr(ti);
+    return (id < t.items() ? t.item_sig[id] : t.sig[id - t.items()]) & ccm;
   }
-  std::string dname(uint32_t s) const { return "D" + std::to_string(s & inx.root_csig()); }
-  void set_d(const char* ind, bool decl) {
-    for (uint32_t s : submasks(inx.root_csig()))
-      o << ind << (decl ? "double " : "") << dname(s) << " = " << inx.top(s) << " - " << iny.top(s) << ";\n";
+  std::string top(int ti, int v, uint32_t S) const {
+    const ProdTree& t = tr(ti);
+    return t.root() < 0 ? std::string() : opnd(ti, v, t.root(), S, nullptr);
   }
+  std::string node(int ti, int v, int i, uint32_t S, std::vector<double>* ks) const {
+    const ProdTree& t = tr(ti);
+    return opnd(ti, v, t.a[i], S, ks) + " * " + opnd(ti, v, t.b[i], S, ks);
+  }
+  uint32_t inner_root_csig() const { return P.inner_tree.root() < 0 ? 0u : csig(1, P.inner_tree.root()); }
+  std::string dname(uint32_t s) const { return "D" + std::to_string(s & inner_root_csig()); }
+
+  // statements of a step of class c after its x^0 adds (same for every
+  // occurrence of the class): live copies of the rows it touches, the dirty
+  // nodes of every copy, D
+  void build_class(int c) {
+    std::vector<Stmt>& st = cls_stmts[c];
+    std::vector<double>& ks = cls_consts[c];
+    const std::vector<int>& rows = c < P.seg_b ? P.touched[c + 1] : P.dyn_rows;
+    for (int r : rows)
+      for (int v = 0; v < (r < len0 ? 2 : 1); ++v)
+        if (live(r, v))
+          for (uint32_t S : submasks(rs(r))) {
+            if (v == 0 && S == 0) continue;
+            ks.push_back(cval(r, S, v));
+            st.push_back({cname(r, S, v) + " = x[" + std::to_string(r) + "] + @" + std::to_string(ks.size() - 1) +
+                          "@;"});
+          }
+    auto upd = [&](int ti, int v) {
+      const ProdTree& t = tr(ti);
+      for (int i = 0; i < t.K(); ++i)
+        if ((t.sig[i] >> c) & 1u)
+          for (uint32_t S : submasks(t.sig[i] & ccm)) {
+            const std::string lhs = opnd(ti, v, t.items() + i, S, nullptr);
+            st.push_back({lhs + " = " + node(ti, v, i, S, &ks) + ";"});
+          }
+    };
+    upd(0, 0);
+    if ((P.inner_tree.root_sig() >> c) & 1u) {
+      upd(1, 0);
+      upd(1, 1);
+      for (uint32_t S : submasks(inner_root_csig()))
+        st.push_back({dname(S) + " = " + top(1, 0, S) + " - " + top(1, 1, S) + ";"});
+    }
+  }
+
+  // One pair step of class c: the x^0 adds of `rows` (values from the table
+  // at `cv`: packed, value i for rows[i], or a full column, value rows[i]),
+  // then the class's statements (constants from its stream in jtab).  Its
+  // operands are wave-uniform dbl8 pieces loaded into SGPRs; the step is cut
+  // into regions of at most kp pieces, each pinned to SGPRs and closed by a
+  // scheduling barrier.  With prefetch the pieces of region r+1 are loaded at
+  // the start of region r and pinned at its end, so their latency hides
+  // behind region r's arithmetic (2 regions' pieces live at a time).
+  // The budget is Plan::seg_kp (4: measured best on the n = 40 bench matrix,
+  // 2.33e12 Gray steps/s against 2.27e12 at 2 and 2.04e12 at 1); compile()
+  // regenerates with a smaller one if the register allocator runs out.
+  // SUP_JIT_PF overrides prefetch (experiments).
+  void emit_step(const std::string& cv_expr, const std::vector<int>& rows, bool full, int c, const char* ind) {
+    const int kp = P.seg_kp;
+    static const bool pf = std::getenv("SUP_JIT_PF") ? std::atoi(std::getenv("SUP_JIT_PF")) != 0 : true;
+    // SUP_JIT_ASMLD: the loads as inline-asm s_load_dwordx16 (issued where
+    // written; the compiler otherwise sinks them to their pin) and the pin as
+    // an explicit s_waitcnt tied to the pieces
+    static const bool asmld = std::getenv("SUP_JIT_ASMLD") ? std::atoi(std::getenv("SUP_JIT_ASMLD")) != 0 : false;
+    struct Item {
+      std::string text;             // with @i@ (stream) / #i# (column value) placeholders
+      std::vector<int> pieces;      // encoded: column piece p -> p, stream piece p -> 1000 + p
+    };
+    std::vector<Item> items;
+    for (size_t i = 0; i < rows.size(); ++i) {
+      const int vi = full ? rows[i] : (int)i;
+      items.push_back({"x[" + std::to_string(rows[i]) + "] += #" + std::to_string(vi) + "#;", {vi / 8}});
+    }
+    if (c >= P.seg_cc)
+      for (const Stmt& st : cls_stmts[c]) {
+        Item it{st.text, {}};
+        for (size_t q = st.text.find('@'); q != std::string::npos; q = st.text.find('@', st.text.find('@', q + 1) + 1)) {
+          const int pc = 1000 + std::atoi(st.text.c_str() + q + 1) / 8;
+          if (std::find(it.pieces.begin(), it.pieces.end(), pc) == it.pieces.end()) it.pieces.push_back(pc);
+        }
+        items.push_back(std::move(it));
+      }
+    if (items.empty()) return;
+    // regions
+    std::vector<std::pair<size_t, size_t>> reg;     // item ranges
+    std::vector<std::vector<int>> rp;                 // their pieces
+    for (size_t i = 0; i < items.size();) {
+      std::vector<int> pcs;
+      size_t j = i;
+      for (; j < items.size(); ++j) {
+        std::vector<int> need = pcs;
+        for (int pc : items[j].pieces)
+          if (std::find(need.begin(), need.end(), pc) == need.end()) need.push_back(pc);
+        if ((int)need.size() > kp && j > i) break;
+        pcs = need;
+      }
+      reg.push_back({i, j});
+      rp.push_back(pcs);
+      i = j;
+    }
+    auto pname = [](size_t r, int pc) {
+      return (pc >= 1000 ? "k" + std::to_string(pc - 1000) : "v" + std::to_string(pc)) + "_" + std::to_string(r);
+    };
+    auto load = [&](size_t r) {
+      for (int pc : rp[r]) {
+        if (asmld) {
+          o << ind << "  jdbl8 " << pname(r, pc) << ";\n";
+          o << ind << "  asm volatile(\"s_load_dwordx16 %0, %1, " << (pc % 1000) * 64 << "\" : \"=s\"(" << pname(r, pc)
+            << ") : \"s\"(" << (pc >= 1000 ? "kvb" : "cvb") << "));\n";
+        } else {
+          o << ind << "  jdbl8 " << pname(r, pc) << " = "
+            << (pc >= 1000 ? "kv[" + std::to_string(pc - 1000) : "cv[" + std::to_string(pc)) << "];\n";
+        }
+      }
+    };
+    auto pin = [&](size_t r) {
+      if (rp[r].empty()) return;
+      o << ind << "  asm volatile(\"" << (asmld ? "s_waitcnt lgkmcnt(0)" : "") << "\" :";
+      for (size_t q = 0; q < rp[r].size(); ++q) o << (q ? ", " : " ") << "\"+s\"(" << pname(r, rp[r][q]) << ")";
+      o << ");\n";
+    };
+    o << ind << "{\n";
+    o << ind << "  cjdbl8* cv = (cjdbl8*)" << cv_expr << ";\n";
+    if (asmld) o << ind << "  const uint64_t cvb = (uint64_t)cv;\n";
+    if (c >= P.seg_cc && !cls_stmts[c].empty()) {
+      o << ind << "  cjdbl8* kv = (cjdbl8*)opaque_c(p.jtab, " << (cbase + kofs[c]) * 8 << "u);\n";
+      if (asmld) o << ind << "  const uint64_t kvb = (uint64_t)kv;\n";
+    }
+    load(0);
+    pin(0);
+    for (size_t r = 0; r < reg.size(); ++r) {
+      if (pf && r + 1 < reg.size()) load(r + 1);
+      for (size_t i = reg[r].first; i < reg[r].second; ++i) {
+        const std::string& t = items[i].text;
+        std::string out;
+        for (size_t q = 0; q < t.size(); ++q) {
+          if (t[q] != '@' && t[q] != '#') {
+            out += t[q];
+            continue;
+          }
+          const size_t e = t.find(t[q], q + 1);
+          const int idx = std::atoi(t.substr(q + 1, e - q - 1).c_str());
+          out += pname(r, (t[q] == '@' ? 1000 : 0) + idx / 8) + "[" + std::to_string(idx % 8) + "]";
+          q = e;
+        }
+        o << ind << "  " << out << "\n";
+      }
+      if (r + 1 < reg.size()) {
+        if (pf) pin(r + 1);
+        o << ind << "  __builtin_amdgcn_sched_barrier(0);\n";
+        if (!pf) {
+          load(r + 1);
+          pin(r + 1);
+        }
+      }
+    }
+    o << ind << "}\n";
+  }
+
   // accumulate pair term with cached state S
   void accumulate(bool neg, uint32_t S, const char* ind) {
-    const std::string D = dname(S), U = outer.top(S);
+    const std::string D = dname(S), U = top(0, 0, S);
     if (U.empty()) o << ind << "acc " << (neg ? "-= " : "+= ") << D << ";\n";
     else o << ind << "acc = __builtin_fma(" << (neg ? "-" : "") << D << ", " << U << ", acc);\n";
   }
 
-  // Add the values at table pointer `cv` (dbl8 pieces) to rows `rows` (every
-  // copy, and their y copies in segment 0): value i of the block belongs to
-  // row rows[i] (packed table), or value rows[i] of the block (full column,
-  // `full`).  At most 2 pieces (32 SGPRs) are pinned at a time.
-  void adds(const std::vector<int>& rows, bool full, const char* ind) {
-    std::vector<std::pair<int, int>> vr;  // (value index, row)
-    for (size_t i = 0; i < rows.size(); ++i) vr.push_back({full ? rows[i] : (int)i, rows[i]});
-    std::vector<int> pieces;
-    for (auto& e : vr)
-      if (pieces.empty() || pieces.back() != e.first / 8) pieces.push_back(e.first / 8);
-    for (size_t g = 0; g < pieces.size(); g += 2) {
-      const size_t ge = std::min(pieces.size(), g + 2);
-      for (size_t q = g; q < ge; ++q) o << ind << "  jdbl8 v" << pieces[q] << " = cv[" << pieces[q] << "];\n";
-      o << ind << "  asm volatile(\"\" :";
-      for (size_t q = g; q < ge; ++q) o << (q > g ? ", " : " ") << "\"+s\"(v" << pieces[q] << ")";
-      o << ");\n";
-      for (auto& e : vr)
-        if (e.first / 8 >= pieces[g] && e.first / 8 <= pieces[ge - 1]) {
-          const std::string v = "v" + std::to_string(e.first / 8) + "[" + std::to_string(e.first % 8) + "]";
-          const int r = e.second;
-          for (uint32_t s : submasks(rsig[r] & nm.ccmask)) {
-            o << ind << "  " << nm.X(r, s, rsig[r], "x") << " += " << v << ";\n";
-            if (r < len0) o << ind << "  " << nm.X(r, s, rsig[r], "y") << " += " << v << ";\n";
-          }
-        }
-      if (ge < pieces.size()) o << ind << "  __builtin_amdgcn_sched_barrier(0);\n";
-    }
-  }
-
-  void products(int c, const char* ind) {
-    tree_update(outer, c, ind);
-    if (tree_update(inx, c, ind)) {
-      tree_update(iny, c, ind);
-      set_d((std::string(ind) + "  ").c_str(), false);
-    }
-  }
-
   // pair step flipping walk bit k <= seg_b: packed touched values; `off` = byte offset expression
   void step(int k, const std::string& off, const char* ind) {
-    const std::vector<int>& t = P.touched[k];
-    if (t.empty()) return;
-    o << ind << "{\n";
-    o << ind << "  cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off << ");\n";
-    adds(t, false, ind);
-    products(step_class(k, P.seg_b), ind);
-    o << ind << "}\n";
+    if (P.touched[k].empty()) return;
+    emit_step("opaque_c(p.jtab, " + off + ")", P.touched[k], false, step_class(k, P.seg_b), ind);
   }
 
   std::string off_const(int k, int neg) const {
@@ -522,12 +794,45 @@ struct Gen {
     return S;
   }
 
+  // the constant tail appended to P.jtab (directory for the chunk start, then
+  // one stream per step class, each 8-double aligned)
+  std::vector<double> tail() const {
+    std::vector<double> t = ctab;
+    t.resize((t.size() + 7) & ~(size_t)7, 0.0);
+    for (size_t c = 0; c < cls_consts.size(); ++c) {
+      t.insert(t.end(), cls_consts[c].begin(), cls_consts[c].end());
+      t.resize((t.size() + 7) & ~(size_t)7, 0.0);
+    }
+    return t;
+  }
+
   std::string source() {
     const int n = P.n, L = P.lay.L, m = P.lay.m, b = P.seg_b, cc = P.seg_cc;
     const unsigned B = 1u << b, Q = 1u << (m - 1 - b);
+    cbase = P.seg_cbase;
+    // the chunk start's directory first (its size fixes the streams' offsets)
+    for (int r = 0; r < n; ++r)
+      for (int v = 0; v < (r < len0 ? 2 : 1); ++v)
+        for (uint32_t S : submasks(rs(r)))
+          if (v == 1 || S != 0) dir(r, S, v);
+    cls_stmts.assign(b + 1, {});
+    cls_consts.assign(b + 1, {});
+    for (int c = cc; c <= b; ++c) build_class(c);
+    kofs.assign(b + 1, 0);
+    {
+      size_t off = (ctab.size() + 7) & ~(size_t)7;
+      for (int c = 0; c <= b; ++c) {
+        kofs[c] = (int)off;
+        off = (off + cls_consts[c].size() + 7) & ~(size_t)7;
+      }
+    }
+    int nlive = 0;
+    for (int r = 0; r < n; ++r)
+      for (int v = 0; v < 2; ++v) nlive += live(r, v);
     o << "// generated by superman_amd jit.cpp: paired segmented Gray walk, n=" << n << " L=" << L << " m=" << m
       << " segment0=" << len0 << " (" << P.inner_tree.K() << " tree nodes) outer tree nodes=" << P.outer_tree.K()
-      << " pair bits specialised=" << b << " cached=" << cc << " live values~" << P.seg_regs << "\n";
+      << " pair bits specialised=" << b << " cached=" << cc << " live values~" << P.seg_regs
+      << " live row-copy sets=" << nlive << "\n";
     o << "#include \"walk_common.hpp\"\n";
     o << "namespace sup {\n";
     o << "typedef double jdbl8 __attribute__((ext_vector_type(8)));\n";
@@ -552,41 +857,44 @@ struct Gen {
     o << "      const uint64_t ga = p.chunk_begin + a;\n";
     o << "      double x[N], y[" << len0 << "];\n";
     o << "      chunk_start<N>(x, p, ga, lane);\n";
-    o << "      {\n";  // y = x + a_0 on segment 0 (the + block of walk bit 0)
+    o << "      {\n";  // y = x + a_0 on segment 0 (the + block of walk bit 0) = y^0
     o << "        cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off_const(0, 0) << ");\n";
     for (int r = 0; r < len0; ++r) o << "        y[" << r << "] = x[" << r << "] + cv[" << r / 8 << "][" << r % 8 << "];\n";
     o << "      }\n";
-    // copies for the cached states: copy i = copy (i without its lowest bit)
-    // + the + column of that bit's walk bit (rows it touches)
+    // every copy for the cached states (init: all named; on-demand ones are
+    // dead after the trees are formed)
     for (int r = 0; r < n; ++r)
-      for (uint32_t s : submasks(rsig[r] & nm.ccmask)) {
-        if (!s) continue;
-        const uint32_t low = s & (0u - s);
-        const int k = __builtin_ctz(low) + 1;
-        const auto& t = P.touched[k];
-        const int pos = (int)(std::lower_bound(t.begin(), t.end(), r) - t.begin());
-        const std::string v = "((cjdbl8*)opaque_c(p.jtab, " + off_const(k, 0) + "))[" + std::to_string(pos / 8) +
-                              "][" + std::to_string(pos % 8) + "]";
-        o << "      double " << nm.X(r, s, rsig[r], "x") << " = " << nm.X(r, s ^ low, rsig[r], "x") << " + " << v
-          << ";\n";
-        if (r < len0)
-          o << "      double " << nm.X(r, s, rsig[r], "y") << " = " << nm.X(r, s ^ low, rsig[r], "y") << " + " << v
+      for (int v = 0; v < (r < len0 ? 2 : 1); ++v)
+        for (uint32_t S : submasks(rs(r))) {
+          if (S == 0) continue;
+          o << "      double " << cname(r, S, v) << " = x[" << r << "] + " << kinit(r, S, v) << ";\n";
+        }
+    // constant items (tails) and every node copy
+    auto tree_init = [&](int ti, int v) {
+      const ProdTree& t = tr(ti);
+      if (t.tail_hi > t.tail_lo)
+        o << "      const double " << (ti == 0 ? "Ro" : (v ? "Cy" : "Cx")) << " = "
+          << tree(t.tail_lo, t.tail_hi, v ? "y" : "x") << ";\n";
+      for (int i = 0; i < t.K(); ++i)
+        for (uint32_t S : submasks(t.sig[i] & ccm))
+          o << "      double " << opnd(ti, v, t.items() + i, S, nullptr) << " = " << node(ti, v, i, S, nullptr)
             << ";\n";
-      }
-    tree_init(outer, "      ");
+    };
+    tree_init(0, 0);
     // Rows no walk bit touches (the outer tree's tail, Ro) are constant over the
     // chunk: when Ro is an exact zero in every valid lane (integer matrices),
     // every product of the chunk is zero and the walk is skipped (part = +0).
     o << "      double acc = 0.0;\n";
     if (P.outer_tree.tail_hi > P.outer_tree.tail_lo)
-      o << "      if (__builtin_amdgcn_ballot_w64(lane_valid && " << outer.T << " != 0.0) != 0) {\n";
+      o << "      if (__builtin_amdgcn_ballot_w64(lane_valid && Ro != 0.0) != 0) {\n";
     else
       o << "      {\n";
-    tree_init(inx, "      ");
-    tree_init(iny, "      ");
-    set_d("      ", true);
+    tree_init(1, 0);
+    tree_init(1, 1);
+    for (uint32_t S : submasks(inner_root_csig()))
+      o << "      double " << dname(S) << " = " << top(1, 0, S) << " - " << top(1, 1, S) << ";\n";
     {
-      const std::string U = outer.top(0);
+      const std::string U = top(0, 0, 0);
       o << "      acc = " << (U.empty() ? dname(0) : dname(0) + " * " + U) << ";\n";
     }
     // two-level lane sum: acc folds into tot after each shared dyn step, so
@@ -618,10 +926,9 @@ struct Gen {
       o << ind << "if (q + 1u < " << Q << "u) {\n";
       o << ind << "  const uint32_t kk = (uint32_t)__builtin_ctz(q + 1u);\n";
       o << ind << "  const uint32_t ng = ((q + 1u) >> (kk + 1u)) & 1u;\n";
-      o << ind << "  cjdbl8* cv = (cjdbl8*)opaque_c(p.cols, (2u * (" << (L + b + 1) << "u + kk) + ng) * "
-        << P.NP * 8 << "u);\n";
-      adds(P.dyn_rows, true, ind);
-      products(P.seg_b, ind);
+      emit_step("opaque_c(p.cols, (2u * (" + std::to_string(L + b + 1) + "u + kk) + ng) * " +
+                    std::to_string(P.NP * 8) + "u)",
+                P.dyn_rows, true, P.seg_b, "          ");
       accumulate(false, 0u, "          ");
       o << ind << "  tot += acc;\n" << ind << "  acc = 0.0;\n";
       o << ind << "}\n";
@@ -701,7 +1008,23 @@ int build_seg(Plan& P) {
       if (cnt > P.sub_start.back()) P.sub_start.push_back(cnt);
     }
   }
-  P.seg_b = seg_static_bits(m);
+  // specialised pair bits: the walk-order search's choice (make_plan), else
+  // the candidate with the cheapest fit on these rows
+  if (P.seg_b < 1 || P.seg_b > m - 1) {
+    P.seg_b = seg_static_bits(m);
+    if (!std::getenv("SUP_JIT_B")) {
+      double best = 1e300;
+      for (const int cb : seg_b_candidates(m)) {
+        SegRows R;
+        R.n = n, R.m = m, R.touched = P.touched;
+        R.len0 = P.seg_start[1], R.s_end = P.sub_start.back(), R.r_end = P.seg_start.back();
+        seg_rows_finish(R, cb);
+        const SegFit f = seg_best(R);
+        const double sc = seg_block_bytes(f, cb) > kMaxBlockBytes ? 1e300 : seg_score(f);
+        if (sc < best - 1e-12) best = sc, P.seg_b = cb;
+      }
+    }
+  }
   P.dyn_rows.clear();
   {
     std::vector<char> in(n, 0);
@@ -714,9 +1037,10 @@ int build_seg(Plan& P) {
     SegRows R;
     R.n = n, R.m = m, R.touched = P.touched;
     R.len0 = P.seg_start[1], R.s_end = P.sub_start.back(), R.r_end = P.seg_start.back();
-    seg_rows_finish(R);
+    seg_rows_finish(R, P.seg_b);
     SegFit f;
-    if (const char* e = std::getenv("SUP_JIT_CC")) f = seg_fit(R, std::max(0, std::min({std::atoi(e), R.b - 1, 2})));
+    if (const char* e = std::getenv("SUP_JIT_CC"))
+      f = seg_fit(R, std::max(0, std::min({std::atoi(e), R.b - 1, kMaxCachedBits})));
     else f = seg_best(R);
     P.outer_tree = std::move(f.outer);
     P.inner_tree = std::move(f.inner);
@@ -724,7 +1048,8 @@ int build_seg(Plan& P) {
     P.seg_ops = f.ops;
     P.seg_regs = f.regs;
     if (std::getenv("SUP_JIT_VERBOSE"))
-      std::fprintf(stderr, "seg plan n=%d m=%d ops/step=%.4f regs=%d cc=%d\n", n, m, f.ops, f.regs, f.cc);
+      std::fprintf(stderr, "seg plan n=%d m=%d b=%d ops/step=%.4f regs=%d cc=%d\n", n, m, P.seg_b, f.ops, f.regs,
+                   f.cc);
   }
   P.jofs.assign(m, 0);
   P.jtab.clear();
@@ -738,8 +1063,15 @@ int build_seg(Plan& P) {
       P.jtab[P.jofs[k] + blk + i] = P.cols[(size_t)(2 * (L + k) + 1) * P.NP + t[i]];
     }
   }
+  P.seg_cbase = P.jtab.size();
+  P.seg_kp = 4;
+  if (const char* e = std::getenv("SUP_JIT_KP")) P.seg_kp = std::max(1, std::atoi(e));
   Gen g(P);
   P.jit_src = g.source();
+  {
+    const std::vector<double> t = g.tail();
+    P.jtab.insert(P.jtab.end(), t.begin(), t.end());
+  }
   std::string key = P.jit_src;
   for (int i = 0; i < kJitNopts; ++i) key += std::string("\n//") + kJitOpts[i];
   key += std::string("\n//") + kWalkCommonSrc + kWalkParamsSrc;
@@ -827,17 +1159,29 @@ int compile(const Plan& P, std::shared_ptr<std::vector<char>>& code) {
   hiprtcProgram prog;
   const char* hdr[] = {kWalkCommonSrc, kWalkParamsSrc};
   const char* names[] = {"walk_common.hpp", "walk_params.hpp"};
-  if (hiprtcCreateProgram(&prog, P.jit_src.c_str(), "sup_walk_seg.hip", 2, hdr, names) != HIPRTC_SUCCESS) {
-    set_error("hiprtcCreateProgram failed");
-    return SUP_EHIP;
-  }
-  const hiprtcResult cr = hiprtcCompileProgram(prog, kJitNopts, kJitOpts);
-  if (cr != HIPRTC_SUCCESS) {
+  // A step region's pinned pieces can exceed the SGPRs the allocator has left
+  // ("ran out of registers"); the source is then regenerated with half the
+  // piece budget (the same operations in the same order: bit-identical
+  // results, same tables), down to one piece.
+  std::string src = P.jit_src;
+  for (int kp = P.seg_kp;; kp /= 2) {
+    if (hiprtcCreateProgram(&prog, src.c_str(), "sup_walk_seg.hip", 2, hdr, names) != HIPRTC_SUCCESS) {
+      set_error("hiprtcCreateProgram failed");
+      return SUP_EHIP;
+    }
+    const hiprtcResult cr = hiprtcCompileProgram(prog, kJitNopts, kJitOpts);
+    if (cr == HIPRTC_SUCCESS) break;
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);
     std::string log(ls, '\0');
     if (ls) hiprtcGetProgramLog(prog, &log[0]);
     hiprtcDestroyProgram(&prog);
+    if (kp > 1 && log.find("ran out of registers") != std::string::npos) {
+      Plan Q = P;
+      Q.seg_kp = kp / 2;
+      src = Gen(Q).source();
+      continue;
+    }
     set_error(std::string("hiprtc compile of the segmented walk failed: ") + hiprtcGetErrorString(cr) + "\n" +
               log.substr(0, 2000));
     return SUP_EHIP;

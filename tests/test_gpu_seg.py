@@ -119,7 +119,7 @@ def test_seg_n40_bench_matrix(sup):
     assert -2 * full == r_seg
 
 
-@pytest.mark.parametrize("cc", [0, 1, 2])
+@pytest.mark.parametrize("cc", [0, 1, 2, 3])
 def test_seg_cached_bits_bitexact(sup, orc, monkeypatch, cc):
     """Each cached-walk-bit count (SUP_JIT_CC forces it) on the GPU: bit-exact
     against the oracle's per-state mirror and the host twin."""
@@ -146,7 +146,7 @@ def test_seg_n40_d02_companion(sup):
     assert sup.perman(b, algo=4, jit=1) == r_seg * 4.0
 
 
-@pytest.mark.parametrize("n,d,seed", [(20, 0.2, 1), (24, 0.15, 3)])
+@pytest.mark.parametrize("n,d,seed", [(24, 0.15, 4), (24, 0.15, 3)])
 def test_seg_chunk_skip_gpu(sup, orc, n, d, seed):
     """Wave-chunks whose walk-untouched rows are exactly zero in every lane are
     skipped by the generated kernel: GPU == host twin (same skip) == oracle
@@ -173,3 +173,20 @@ def test_seg_shared_steps_and_lane_fold_gpu(sup, orc):
     got, st = sup.perman(a, algo=4, kernel="seg", return_stats=True)
     assert st["walk_kind"] == 3
     assert got == sup.perman_cpu(a, "seg", threads=8) == orc.engine_perman_as(sup, a, "seg", threads=8)
+
+
+@pytest.mark.parametrize("b", [6, 7, 8])
+def test_seg_pair_bits_bitexact_gpu(sup, orc, monkeypatch, b):
+    """Specialised pair-bit counts above the old fixed 5 (the plan now picks
+    5-8 by op count; SUP_JIT_B forces one): n = 30 (10 walk bits, so a shared
+    step remains): GPU == host twin == oracle mirror bit for bit."""
+    monkeypatch.setenv("SUP_JIT_B", str(b))
+    rng = np.random.default_rng(300 + b)
+    n = 30
+    a = np.where(rng.random((n, n)) < 0.3, rng.random((n, n)) * 5, 0.0)
+    a[np.arange(n), rng.permutation(n)] = 1.0
+    info = sup.plan_info(a, "seg")
+    assert info["pair_bits"] == b and info["m"] - 1 > b
+    got = sup.perman(a, algo=4, kernel="seg")
+    assert got == orc.engine_perman_as(sup, a, "seg", threads=16)
+    assert got == sup.perman_cpu(a, "seg", threads=16)

@@ -35,7 +35,7 @@ def _worker(rank, world, port, mat, q):
     c0, c1 = bench.shard_chunks(n, rank, world)
     info = S.plan_info(mat, "dense")  # the plan sup_perman_shard runs
     part, _ = oracle.engine_range(mat, info["kind"], c0, c1, info["L"], info["m"], info["colmap"], 1,
-                                  info["cached"])
+                                  info["cached"], info["pair_bits"])
     t = torch.tensor([part], dtype=torch.float64)
     dist.all_reduce(t)
     el = torch.tensor([float(rank)], dtype=torch.float64)

@@ -22,12 +22,12 @@ def test_cpu_seg_vs_mirror_and_exact(sup, orc, n, d, seed):
     a = _rand(n, d, seed)
     got = sup.perman_cpu(a, "seg", threads=4)
     assert got == orc.engine_perman_as(sup, a, "seg", threads=4)
-    assert sup.plan_info(a, "seg")["cached"] in (0, 1, 2)
+    assert sup.plan_info(a, "seg")["cached"] in (0, 1, 2, 3)
     exact = float(orc.exact_perman(a))
     assert abs(got - exact) <= 1e-12 * max(abs(exact), 1.0)
 
 
-@pytest.mark.parametrize("cc", [0, 1, 2])
+@pytest.mark.parametrize("cc", [0, 1, 2, 3])
 @pytest.mark.parametrize("n,d,seed", [(13, 0.5, 11), (16, 0.35, 12)])
 def test_cpu_seg_cached_bits(sup, orc, monkeypatch, cc, n, d, seed):
     """Every cached-bit count (walk bits held in every state, SUP_JIT_CC forces
@@ -116,10 +116,10 @@ def _skip_case(sup, n, d, seed):
     return sup.skip_order(a)[0]
 
 
-@pytest.mark.parametrize("n,d,seed", [(20, 0.2, 1), (24, 0.15, 3)])
+@pytest.mark.parametrize("n,d,seed", [(24, 0.15, 4), (24, 0.15, 3)])
 def test_cpu_seg_chunk_skip(sup, orc, n, d, seed):
     """Integer matrices whose rows untouched by the walk are exactly zero in
-    whole wave-chunks: the walk skips those chunks (25 % and 56 % here); the
+    whole wave-chunks: the walk skips those chunks (66 % and 84 % here); the
     host twin (which skips the same chunks) == the oracle mirror (which walks
     them and gets +-0) == the exact permanent."""
     from conftest import seg_skip_fraction
@@ -131,19 +131,47 @@ def test_cpu_seg_chunk_skip(sup, orc, n, d, seed):
 
 
 
-def test_cpu_seg_shared_steps_and_lane_fold(sup, orc):
-    """n = 28 (8 walk bits, 5 specialised pair bits): the shared step of the
-    walk bits above them and the two-level lane sum (acc folds into the running
-    total after each shared step) run on the CPU too; host twin == oracle
-    mirror bit for bit, and the prefix walk to 1e-11."""
+def _n28(sup):
     rng = np.random.default_rng(28)
     n = 28
     mask = rng.random((n, n)) < 0.15
     mask[np.arange(n), rng.permutation(n)] = True
     a = np.where(mask, rng.random((n, n)) * 3, 0).astype(np.float64)
-    a = sup.sort_order(a)[0]
+    return sup.sort_order(a)[0]
+
+
+@pytest.mark.parametrize("b", [3, 4, 5, 6])
+def test_cpu_seg_shared_steps_and_lane_fold(sup, orc, monkeypatch, b):
+    """n = 28 (8 walk bits, b specialised pair bits, SUP_JIT_B forces b): the
+    shared step of the walk bits above them and the two-level lane sum (acc
+    folds into the running total after each shared step) run on the CPU too;
+    host twin == oracle mirror bit for bit, and the prefix walk to 1e-11."""
+    monkeypatch.setenv("SUP_JIT_B", str(b))
+    a = _n28(sup)
     info = sup.plan_info(a, "seg")
-    assert info["m"] - 1 > 5  # more pair bits than specialised ones: shared steps + folds
+    assert info["pair_bits"] == b
+    assert info["m"] - 1 > b  # more pair bits than specialised ones: shared steps + folds
     got = sup.perman_cpu(a, "seg", threads=8)
     assert got == orc.engine_perman_as(sup, a, "seg", threads=8)
     assert rel(got, sup.perman_cpu(a, "sparse", threads=8)) < 1e-11
+
+
+def test_seg_pair_bits_chosen_by_cost(sup, monkeypatch):
+    """Without SUP_JIT_B the plan takes the specialised pair-bit count (5-8,
+    at most m - 1) whose generated code has the fewest ops per Gray step
+    (measured on MI355X, profiles/r2/probe_b.log: 5 -> 6 on the n = 40 bench
+    matrix, 2.06e12 -> 2.14e12 Gray steps/s, as the op count predicts)."""
+    for name, kernel in (("double__40_0.50_0", "dense"), ("double__40_0.20_0", "dense")):
+        a, _, _ = sup.read_matrix(fixture_path(name))
+        auto = sup.plan_info(a, kernel, jit=1)
+        assert auto["kind"] == "seg" and 5 <= auto["pair_bits"] <= min(8, auto["m"] - 1)
+        forced = {}
+        for b in (5, 6, 7, 8):
+            monkeypatch.setenv("SUP_JIT_B", str(b))
+            info = sup.plan_info(a, kernel, jit=1)
+            assert info["pair_bits"] == b
+            forced[b] = info["est_ops_per_step"]
+        monkeypatch.delenv("SUP_JIT_B")
+        # the chosen plan is at least as cheap as every forced b whose code fits
+        assert auto["est_ops_per_step"] <= min(forced[5], forced[6]) + 1e-9, (name, auto, forced)
+        assert auto["est_ops_per_step"] == pytest.approx(forced[auto["pair_bits"]], abs=1e-9)
