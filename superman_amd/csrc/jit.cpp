@@ -650,51 +650,92 @@ struct Gen {
     }
   }
 
-  // One pair step of class c: the x^0 adds of `rows` (values from the table
-  // at `cv`: packed, value i for rows[i], or a full column, value rows[i]),
-  // then the class's statements (constants from its stream in jtab).  Its
-  // operands are wave-uniform dbl8 pieces loaded into SGPRs; the step is cut
-  // into regions of at most kp pieces, each pinned to SGPRs and closed by a
-  // scheduling barrier.  With prefetch the pieces of region r+1 are loaded at
-  // the start of region r and pinned at its end, so their latency hides
-  // behind region r's arithmetic (2 regions' pieces live at a time).
-  // The budget is Plan::seg_kp (4: measured best on the n = 40 bench matrix,
-  // 2.33e12 Gray steps/s against 2.27e12 at 2 and 2.04e12 at 1); compile()
+  // ---- straight-line code as a stream of items over SGPR pieces ----
+  // An item is one statement; its operands are wave-uniform dbl8 pieces
+  // (column values, row-copy constants) loaded with s_load_dwordx16.  `$i:e$`
+  // in an item's text is element e of piece i (pieces[i] = its load
+  // expression).  emit_items cuts the stream into regions of at most seg_kp
+  // distinct pieces, each region's pieces pinned to SGPRs at its start and a
+  // scheduling barrier after it; a region may span several pair steps (a
+  // sparse step needs one or two pieces, so the waits are shared).  With
+  // prefetch the pieces of region r+1 are requested at the start of region r.
+  // The budget (Plan::seg_kp, 4) was measured on the n = 40 bench matrix:
+  // 2.33e12 Gray steps/s against 2.27e12 at 2 and 2.04e12 at 1; compile()
   // regenerates with a smaller one if the register allocator runs out.
   // SUP_JIT_PF overrides prefetch (experiments).
-  void emit_step(const std::string& cv_expr, const std::vector<int>& rows, bool full, int c, const char* ind) {
+  struct Item {
+    std::string text;
+    std::vector<int> pieces;
+    int step = -1;  // pair step the item belongs to (-1: none)
+  };
+  std::vector<std::string> pieces;
+  std::map<std::string, int> piece_id;
+  int piece(const std::string& load_expr) {
+    auto it = piece_id.find(load_expr);
+    if (it != piece_id.end()) return it->second;
+    pieces.push_back(load_expr);
+    return piece_id[load_expr] = (int)pieces.size() - 1;
+  }
+  static std::string pref(int pc, int e) { return "$" + std::to_string(pc) + ":" + std::to_string(e) + "$"; }
+
+  // Items of one pair step of class c: the x^0 adds of `rows` (value i of the
+  // table at byte offset expression `off` from `base` for rows[i], or value
+  // rows[i] of a full column, `full`), then the class's statements (row-copy
+  // constants from its stream in jtab).
+  void step_items(std::vector<Item>& out, const std::string& base, const std::string& off,
+                  const std::vector<int>& rows, bool full, int c) {
+    auto col_piece = [&](int pc) {
+      return piece("((cjdbl8*)(" + base + " + " + off + "))[" + std::to_string(pc) + "]");
+    };
+    const int sid = out.empty() ? 0 : out.back().step + 1;
+    for (size_t i = 0; i < rows.size(); ++i) {
+      const int vi = full ? rows[i] : (int)i, pc = col_piece(vi / 8);
+      out.push_back({"x[" + std::to_string(rows[i]) + "] += " + pref(pc, vi % 8) + ";", {pc}, sid});
+    }
+    if (c < P.seg_cc) return;
+    for (const Stmt& st : cls_stmts[c]) {
+      Item it;
+      it.step = sid;
+      const std::string& t = st.text;
+      for (size_t q = 0; q < t.size(); ++q) {
+        if (t[q] != '@') {
+          it.text += t[q];
+          continue;
+        }
+        const size_t e = t.find('@', q + 1);
+        const int idx = std::atoi(t.substr(q + 1, e - q - 1).c_str());
+        const int pc = piece("((cjdbl8*)(jt + " + std::to_string((cbase + kofs[c]) * 8 + (idx / 8) * 64) + "u))[0]");
+        it.text += pref(pc, idx % 8);
+        if (std::find(it.pieces.begin(), it.pieces.end(), pc) == it.pieces.end()) it.pieces.push_back(pc);
+        q = e;
+      }
+      out.push_back(std::move(it));
+    }
+  }
+
+  void emit_items(const std::vector<Item>& items, const char* ind) {
     const int kp = P.seg_kp;
     static const bool pf = std::getenv("SUP_JIT_PF") ? std::atoi(std::getenv("SUP_JIT_PF")) != 0 : true;
-    // SUP_JIT_ASMLD: the loads as inline-asm s_load_dwordx16 (issued where
-    // written; the compiler otherwise sinks them to their pin) and the pin as
-    // an explicit s_waitcnt tied to the pieces
-    static const bool asmld = std::getenv("SUP_JIT_ASMLD") ? std::atoi(std::getenv("SUP_JIT_ASMLD")) != 0 : false;
-    struct Item {
-      std::string text;             // with @i@ (stream) / #i# (column value) placeholders
-      std::vector<int> pieces;      // encoded: column piece p -> p, stream piece p -> 1000 + p
-    };
-    std::vector<Item> items;
-    for (size_t i = 0; i < rows.size(); ++i) {
-      const int vi = full ? rows[i] : (int)i;
-      items.push_back({"x[" + std::to_string(rows[i]) + "] += #" + std::to_string(vi) + "#;", {vi / 8}});
-    }
-    if (c >= P.seg_cc)
-      for (const Stmt& st : cls_stmts[c]) {
-        Item it{st.text, {}};
-        for (size_t q = st.text.find('@'); q != std::string::npos; q = st.text.find('@', st.text.find('@', q + 1) + 1)) {
-          const int pc = 1000 + std::atoi(st.text.c_str() + q + 1) / 8;
-          if (std::find(it.pieces.begin(), it.pieces.end(), pc) == it.pieces.end()) it.pieces.push_back(pc);
-        }
-        items.push_back(std::move(it));
-      }
     if (items.empty()) return;
-    // regions
-    std::vector<std::pair<size_t, size_t>> reg;     // item ranges
-    std::vector<std::vector<int>> rp;                 // their pieces
+    std::vector<std::pair<size_t, size_t>> reg;
+    std::vector<std::vector<int>> rp;
+    // a region takes a following pair step only whole (small sparse steps
+    // share a region; a large step starts its own: measured, n = 40 bench
+    // matrix 2.33e12 per-step against 2.21e12 with regions cut anywhere)
+    auto step_pieces = [&](size_t j, std::vector<int> need) {
+      for (size_t k = j; k < items.size() && (items[k].step == items[j].step || items[k].step < 0); ++k)
+        for (int pc : items[k].pieces)
+          if (std::find(need.begin(), need.end(), pc) == need.end()) need.push_back(pc);
+      return need;
+    };
+    static const bool xstep = std::getenv("SUP_JIT_XSTEP") ? std::atoi(std::getenv("SUP_JIT_XSTEP")) != 0 : true;
     for (size_t i = 0; i < items.size();) {
       std::vector<int> pcs;
       size_t j = i;
       for (; j < items.size(); ++j) {
+        if (j > i && items[j].step >= 0 && items[j].step != items[j - 1].step &&
+            (!xstep || (int)step_pieces(j, pcs).size() > kp))
+          break;
         std::vector<int> need = pcs;
         for (int pc : items[j].pieces)
           if (std::find(need.begin(), need.end(), pc) == need.end()) need.push_back(pc);
@@ -705,34 +746,17 @@ struct Gen {
       rp.push_back(pcs);
       i = j;
     }
-    auto pname = [](size_t r, int pc) {
-      return (pc >= 1000 ? "k" + std::to_string(pc - 1000) : "v" + std::to_string(pc)) + "_" + std::to_string(r);
-    };
+    auto pname = [&](size_t r, int pc) { return "s" + std::to_string(pc) + "_" + std::to_string(r); };
     auto load = [&](size_t r) {
-      for (int pc : rp[r]) {
-        if (asmld) {
-          o << ind << "  jdbl8 " << pname(r, pc) << ";\n";
-          o << ind << "  asm volatile(\"s_load_dwordx16 %0, %1, " << (pc % 1000) * 64 << "\" : \"=s\"(" << pname(r, pc)
-            << ") : \"s\"(" << (pc >= 1000 ? "kvb" : "cvb") << "));\n";
-        } else {
-          o << ind << "  jdbl8 " << pname(r, pc) << " = "
-            << (pc >= 1000 ? "kv[" + std::to_string(pc - 1000) : "cv[" + std::to_string(pc)) << "];\n";
-        }
-      }
+      for (int pc : rp[r]) o << ind << "  jdbl8 " << pname(r, pc) << " = " << pieces[pc] << ";\n";
     };
     auto pin = [&](size_t r) {
       if (rp[r].empty()) return;
-      o << ind << "  asm volatile(\"" << (asmld ? "s_waitcnt lgkmcnt(0)" : "") << "\" :";
+      o << ind << "  asm volatile(\"\" :";
       for (size_t q = 0; q < rp[r].size(); ++q) o << (q ? ", " : " ") << "\"+s\"(" << pname(r, rp[r][q]) << ")";
       o << ");\n";
     };
     o << ind << "{\n";
-    o << ind << "  cjdbl8* cv = (cjdbl8*)" << cv_expr << ";\n";
-    if (asmld) o << ind << "  const uint64_t cvb = (uint64_t)cv;\n";
-    if (c >= P.seg_cc && !cls_stmts[c].empty()) {
-      o << ind << "  cjdbl8* kv = (cjdbl8*)opaque_c(p.jtab, " << (cbase + kofs[c]) * 8 << "u);\n";
-      if (asmld) o << ind << "  const uint64_t kvb = (uint64_t)kv;\n";
-    }
     load(0);
     pin(0);
     for (size_t r = 0; r < reg.size(); ++r) {
@@ -741,13 +765,13 @@ struct Gen {
         const std::string& t = items[i].text;
         std::string out;
         for (size_t q = 0; q < t.size(); ++q) {
-          if (t[q] != '@' && t[q] != '#') {
+          if (t[q] != '$') {
             out += t[q];
             continue;
           }
-          const size_t e = t.find(t[q], q + 1);
-          const int idx = std::atoi(t.substr(q + 1, e - q - 1).c_str());
-          out += pname(r, (t[q] == '@' ? 1000 : 0) + idx / 8) + "[" + std::to_string(idx % 8) + "]";
+          const size_t colon = t.find(':', q + 1), e = t.find('$', q + 1);
+          const int pc = std::atoi(t.substr(q + 1, colon - q - 1).c_str());
+          out += pname(r, pc) + "[" + t.substr(colon + 1, e - colon - 1) + "]";
           q = e;
         }
         o << ind << "  " << out << "\n";
@@ -765,16 +789,10 @@ struct Gen {
   }
 
   // accumulate pair term with cached state S
-  void accumulate(bool neg, uint32_t S, const char* ind) {
+  std::string accumulate_text(bool neg, uint32_t S) const {
     const std::string D = dname(S), U = top(0, 0, S);
-    if (U.empty()) o << ind << "acc " << (neg ? "-= " : "+= ") << D << ";\n";
-    else o << ind << "acc = __builtin_fma(" << (neg ? "-" : "") << D << ", " << U << ", acc);\n";
-  }
-
-  // pair step flipping walk bit k <= seg_b: packed touched values; `off` = byte offset expression
-  void step(int k, const std::string& off, const char* ind) {
-    if (P.touched[k].empty()) return;
-    emit_step("opaque_c(p.jtab, " + off + ")", P.touched[k], false, step_class(k, P.seg_b), ind);
+    if (U.empty()) return std::string("acc ") + (neg ? "-= " : "+= ") + D + ";";
+    return "acc = __builtin_fma(" + std::string(neg ? "-" : "") + D + ", " + U + ", acc);";
   }
 
   std::string off_const(int k, int neg) const {
@@ -904,18 +922,22 @@ struct Gen {
     const char* ind = "        ";
     // pair index j = B*q + s, s = 1 .. B-1: pair bit p = ctz(s) (walk bit p+1);
     // neg = (j >> (p+1)) & 1 = bit p+1 of s for p < b-1, bit 0 of q for p = b-1
-    for (unsigned st = 1; st < B; ++st) {
-      const int pb = __builtin_ctz(st);
-      if (pb < cc) {
-        // cached walk bit: its state's copies are already there
-      } else if (pb < b - 1) {
-        step(pb + 1, off_const(pb + 1, (st >> (pb + 1)) & 1u), ind);
-      } else {
-        o << ind << "{\n" << ind << "  const uint32_t ng = q & 1u;\n";
-        step(pb + 1, off_dyn(pb + 1, "ng"), "          ");
-        o << ind << "}\n";
+    // the 2^b - 1 pair steps of the block as one item stream (regions may
+    // span steps); the top specialised bit's sign is bit 0 of q
+    // one opaque base per iteration: the pieces' loads cannot leave the loop,
+    // and their constant offsets fold into the s_load immediates
+    o << ind << "const char* jt = (const char*)opaque_c(p.jtab, 0u);\n";
+    o << ind << "const uint32_t ng = q & 1u;\n";
+    {
+      std::vector<Item> items;
+      for (unsigned st = 1; st < B; ++st) {
+        const int pb = __builtin_ctz(st), k = pb + 1;
+        if (pb >= cc && !P.touched[k].empty())  // cached walk bits: their state's copies are already there
+          step_items(items, "jt", pb < b - 1 ? off_const(k, (st >> (pb + 1)) & 1u) : off_dyn(k, "ng"),
+                     P.touched[k], false, step_class(k, b));
+        items.push_back({accumulate_text(st & 1u, state(st)), {}});
       }
-      accumulate(st & 1u, state(st), ind);
+      emit_items(items, ind);
     }
     if (Q > 1) {
       // j = B(q+1): pair bit b + ctz(q+1) (walk bit b+1+ctz(q+1)), neg =
@@ -925,11 +947,15 @@ struct Gen {
       // a row is re-formed.  Cached state 0.
       o << ind << "if (q + 1u < " << Q << "u) {\n";
       o << ind << "  const uint32_t kk = (uint32_t)__builtin_ctz(q + 1u);\n";
-      o << ind << "  const uint32_t ng = ((q + 1u) >> (kk + 1u)) & 1u;\n";
-      emit_step("opaque_c(p.cols, (2u * (" + std::to_string(L + b + 1) + "u + kk) + ng) * " +
-                    std::to_string(P.NP * 8) + "u)",
-                P.dyn_rows, true, P.seg_b, "          ");
-      accumulate(false, 0u, "          ");
+      o << ind << "  const uint32_t ngd = ((q + 1u) >> (kk + 1u)) & 1u;\n";
+      {
+        std::vector<Item> items;
+        step_items(items, "(const char*)opaque_c(p.cols, 0u)",
+                   "(2u * (" + std::to_string(L + b + 1) + "u + kk) + ngd) * " + std::to_string(P.NP * 8) + "u",
+                   P.dyn_rows, true, P.seg_b);
+        items.push_back({accumulate_text(false, 0u), {}});
+        emit_items(items, "          ");
+      }
       o << ind << "  tot += acc;\n" << ind << "  acc = 0.0;\n";
       o << ind << "}\n";
     }
