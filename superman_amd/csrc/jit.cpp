@@ -211,8 +211,10 @@ SegFit seg_fit(const SegRows& R, int cc) {
   f.inner = make_tree(irow, R.rsig, R.s_end, R.len0, W);
   const uint32_t ccm = (1u << cc) - 1u;
   uint64_t ops = 0;                        // x 2^b per pair step
+  uint64_t brk[6] = {0, 0, 0, 0, 0, 0};    // x^0 adds, live copies, outer nodes, inner nodes, on-demand, D
   int regs = 6 + R.n;                      // x^0, acc, tot, loop state
   for (int r = 0; r < R.n; ++r) ops += freq(R.rsig[r], R.b, cc);  // x^0 adds
+  brk[0] = ops;
   for (int ti = 0; ti < 2; ++ti) {
     ProdTree& t = ti ? f.inner : f.outer;
     const int nv = ti ? 2 : 1;             // inner: over x and over y
@@ -220,6 +222,7 @@ SegFit seg_fit(const SegRows& R, int cc) {
     for (int j = 0; j < t.K(); ++j) par[t.a[j]] = j, par[t.b[j]] = j;
     for (int i = 0; i < t.K(); ++i) {
       ops += freq(t.sig[i], R.b, cc) * (uint64_t)(copies(t.sig[i], cc) * nv);
+      brk[2 + ti] += freq(t.sig[i], R.b, cc) * (uint64_t)(copies(t.sig[i], cc) * nv);
       const int p = par[t.items() + i];
       if (p < 0 || t.sig[p] != t.sig[i]) regs += copies(t.sig[i], cc) * nv;
     }
@@ -241,16 +244,24 @@ SegFit seg_fit(const SegRows& R, int cc) {
           dem = freq(ps, R.b, cc) * (uint64_t)(v == 0 ? pc - (1 << __builtin_popcount(ps & ~rs & ccm)) : pc);
           keep = dem > live;
         }
-        if (keep) t.item_live[j] |= (uint8_t)(1u << v), ops += live, regs += ncopy;
-        else ops += dem;
+        if (keep) t.item_live[j] |= (uint8_t)(1u << v), ops += live, regs += ncopy, brk[1] += live;
+        else ops += dem, brk[4] += dem;
       }
     }
     if (ti == 1 && t.root() >= 0) {  // D per copy of the inner root
       const uint32_t rs = t.root_sig();
       ops += freq(rs, R.b, cc) * (uint64_t)copies(rs, cc);
+      brk[5] += freq(rs, R.b, cc) * (uint64_t)copies(rs, cc);
       regs += copies(rs, cc);
     }
   }
+  if (const char* e = std::getenv("SUP_JIT_VERBOSE"))
+    if (std::atoi(e) >= 2) {
+      const double sc = 0.5 / (double)(1u << R.b);
+      std::fprintf(stderr, "  seg_fit b=%d cc=%d per Gray step: x0 adds %.2f, live copies %.2f, outer nodes %.2f, "
+                   "inner nodes %.2f, on-demand adds %.2f, D %.2f, fma 0.5\n", R.b, cc, brk[0] * sc, brk[1] * sc,
+                   brk[2] * sc, brk[3] * sc, brk[4] * sc, brk[5] * sc);
+    }
   // + the accumulate fma per pair step; / 2 pair -> Gray steps
   f.ops = ((double)ops / (double)(1u << R.b) + 1.0) / 2.0;
   f.regs = regs;

@@ -16,7 +16,8 @@ import superman_amd as S  # noqa: E402
 
 exact = json.load(open(os.path.join(ROOT, "tests", "golden", "exact_corpus.json")))
 runs = [("plain", "dense_plain", -1, None), ("prefix", "sparse", -1, None), ("seg cc0", "seg", 1, "0"),
-        ("seg cc1", "seg", 1, "1"), ("seg cc2", "seg", 1, "2"), ("skipper", "skip", -1, None)]
+        ("seg cc1", "seg", 1, "1"), ("seg cc2", "seg", 1, "2"), ("seg cc3", "seg", 1, "3"),
+        ("seg (plan)", "seg", 1, None), ("skipper", "skip", -1, None)]
 for name in [k for k in exact if not k.startswith("_")]:
     a = S.read_matrix(os.path.join(ROOT, "tests", "fixtures", name))[0]
     e = Fraction(exact[name])
