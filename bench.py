@@ -7,7 +7,8 @@ matrix double/40_0.50_0 (n = 40, d = 0.5), dense walk (-p4/-p6 path), all
 torch.distributed.run) the 2^h wave-chunks are split into N contiguous
 power-of-two-aligned shards; each rank walks its shard through the C ABI
 (sup_perman_shard) and one RCCL all-reduce (torch.distributed, backend nccl)
-sums the fp64 partials — the only data-path collective.  Total work per
+of a one-slot-per-rank vector, folded pairwise, sums the fp64 partials — the
+only data-path collective; the result is bit-identical to the one-GPU walk.  Total work per
 step is fixed (one permanent), so scaling is "strong".
 
 The walk kernel is the segmented walk specialised for the matrix's pattern
@@ -75,6 +76,33 @@ def shard_chunks(n: int, rank: int, world: int) -> tuple[int, int]:
     L, m, h = S.layout(n)
     C = 1 << h
     return C * rank // world, C * (rank + 1) // world
+
+
+def pairwise(parts):
+    """Pairwise fold in index order (zero-padded to even length at each level):
+    the engine's reduction tree, so power-of-two aligned shards combine to the
+    single-device sum bit for bit."""
+    parts = list(parts)
+    while len(parts) > 1:
+        if len(parts) & 1:
+            parts.append(0.0)
+        parts = [parts[i] + parts[i + 1] for i in range(0, len(parts), 2)]
+    return parts[0]
+
+
+def combine(part: float, rank: int, world: int, device) -> float:
+    """Sum of every rank's shard partial with one all-reduce (RCCL over xGMI on
+    the GPU ranks): a vector with one slot per rank, each rank filling its own,
+    so every slot has a single nonzero addend and the all-reduce is exact in any
+    ring order; then the pairwise fold.  The N-GPU permanent is therefore
+    bit-identical to the one-GPU walk (the scalar all-reduce's own summation
+    order differed from it in the last bits)."""
+    import torch
+    import torch.distributed as dist
+    v = torch.zeros(world, dtype=torch.float64, device=device)
+    v[rank] = part
+    dist.all_reduce(v)  # the single data-path collective
+    return pairwise(v.cpu().tolist())
 
 
 def pmc_record(n: int, kernel: str):
@@ -196,9 +224,7 @@ def main():
             part, st = S.perman_shard(a, rank, world, kernel=kernel, device_id=dev, return_stats=True,
                                       jit=jit)
             if world > 1:
-                t = torch.tensor([part], dtype=torch.float64, device=tdev)
-                dist.all_reduce(t)  # RCCL over xGMI: the single data-path collective
-                part = float(t.item())
+                part = combine(part, rank, world, tdev)  # one RCCL all-reduce over xGMI
             return (4 * (n & 1) - 2) * part, st
 
         for _ in range(args.warmup):

@@ -1,4 +1,4 @@
-"""N > 1 path on CPU: gloo, world_size 2 (and 4) — the bench's shard
+"""N > 1 path on CPU: gloo, world_size 2, 4 and 8 — the bench's shard
 arithmetic and its single all-reduce reproduce the 1-device sum bit for bit.
 Each rank's shard is walked by the oracle's mirror of the engine schedule (the
 CPU stand-in for the GPU kernel, which is bit-identical to it)."""
@@ -36,16 +36,15 @@ def _worker(rank, world, port, mat, q):
     info = S.plan_info(mat, "dense")  # the plan sup_perman_shard runs
     part, _ = oracle.engine_range(mat, info["kind"], c0, c1, info["L"], info["m"], info["colmap"], 1,
                                   info["cached"], info["pair_bits"])
-    t = torch.tensor([part], dtype=torch.float64)
-    dist.all_reduce(t)
+    total = bench.combine(part, rank, world, "cpu")
     el = torch.tensor([float(rank)], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     if rank == 0:
-        q.put(((4 * (n & 1) - 2) * float(t.item()), float(el.item()), (c0, c1)))
+        q.put(((4 * (n & 1) - 2) * total, float(el.item()), (c0, c1)))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_allreduce_matches_single(world, orc):
     n = 22
     mat = np.random.default_rng(5).random((n, n))
@@ -63,12 +62,9 @@ def test_sharded_allreduce_matches_single(world, orc):
     assert max_rank == world - 1
     import superman_amd as S
     want = orc.engine_perman_as(S, mat, "dense", threads=2)
-    if world == 2:
-        assert got == want  # bitwise: the two shards are the two top subtrees
-    else:
-        # the all-reduce's own summation order (ring / halving-doubling) differs
-        # from the pairwise tree only in the last combine steps: ulp level
-        assert abs(got - want) <= 4e-16 * world * abs(want)
+    # bitwise: the shards are the top subtrees of the engine's pairwise tree,
+    # the one-slot-per-rank all-reduce is exact and the fold is that tree's top
+    assert got == want
 
 
 def test_shard_chunks_cover_space():
@@ -82,3 +78,11 @@ def test_shard_chunks_cover_space():
             assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
             if world in (1, 2, 4, 8) and (1 << h) >= world:
                 assert all((c1 - c0) == (1 << h) // world for c0, c1 in b)
+
+
+def test_pairwise_fold_is_engine_tree():
+    import bench
+    v = np.random.default_rng(1).random(8).tolist()
+    assert bench.pairwise(v) == ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]))
+    assert bench.pairwise(v[:3]) == (v[0] + v[1]) + (v[2] + 0.0)
+    assert bench.pairwise([2.5]) == 2.5
