@@ -255,10 +255,11 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
 // fp64 VALU lane-ops per second of one MI355X on the walk kernels (measured:
 // 46.6 ops/step at 7.98e11 steps/s on the n=40 bench), for jit's auto mode.
 static constexpr double kLaneOpsPerSec = 3.7e13;
-// Compile + load of a specialised kernel is 0.15-0.2 s on the MI355X box's
-// host (profiles/r1/probe_seg.log; 0 when the disk cache holds it); auto mode
-// specialises when the predicted walk time saved is clearly larger.
-static constexpr double kJitMinSavingSec = 0.3;
+// The segmented walk's plan (walk-order searches, 0.1-1 s at n = 30-44) and
+// compile + load (0.4-0.7 s with hiprtc; 0 when the disk cache holds it) are
+// paid once per matrix; auto mode specialises when the predicted walk time
+// saved is larger than both.
+static constexpr double kJitMinSavingSec = 1.0;
 
 static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit,
                              int ndev, int dev);
@@ -354,10 +355,13 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
       if (rc || jit < 0 || n < 10 || lay.m < 3) return rc;
       bool integral = true;
       for (size_t i = 0; i < (size_t)n * n && integral; ++i) integral = A[i] == std::floor(A[i]);
-      Plan s;
-      if (make_seg(s) != SUP_OK) return SUP_OK;
       const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
       double skip_cost = walk_cost(P) / (integral ? kSkipEfficiency : 1.0);  // f <= 1
+      // auto mode: no segmented plan (its search takes ~0.1-1 s) where even a
+      // free walk could not save the compile
+      if (jit < 1 && steps * skip_cost / kLaneOpsPerSec < kJitMinSavingSec) return SUP_OK;
+      Plan s;
+      if (make_seg(s) != SUP_OK) return SUP_OK;
       if (walk_cost(s) >= skip_cost) return SUP_OK;
       if (jit < 1 && steps * (skip_cost - walk_cost(s)) / kLaneOpsPerSec < kJitMinSavingSec) return SUP_OK;
       if (integral) {
@@ -392,7 +396,9 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
     Plan c;
     if (make_plan(A, n, kinds[i], false, lay, c) == SUP_OK && walk_cost(c) < walk_cost(best)) best = std::move(c);
   }
-  if (jit >= 0 && n >= 8 && lay.m >= 3) {
+  const bool may_save = std::ldexp(1.0, n - 1) / std::max(ndev, 1) * walk_cost(best) / kLaneOpsPerSec >=
+                        kJitMinSavingSec;  // auto mode: skip the segmented plan's search where it cannot pay
+  if (jit >= 0 && n >= 8 && lay.m >= 3 && (jit >= 1 || may_save)) {
     Plan s;
     if (make_seg(s) == SUP_OK && walk_cost(s) < walk_cost(best)) {
       const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);

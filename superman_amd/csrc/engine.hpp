@@ -49,10 +49,11 @@ struct ProdTree {
   int tail_lo = 0, tail_hi = 0;
   std::vector<int> a, b;
   std::vector<uint32_t> sig;
-  // per item (segmented walk's row copies, jit.cpp seg_fit): bit 0 = the
-  // copies over x are kept live, bit 1 = the copies over y (inner tree) are;
-  // otherwise they are formed on demand when the parent node is re-formed
-  std::vector<uint8_t> item_live;
+  // storage plan (segmented walk, jit.cpp seg_fit), per item and per node:
+  // bit 0 = its copies over x are kept live, bit 1 = its copies over y (inner
+  // tree); otherwise they are formed on demand inside the nearest live
+  // ancestor (the value is the same either way)
+  std::vector<uint8_t> item_live, node_live;
   int items() const { return (int)item_row.size(); }
   int K() const { return (int)a.size(); }
   int root() const { return K() ? items() + K() - 1 : (items() ? 0 : -1); }

@@ -187,20 +187,32 @@ inline uint64_t freq(uint32_t s, int b, int cc) {
   return v;
 }
 
-// Trees, cost, live values and the live/on-demand choice of every row copy
-// with cc cached classes.
+// Live-value budgets (seg_fit's estimate, doubles): <= kRegs3 fits 3 waves
+// per SIMD (168 VGPRs), <= kRegsMax fits 2 (256 VGPRs) without spills.  The
+// estimate runs ~10% above what the compiler allocates (n = 40 bench matrix:
+// 102 -> 188 VGPRs, 142 -> 246 VGPRs no spill, 205 -> 175 spilled VGPRs).
+// Occupancy 2 costs ~2% against 3 on this walk (measured, n = 40), 1 ~35%.
+constexpr int kRegs3 = 90;
+static const int kRegsMax = std::getenv("SUP_JIT_REGMAX") ? std::atoi(std::getenv("SUP_JIT_REGMAX")) : 142;
+constexpr double kOcc2Penalty = 1.02;
+
+// Trees, cost, live values and the storage plan of every value, with cc
+// cached classes, fitted to `budget` live values.
 //
-// Row copies.  Only x^0 (the lane state with walk bits 0..cc clear) is walked;
-// every other value of row r is a pure function of it: the copy for cached
-// state S is x^S_r = x^0_r + cx_r[S] (x^0_r itself when no bit of S touches
-// r) and its walk-bit-0 twin y^S_r = x^0_r + cy_r[S] (seg_consts).  A copy is
-// either kept live (re-formed when x^0_r changes) or formed on demand when its
-// parent node is re-formed: the same value either way, so the choice is free
-// of numerical effect.  On demand costs nothing extra when the parent is
-// re-formed exactly as often as the row changes (the tree joins rows of equal
-// step classes first) and frees the register; it is taken whenever it costs
-// no more ops than keeping the copy.
-SegFit seg_fit(const SegRows& R, int cc) {
+// Values.  Only x^0 (the lane state with walk bits 0..cc clear) is walked;
+// every other value is a pure function of it: the copy of row r for cached
+// state S is x^S_r = x^0_r + cx_r[S] (x^0_r when no bit of S touches r), its
+// walk-bit-0 twin y^S_r = x^0_r + cy_r[S] (seg_cx / seg_cy), and a tree node
+// copy is the product of its children's copies.  Each row copy and node copy
+// set (per tree and variant x / y) is either live — formed on the steps of
+// its own classes and kept — or formed on demand inside its nearest live
+// ancestor (D for segment 0's roots).  The choice changes no value (the same
+// operations on the same operands), only ops and registers: starting from all
+// live (segment 0's roots excepted: D reads them once), values are dropped
+// greedily by ops added per register freed — first every one that adds
+// nothing (a parent formed exactly when the child is: the tree joins equal
+// step classes first), then the cheapest until the live values fit `budget`.
+SegFit seg_fit(const SegRows& R, int cc, int budget, int budget_hi = -1, SegFit* fit_hi = nullptr) {
   SegFit f;
   f.cc = cc;
   const ClassWeights W(R.b, cc);
@@ -209,83 +221,143 @@ SegFit seg_fit(const SegRows& R, int cc) {
   for (int r = 0; r < R.s_end; ++r) irow.push_back(r);
   f.outer = make_tree(orow, R.rsig, R.r_end, R.n, W);
   f.inner = make_tree(irow, R.rsig, R.s_end, R.len0, W);
-  const uint32_t ccm = (1u << cc) - 1u;
-  uint64_t ops = 0;                        // x 2^b per pair step
-  uint64_t brk[6] = {0, 0, 0, 0, 0, 0};    // x^0 adds, live copies, outer nodes, inner nodes, on-demand, D
-  int regs = 6 + R.n;                      // x^0, acc, tot, loop state
-  for (int r = 0; r < R.n; ++r) ops += freq(R.rsig[r], R.b, cc);  // x^0 adds
-  brk[0] = ops;
-  for (int ti = 0; ti < 2; ++ti) {
-    ProdTree& t = ti ? f.inner : f.outer;
-    const int nv = ti ? 2 : 1;             // inner: over x and over y
-    std::vector<int> par(t.items() + t.K(), -1);
-    for (int j = 0; j < t.K(); ++j) par[t.a[j]] = j, par[t.b[j]] = j;
-    for (int i = 0; i < t.K(); ++i) {
-      ops += freq(t.sig[i], R.b, cc) * (uint64_t)(copies(t.sig[i], cc) * nv);
-      brk[2 + ti] += freq(t.sig[i], R.b, cc) * (uint64_t)(copies(t.sig[i], cc) * nv);
-      const int p = par[t.items() + i];
-      if (p < 0 || t.sig[p] != t.sig[i]) regs += copies(t.sig[i], cc) * nv;
-    }
-    t.item_live.assign(t.items(), 0);
-    for (int j = 0; j < t.items(); ++j) {
-      const int r = t.item_row[j];
-      if (r < 0) continue;
-      const uint32_t rs = R.rsig[r];
-      for (int v = 0; v < nv; ++v) {
-        const int own = copies(rs, cc), ncopy = v == 0 ? own - 1 : own;  // copies other than x^0
-        if (ncopy == 0) continue;
-        const uint64_t live = freq(rs, R.b, cc) * (uint64_t)ncopy;
-        const int p = par[j];
-        bool keep = p < 0;  // a root row stays live (read by every accumulate)
-        uint64_t dem = 0;
-        if (!keep) {
-          const uint32_t ps = t.sig[p];
-          const int pc = copies(ps, cc);
-          dem = freq(ps, R.b, cc) * (uint64_t)(v == 0 ? pc - (1 << __builtin_popcount(ps & ~rs & ccm)) : pc);
-          keep = dem > live;
-        }
-        if (keep) t.item_live[j] |= (uint8_t)(1u << v), ops += live, regs += ncopy, brk[1] += live;
-        else ops += dem, brk[4] += dem;
+  struct Val {
+    int parent = -1;            // parent value (-1: a root)
+    int kids[2] = {-1, -1};
+    double fr = 0;              // formations per 2^b pair steps
+    int cop = 1;                // copies
+    double own = 0;             // own ops to form all copies
+    int store = 0;              // registers if live
+    bool live = true, fixed = false;
+    double F = 0;               // ops to form all copies, non-live descendants included
+  };
+  std::vector<Val> V;
+  // values of tree t over x (yv = false) or y; returns the index of item 0
+  auto add_tree = [&](const ProdTree& t, bool yv, bool outer) {
+    const int base = (int)V.size();
+    for (int id = 0; id < t.items() + t.K(); ++id) {
+      Val v;
+      uint32_t sig;
+      if (id < t.items()) {
+        const int r = t.item_row[id];
+        sig = r < 0 ? 0u : R.rsig[r];
+        v.cop = copies(sig, cc);
+        v.store = r < 0 ? 0 : (yv ? v.cop : v.cop - 1);  // x^0 itself needs no copy
+        v.own = v.store;
+        v.fixed = v.store == 0;
+      } else {
+        const int i = id - t.items();
+        sig = t.sig[i];
+        v.cop = copies(sig, cc);
+        v.own = v.store = v.cop;
+        v.kids[0] = base + t.a[i], v.kids[1] = base + t.b[i];
       }
+      v.fr = (double)freq(sig, R.b, cc);
+      V.push_back(v);
     }
-    if (ti == 1 && t.root() >= 0) {  // D per copy of the inner root
-      const uint32_t rs = t.root_sig();
-      ops += freq(rs, R.b, cc) * (uint64_t)copies(rs, cc);
-      brk[5] += freq(rs, R.b, cc) * (uint64_t)copies(rs, cc);
-      regs += copies(rs, cc);
+    for (int i = 0; i < t.K(); ++i) V[base + t.a[i]].parent = V[base + t.b[i]].parent = base + t.items() + i;
+    if (t.root() >= 0) {
+      Val& rt = V[base + t.root()];
+      if (outer) rt.fixed = true;           // the outer root: read by every accumulate
+      else if (!rt.fixed) rt.live = false;  // segment 0's roots: read by D only
     }
+    return base;
+  };
+  const int bo = add_tree(f.outer, false, true), bx = add_tree(f.inner, false, false),
+            by = add_tree(f.inner, true, false);
+  const uint32_t dsig = f.inner.root() >= 0 ? f.inner.root_sig() : 0u;
+  const double fD = (double)freq(dsig, R.b, cc);
+  const int cD = copies(dsig, cc);
+  double xadds = 0;
+  for (int r = 0; r < R.n; ++r) xadds += (double)freq(R.rsig[r], R.b, cc);
+  auto total = [&](int* regs) {
+    for (auto& v : V) {  // children precede parents
+      v.F = v.own;
+      for (int k : v.kids)
+        if (k >= 0 && !V[k].live) v.F += (double)v.cop / V[k].cop * V[k].F;
+    }
+    double ops = xadds;
+    int rg = 6 + R.n;  // x^0, acc, tot, loop state
+    for (auto& v : V)
+      if (v.live) ops += v.fr * v.F, rg += v.store;
+    if (f.inner.root() >= 0) {  // D per copy: the sub and its non-live tops
+      ops += fD * cD;
+      for (int rt : {bx + f.inner.root(), by + f.inner.root()})
+        if (!V[rt].live) ops += fD * (double)cD / V[rt].cop * V[rt].F;
+      rg += cD;
+    }
+    *regs = rg;
+    return ops;
+  };
+  // values formed exactly as often as their parent (same step classes, same
+  // copies) cost nothing on demand: all at once (a chain of them keeps the
+  // property up to its nearest live ancestor)
+  for (auto& v : V)
+    if (v.live && !v.fixed && v.parent >= 0 && V[v.parent].fr * V[v.parent].cop == v.fr * v.cop) v.live = false;
+  for (const int rt : {bx + f.inner.root(), by + f.inner.root()})
+    if (f.inner.root() >= 0)
+      for (int k : V[rt].kids)  // children of segment 0's roots: consumer D
+        if (k >= 0 && V[k].live && !V[k].fixed && fD * cD == V[k].fr * V[k].cop) V[k].live = false;
+  int regs = 0;
+  double ops = total(&regs);
+  // the decisions: bit 0 over x, bit 1 over y
+  auto out = [&](SegFit& g, double ops_now, int regs_now) {
+    g.cc = cc;
+    g.outer = f.outer, g.inner = f.inner;
+    auto put = [&](ProdTree& t, int base, int bit) {
+      t.item_live.assign(t.items(), 0);
+      t.node_live.assign(t.K(), 0);
+      for (int j = 0; j < t.items(); ++j)
+        if (V[base + j].live && !V[base + j].fixed) t.item_live[j] |= (uint8_t)(1u << bit);
+      for (int i = 0; i < t.K(); ++i)
+        if (V[base + t.items() + i].live) t.node_live[i] |= (uint8_t)(1u << bit);
+    };
+    put(g.outer, bo, 0);
+    put(g.inner, bx, 0);
+    for (int j = 0; j < g.inner.items(); ++j)
+      if (V[by + j].live && !V[by + j].fixed) g.inner.item_live[j] |= 2u;
+    for (int i = 0; i < g.inner.K(); ++i)
+      if (V[by + g.inner.items() + i].live) g.inner.node_live[i] |= 2u;
+    g.ops = (ops_now / (double)(1u << R.b) + 1.0) / 2.0;  // + the accumulate fma; pair -> Gray steps
+    g.regs = regs_now;
+  };
+  bool took_hi = fit_hi == nullptr;
+  for (;;) {
+    int best = -1;
+    double bratio = 1e300, bd = 0;
+    for (int i = 0; i < (int)V.size(); ++i) {
+      const Val& v = V[i];
+      if (!v.live || v.fixed) continue;
+      int a = v.parent;
+      while (a >= 0 && !V[a].live) a = V[a].parent;
+      const double fa = a >= 0 ? V[a].fr : fD, ca = a >= 0 ? V[a].cop : cD;
+      const double d = v.F * (fa * ca / v.cop - v.fr);
+      if (d / v.store < bratio) bratio = d / v.store, best = i, bd = d;
+    }
+    // the larger budget's plan is the state where its greedy would stop
+    if (!took_hi && (best < 0 || (bd > 1e-9 && regs <= budget_hi))) out(*fit_hi, ops, regs), took_hi = true;
+    if (best < 0 || (bd > 1e-9 && regs <= budget)) break;
+    V[best].live = false;
+    ops = total(&regs);
   }
-  if (const char* e = std::getenv("SUP_JIT_VERBOSE"))
-    if (std::atoi(e) >= 2) {
-      const double sc = 0.5 / (double)(1u << R.b);
-      std::fprintf(stderr, "  seg_fit b=%d cc=%d per Gray step: x0 adds %.2f, live copies %.2f, outer nodes %.2f, "
-                   "inner nodes %.2f, on-demand adds %.2f, D %.2f, fma 0.5\n", R.b, cc, brk[0] * sc, brk[1] * sc,
-                   brk[2] * sc, brk[3] * sc, brk[4] * sc, brk[5] * sc);
-    }
-  // + the accumulate fma per pair step; / 2 pair -> Gray steps
-  f.ops = ((double)ops / (double)(1u << R.b) + 1.0) / 2.0;
-  f.regs = regs;
+  if (!took_hi) out(*fit_hi, ops, regs);
+  out(f, ops, regs);
   return f;
 }
-
-// Live-value budgets (seg_fit's estimate, doubles): <= kRegs3 fits 3 waves
-// per SIMD (168 VGPRs), <= kRegsMax fits 2 (256 VGPRs) without spills.  The
-// estimate runs ~10% above what the compiler allocates (n = 40 bench matrix:
-// 102 -> 188 VGPRs, 142 -> 246 VGPRs no spill, 205 -> 175 spilled VGPRs).
-// Occupancy 2 costs ~2% against 3 on this walk (measured, n = 40), 1 ~35%.
-constexpr int kRegs3 = 90, kRegsMax = 142;
-constexpr double kOcc2Penalty = 1.02;
 
 // Best number of cached classes (0 .. min(kMaxCachedBits, b-1)) within the
 // register budget.
 SegFit seg_best(const SegRows& R, int cc_max = kMaxCachedBits) {
-  SegFit best = seg_fit(R, 0);
-  double bscore = best.ops * (best.regs <= kRegs3 ? 1.0 : kOcc2Penalty);
-  for (int cc = 1; cc <= std::min(cc_max, R.b - 1); ++cc) {
-    SegFit f = seg_fit(R, cc);
-    if (f.regs > kRegsMax) continue;
-    const double score = f.ops * (f.regs <= kRegs3 ? 1.0 : kOcc2Penalty);
-    if (score < bscore) bscore = score, best = std::move(f);
+  SegFit best;
+  double bscore = 1e300;
+  for (int cc = 0; cc <= std::min(cc_max, std::max(0, R.b - 1)); ++cc) {
+    SegFit hi;
+    SegFit lo = seg_fit(R, cc, kRegs3, kRegsMax, &hi);  // one greedy: both budgets' plans
+    for (SegFit* f : {&lo, &hi}) {
+      if (f->regs > kRegsMax && cc > 0) continue;
+      const double score = f->ops * (f->regs <= kRegs3 ? 1.0 : kOcc2Penalty) * (f->regs > kRegsMax ? 2.0 : 1.0);
+      if (score < bscore) bscore = score, best = std::move(*f);
+    }
   }
   return best;
 }
@@ -355,6 +427,12 @@ int seg_static_bits(int m) {
 
 double seg_walk_cost(const Plan& P) { return P.seg_ops; }
 
+// Greedy starts the walk-order descent runs from (SUP_JIT_STARTS overrides).
+int seg_search_starts() {
+  if (const char* e = std::getenv("SUP_JIT_STARTS")) return std::max(1, std::atoi(e));
+  return 3;
+}
+
 std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b_out) {
   const int nb = n - 1;
   m = std::min(m, nb);
@@ -403,30 +481,42 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
   std::vector<double> bcosts(cands.size(), 1e300);
   auto search = [&](size_t ci) {
     const int b = cands[ci];
-    std::vector<int> best;
-    double bcost = 1e300;
+    // greedy continuations from every first column, the few cheapest kept
+    std::vector<std::pair<double, std::vector<int>>> starts;
     for (int f = 0; f < nb; ++f) {
       std::vector<int> o = extend({f}, m);
-      const double c = cost(o, b);
-      if (c < bcost || best.empty()) bcost = c, best = o;
+      starts.push_back({cost(o, b), std::move(o)});
     }
-    // descent: swap a walk position with another walk position or an unused
-    // column while the cost drops (positions whose weight 2^-(k+1) is visible)
-    const int hot = std::getenv("SUP_JIT_HOT") ? std::min(m, std::atoi(std::getenv("SUP_JIT_HOT"))) : std::min(m, 12);
-    for (int pass = 0; pass < 8 && bcost < 1e300; ++pass) {
-      bool improved = false;
-      for (int a = 0; a < hot; ++a) {
-        for (int c = 0; c < nb; ++c) {
-          if (c == best[a]) continue;
-          std::vector<int> o = best;
-          auto it = std::find(o.begin(), o.end(), c);
-          if (it != o.end()) std::swap(o[a], *it);
-          else o[a] = c;
-          const double v = cost(o, b);
-          if (v < bcost - 1e-12) bcost = v, best = o, improved = true;
+    std::stable_sort(starts.begin(), starts.end(),
+                     [](const std::pair<double, std::vector<int>>& x, const std::pair<double, std::vector<int>>& y) {
+                       return x.first < y.first;
+                     });
+    // descent from each: swap a walk position with another walk position or
+    // an unused column while the cost drops (positions whose weight 2^-(k+1)
+    // is visible); the best result wins
+    const int hot = std::min(m, 12);
+    std::vector<int> best;
+    double bcost = 1e300;
+    const size_t nstart = std::min(starts.size(), (size_t)seg_search_starts());
+    for (size_t si = 0; si < nstart; ++si) {
+      std::vector<int> cur = starts[si].second;
+      double ccost = starts[si].first;
+      for (int pass = 0; pass < 8 && ccost < 1e300; ++pass) {
+        bool improved = false;
+        for (int a = 0; a < hot; ++a) {
+          for (int c = 0; c < nb; ++c) {
+            if (c == cur[a]) continue;
+            std::vector<int> o = cur;
+            auto it = std::find(o.begin(), o.end(), c);
+            if (it != o.end()) std::swap(o[a], *it);
+            else o[a] = c;
+            const double v = cost(o, b);
+            if (v < ccost - 1e-12) ccost = v, cur = o, improved = true;
+          }
         }
+        if (!improved) break;
       }
-      if (!improved) break;
+      if (best.empty() || ccost < bcost - 1e-12) bcost = ccost, best = cur;
     }
     if (const char* e = std::getenv("SUP_JIT_ANNEAL")) {  // experiment: simulated annealing on the order
       const int iters = std::atoi(e);
@@ -609,8 +699,15 @@ struct Gen {
       return "(x[" + std::to_string(r) + "] + @" + std::to_string(ks->size() - 1) + "@)";
     }
     const int i = id - t.items();
+    if (ks && !nlive(ti, v, i)) return "(" + node(ti, v, i, S, ks) + ")";  // formed on demand
     const char* N = ti == 0 ? "o" : (v ? "py" : "px");
     return N + std::to_string(i) + "_" + std::to_string(S & t.sig[i] & ccm);
+  }
+  bool nlive(int ti, int v, int i) const { return (tr(ti).node_live[i] >> v) & 1u; }
+  // node i's variable name for copy S (chunk start and live nodes)
+  std::string nname(int ti, int v, int i, uint32_t S) const {
+    const char* N = ti == 0 ? "o" : (v ? "py" : "px");
+    return N + std::to_string(i) + "_" + std::to_string(S & tr(ti).sig[i] & ccm);
   }
   uint32_t csig(int ti, int id) const {
     const ProdTree& t = tr(ti);
@@ -646,18 +743,17 @@ struct Gen {
     auto upd = [&](int ti, int v) {
       const ProdTree& t = tr(ti);
       for (int i = 0; i < t.K(); ++i)
-        if ((t.sig[i] >> c) & 1u)
-          for (uint32_t S : submasks(t.sig[i] & ccm)) {
-            const std::string lhs = opnd(ti, v, t.items() + i, S, nullptr);
-            st.push_back({lhs + " = " + node(ti, v, i, S, &ks) + ";"});
-          }
+        if (((t.sig[i] >> c) & 1u) && nlive(ti, v, i))
+          for (uint32_t S : submasks(t.sig[i] & ccm))
+            st.push_back({nname(ti, v, i, S) + " = " + node(ti, v, i, S, &ks) + ";"});
     };
     upd(0, 0);
     if ((P.inner_tree.root_sig() >> c) & 1u) {
       upd(1, 0);
       upd(1, 1);
+      const int rt = P.inner_tree.root();
       for (uint32_t S : submasks(inner_root_csig()))
-        st.push_back({dname(S) + " = " + top(1, 0, S) + " - " + top(1, 1, S) + ";"});
+        st.push_back({dname(S) + " = " + opnd(1, 0, rt, S, &ks) + " - " + opnd(1, 1, rt, S, &ks) + ";"});
     }
   }
 
@@ -1077,7 +1173,7 @@ int build_seg(Plan& P) {
     seg_rows_finish(R, P.seg_b);
     SegFit f;
     if (const char* e = std::getenv("SUP_JIT_CC"))
-      f = seg_fit(R, std::max(0, std::min({std::atoi(e), R.b - 1, kMaxCachedBits})));
+      f = seg_fit(R, std::max(0, std::min({std::atoi(e), R.b - 1, kMaxCachedBits})), kRegsMax);
     else f = seg_best(R);
     P.outer_tree = std::move(f.outer);
     P.inner_tree = std::move(f.inner);
