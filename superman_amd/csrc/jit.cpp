@@ -60,6 +60,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -188,12 +189,17 @@ inline uint64_t freq(uint32_t s, int b, int cc) {
 }
 
 // Live-value budgets (seg_fit's estimate, doubles): <= kRegs3 fits 3 waves
-// per SIMD (168 VGPRs), <= kRegsMax fits 2 (256 VGPRs) without spills.  The
-// estimate runs ~10% above what the compiler allocates (n = 40 bench matrix:
+// per SIMD (168 VGPRs), <= kRegsMax fits 2 (256 VGPRs) without spills in the
+// walk loop.  The estimate runs above what the compiler allocates (round 1:
 // 102 -> 188 VGPRs, 142 -> 246 VGPRs no spill, 205 -> 175 spilled VGPRs).
 // Occupancy 2 costs ~2% against 3 on this walk (measured, n = 40), 1 ~35%.
 constexpr int kRegs3 = 90;
-static const int kRegsMax = std::getenv("SUP_JIT_REGMAX") ? std::atoi(std::getenv("SUP_JIT_REGMAX")) : 142;
+// Calibrated against the compiler (round 2, storage plans): at an estimate of
+// 170 no walk loop spills VGPRs on the bench matrix or on random n = 30-64
+// matrices of density 0.1-0.9 (scratch traffic only in the chunk start); at
+// 180-200 some do.  On the bench matrix (MI355X): 142 -> 2.55e12, 160 ->
+// 2.80e12, 180 -> 2.81e12 Gray steps/s.  SUP_JIT_REGMAX overrides (experiments).
+static const int kRegsMax = std::getenv("SUP_JIT_REGMAX") ? std::atoi(std::getenv("SUP_JIT_REGMAX")) : 170;
 constexpr double kOcc2Penalty = 1.02;
 
 // Trees, cost, live values and the storage plan of every value, with cc
@@ -322,14 +328,18 @@ SegFit seg_fit(const SegRows& R, int cc, int budget, int budget_hi = -1, SegFit*
     g.regs = regs_now;
   };
   bool took_hi = fit_hi == nullptr;
+  std::vector<int> anc(V.size(), -1);  // nearest live ancestor
   for (;;) {
+    for (int i = (int)V.size() - 1; i >= 0; --i) {  // parents follow their children
+      const int p = V[i].parent;
+      anc[i] = p < 0 ? -1 : (V[p].live ? p : anc[p]);
+    }
     int best = -1;
     double bratio = 1e300, bd = 0;
     for (int i = 0; i < (int)V.size(); ++i) {
       const Val& v = V[i];
       if (!v.live || v.fixed) continue;
-      int a = v.parent;
-      while (a >= 0 && !V[a].live) a = V[a].parent;
+      const int a = anc[i];
       const double fa = a >= 0 ? V[a].fr : fD, ca = a >= 0 ? V[a].cop : cD;
       const double d = v.F * (fa * ca / v.cop - v.fr);
       if (d / v.store < bratio) bratio = d / v.store, best = i, bd = d;
@@ -347,7 +357,9 @@ SegFit seg_fit(const SegRows& R, int cc, int budget, int budget_hi = -1, SegFit*
 
 // Best number of cached classes (0 .. min(kMaxCachedBits, b-1)) within the
 // register budget.
+std::atomic<long> g_fit_calls{0};  // planning effort (SUP_JIT_VERBOSE)
 SegFit seg_best(const SegRows& R, int cc_max = kMaxCachedBits) {
+  ++g_fit_calls;
   SegFit best;
   double bscore = 1e300;
   for (int cc = 0; cc <= std::min(cc_max, std::max(0, R.b - 1)); ++cc) {
@@ -1181,8 +1193,8 @@ int build_seg(Plan& P) {
     P.seg_ops = f.ops;
     P.seg_regs = f.regs;
     if (std::getenv("SUP_JIT_VERBOSE"))
-      std::fprintf(stderr, "seg plan n=%d m=%d b=%d ops/step=%.4f regs=%d cc=%d\n", n, m, P.seg_b, f.ops, f.regs,
-                   f.cc);
+      std::fprintf(stderr, "seg plan n=%d m=%d b=%d ops/step=%.4f regs=%d cc=%d (storage plans evaluated: %ld)\n", n,
+                   m, P.seg_b, f.ops, f.regs, f.cc, g_fit_calls.load());
   }
   P.jofs.assign(m, 0);
   P.jtab.clear();
