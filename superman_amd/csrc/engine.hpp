@@ -116,6 +116,10 @@ std::vector<int> greedy_walk_order(const double* A, int n, int count);
 // then pairwise-swap descent on seg_cost (first `count` columns returned).
 // *b_out = the specialised pair bits the order was chosen for (seg_b).
 std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b_out);
+// Sampled fraction of wave-chunks the segmented kernel skips (walk-untouched
+// rows exactly zero in every lane) for an extended walk order (m walk
+// columns, then the lane columns); integer matrices.
+double seg_skip_estimate(const double* A, int n, const std::vector<int>& order, int m, int samples);
 // Engine row order of the segmented walk for walk columns `walk`: rows in
 // first-touch order, segment 0 (the rows of walk[0]) internally ordered by
 // first touch among walk[1..], its rows no other walk column touches last.

@@ -158,7 +158,7 @@ def test_seg_chunk_skip_gpu(sup, orc, n, d, seed):
     got, st = sup.perman(a, algo=4, kernel="seg", return_stats=True)
     assert st["walk_kind"] == 3
     assert got == sup.perman_cpu(a, "seg", threads=8) == orc.engine_perman_as(sup, a, "seg", threads=8)
-    assert rel(got, float(orc.exact_perman_crt(a))) < 1e-13
+    assert rel(got, float(orc.exact_perman_crt(a))) < 1e-12
 
 
 def test_seg_shared_steps_and_lane_fold_gpu(sup, orc):
