@@ -66,6 +66,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <queue>
 #include <memory>
 #include <mutex>
 #include <sstream>
@@ -328,27 +329,58 @@ SegFit seg_fit(const SegRows& R, int cc, int budget, int budget_hi = -1, SegFit*
     g.regs = regs_now;
   };
   bool took_hi = fit_hi == nullptr;
-  std::vector<int> anc(V.size(), -1);  // nearest live ancestor
+  // Greedy with a lazy heap: removing V changes only the F of its ancestors
+  // up to its nearest live ancestor A (A's own entry) and the consumer of the
+  // live values nearest below V (now A): only those entries are renewed.
+  auto nearest_live = [&](int i) {
+    int a = V[i].parent;
+    while (a >= 0 && !V[a].live) a = V[a].parent;
+    return a;
+  };
+  auto delta = [&](int i) {
+    const int a = nearest_live(i);
+    const double fa = a >= 0 ? V[a].fr : fD, ca = a >= 0 ? V[a].cop : cD;
+    return V[i].F * (fa * ca / V[i].cop - V[i].fr);
+  };
+  typedef std::tuple<double, int, int> Entry;  // (ops added per register, value, version)
+  std::priority_queue<Entry, std::vector<Entry>, std::greater<Entry>> heap;
+  std::vector<int> ver(V.size(), 0);
+  std::vector<double> dlt(V.size(), 0.0);
+  auto push = [&](int i) {
+    if (!V[i].live || V[i].fixed) return;
+    dlt[i] = delta(i);
+    heap.push(Entry{dlt[i] / V[i].store, i, ++ver[i]});
+  };
+  for (int i = 0; i < (int)V.size(); ++i) push(i);
+  std::vector<int> stack;
   for (;;) {
-    for (int i = (int)V.size() - 1; i >= 0; --i) {  // parents follow their children
-      const int p = V[i].parent;
-      anc[i] = p < 0 ? -1 : (V[p].live ? p : anc[p]);
-    }
-    int best = -1;
-    double bratio = 1e300, bd = 0;
-    for (int i = 0; i < (int)V.size(); ++i) {
-      const Val& v = V[i];
-      if (!v.live || v.fixed) continue;
-      const int a = anc[i];
-      const double fa = a >= 0 ? V[a].fr : fD, ca = a >= 0 ? V[a].cop : cD;
-      const double d = v.F * (fa * ca / v.cop - v.fr);
-      if (d / v.store < bratio) bratio = d / v.store, best = i, bd = d;
-    }
+    while (!heap.empty() && std::get<2>(heap.top()) != ver[std::get<1>(heap.top())]) heap.pop();  // stale
+    const int best = heap.empty() ? -1 : std::get<1>(heap.top());
+    const double bd = best < 0 ? 0.0 : dlt[best];
     // the larger budget's plan is the state where its greedy would stop
     if (!took_hi && (best < 0 || (bd > 1e-9 && regs <= budget_hi))) out(*fit_hi, ops, regs), took_hi = true;
     if (best < 0 || (bd > 1e-9 && regs <= budget)) break;
+    heap.pop();
     V[best].live = false;
-    ops = total(&regs);
+    ++ver[best];
+    ops += bd, regs -= V[best].store;
+    for (int p = V[best].parent; p >= 0; p = V[p].parent) {  // F up to the nearest live ancestor
+      V[p].F += (double)V[p].cop / V[best].cop * V[best].F;
+      if (V[p].live) {
+        push(p);
+        break;
+      }
+    }
+    stack.assign(1, best);  // live values nearest below: new consumer
+    while (!stack.empty()) {
+      const int u = stack.back();
+      stack.pop_back();
+      for (int k : V[u].kids)
+        if (k >= 0) {
+          if (V[k].live) push(k);
+          else stack.push_back(k);
+        }
+    }
   }
   if (!took_hi) out(*fit_hi, ops, regs);
   out(f, ops, regs);
@@ -439,10 +471,14 @@ int seg_static_bits(int m) {
 
 double seg_walk_cost(const Plan& P) { return P.seg_ops; }
 
-// Greedy starts the walk-order descent runs from (SUP_JIT_STARTS overrides).
-int seg_search_starts() {
+// Greedy starts the walk-order descent runs from (SUP_JIT_STARTS overrides):
+// 8 when the plain walk would take a second or more on one MI355X (2n + 1 ops
+// per Gray step at 3.7e13 lane-ops/s: n >= 40), else 3.  More starts find
+// cheaper walks (n = 40 bench matrix: 13.05 ops per step from 3 starts, 12.66
+// from 8) for ~2x the plan time (1.3 s -> 2.3 s).
+int seg_search_starts(int n) {
   if (const char* e = std::getenv("SUP_JIT_STARTS")) return std::max(1, std::atoi(e));
-  return 3;
+  return std::ldexp(1.0, n - 1) * (2.0 * n + 1.0) / 3.7e13 >= 1.0 ? 8 : 3;
 }
 
 std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b_out) {
@@ -510,7 +546,7 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
     const int hot = std::min(m, 12);
     std::vector<int> best;
     double bcost = 1e300;
-    const size_t nstart = std::min(starts.size(), (size_t)seg_search_starts());
+    const size_t nstart = std::min(starts.size(), (size_t)seg_search_starts(n));
     finals[ci].clear();
     for (size_t si = 0; si < nstart; ++si) {
       std::vector<int> cur = starts[si].second;
