@@ -1321,9 +1321,13 @@ int build_seg(Plan& P) {
     R.len0 = P.seg_start[1], R.s_end = P.sub_start.back(), R.r_end = P.seg_start.back();
     seg_rows_finish(R, P.seg_b);
     SegFit f;
+    // experiments / tests: SUP_JIT_CC forces cc; SUP_JIT_STORAGE forces the
+    // storage budget of the chosen plan (same walk order and trees, other
+    // live/on-demand choices: the same values, so bit-identical results)
     if (const char* e = std::getenv("SUP_JIT_CC"))
       f = seg_fit(R, std::max(0, std::min({std::atoi(e), R.b - 1, kMaxCachedBits})), kRegsMax);
     else f = seg_best(R);
+    if (const char* e = std::getenv("SUP_JIT_STORAGE")) f = seg_fit(R, f.cc, std::max(0, std::atoi(e)));
     P.outer_tree = std::move(f.outer);
     P.inner_tree = std::move(f.inner);
     P.seg_cc = f.cc;

@@ -190,3 +190,19 @@ def test_seg_pair_bits_bitexact_gpu(sup, orc, monkeypatch, b):
     got = sup.perman(a, algo=4, kernel="seg")
     assert got == orc.engine_perman_as(sup, a, "seg", threads=16)
     assert got == sup.perman_cpu(a, "seg", threads=16)
+
+
+def test_seg_storage_plan_invariance_gpu(sup, orc, monkeypatch):
+    """The generated kernel at storage budgets 0 (every copy and node formed on
+    demand inside its consumer), the default and 1000 (everything live): the
+    same bits, equal to the oracle mirror, at n = 26 and n = 30."""
+    rng = np.random.default_rng(77)
+    for n, d in ((26, 0.5), (30, 0.3)):
+        a = np.where(rng.random((n, n)) < d, rng.random((n, n)) * 5, 0.0)
+        a[np.arange(n), rng.permutation(n)] = 1.0
+        want = orc.engine_perman_as(sup, a, "seg", threads=16)
+        for budget in (0, 1000):
+            monkeypatch.setenv("SUP_JIT_STORAGE", str(budget))
+            assert sup.perman(a, algo=4, kernel="seg") == want, (n, budget)
+        monkeypatch.delenv("SUP_JIT_STORAGE")
+        assert sup.perman(a, algo=4, kernel="seg") == want, n

@@ -175,3 +175,38 @@ def test_seg_pair_bits_chosen_by_cost(sup, monkeypatch):
         # the chosen plan is at least as cheap as every forced b whose code fits
         assert auto["est_ops_per_step"] <= min(forced[5], forced[6]) + 1e-9, (name, auto, forced)
         assert auto["est_ops_per_step"] == pytest.approx(forced[auto["pair_bits"]], abs=1e-9)
+
+
+@pytest.mark.parametrize("n,d,seed", [(16, 0.5, 31), (18, 0.35, 32)])
+def test_cpu_seg_storage_plan_invariance(sup, orc, monkeypatch, tmp_path, n, d, seed):
+    """Every value of the segmented walk is a pure function of x^0, so keeping a
+    row or node copy live or forming it on demand changes ops and registers,
+    never a bit.  Storage budgets from "everything on demand" (0) to
+    "everything live" (1000) keep the walk order and the arithmetic (host twin
+    == oracle mirror, which restate no storage plan), and every such kernel
+    compiles for gfx950 (the GPU twin of this test checks the bits)."""
+    monkeypatch.setenv("SUP_JIT_CACHE_DIR", str(tmp_path))
+    a = _rand(n, d, seed, ints=False)
+    want = orc.engine_perman_as(sup, a, "seg", threads=4)
+    cm = sup.plan_info(a, "seg")["colmap"]
+    for budget in (0, 40, 1000):
+        monkeypatch.setenv("SUP_JIT_STORAGE", str(budget))
+        assert (sup.plan_info(a, "seg")["colmap"] == cm).all()
+        assert sup.perman_cpu(a, "seg", threads=4) == want, budget
+        assert sup.prepare(a, "seg")["kind"] == "seg"
+
+
+def test_seg_skip_aware_plan(sup, monkeypatch):
+    """Integer matrices: the planner weighs each walk by its ops per Gray step
+    times the fraction of wave-chunks it cannot skip (sampled); measured over
+    every chunk (conftest.seg_skip_fraction, numpy), the chosen plan's effective
+    cost is no worse than the op-count-only plan's."""
+    from conftest import seg_skip_fraction
+    for n, d, seed in ((24, 0.15, 4), (26, 0.15, 5)):
+        a = _skip_case(sup, n, d, seed)
+        eff = {}
+        for polish in ("1", "0"):
+            monkeypatch.setenv("SUP_JIT_POLISH", polish)
+            info = sup.plan_info(a, "seg")
+            eff[polish] = info["est_ops_per_step"] * (1.0 - seg_skip_fraction(sup, a, "seg"))
+        assert eff["1"] <= eff["0"] * 1.05 + 1e-12, (n, eff)
