@@ -162,7 +162,7 @@ int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int
 /* The plan sup_perman would run with options `o` (NULL = defaults; o->jit and
  * o->gpu_num matter): walk kind (0 dense, 1 prefix/SpaRyser, 2 SkipPer,
  * 3 segmented), engine-bit -> column map (n-1 entries), lane and walk bits,
- * and (segmented walk) the walk bits held in every state (*cached_bits, 0-2)
+ * and (segmented walk) the walk bits held in every state (*cached_bits, 0-3)
  * and the pair bits with a specialised step (*pair_bits, 3-8; the walk loop is
  * unrolled by 2^pair_bits pair steps); *est_ops_per_step = the walk's cost
  * model (sup_stats.est_ops_per_step); any pointer may be NULL.  For the test

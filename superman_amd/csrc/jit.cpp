@@ -21,25 +21,29 @@
 // accumulated with one fma.  The walk is then a Gray walk over walk bits
 // 1..m-1 at half the step count; a step touching segment 0 updates both copies
 // and re-forms both products.  The loop is unrolled by 2^b pair steps
-// (b = seg_static_bits): pair bits below b get straight-line steps with
+// (b chosen per plan, 5..8): pair bits below b get straight-line steps with
 // compile-time table offsets (the top one with sign q&1), and every higher
 // bit shares one straight-line step over the union of their rows (full signed
 // column, zeros included) — a switch over per-bit steps would make LLVM
 // carry copies of x across its arms (measured: 120 -> 242 VGPRs).
 //
-// Cached walk bits.  Walk bits 1..cc (cc <= 2, seg_best) are held in every
-// state: each value that depends on them has one copy per state of those
+// Cached walk bits.  Walk bits 1..cc (cc <= 3, seg_best) are held in every
+// state: each node that depends on them has one copy per state of those
 // bits, so their pair steps only accumulate (the state is a compile-time
 // constant inside the unrolled block) and the other steps update every copy.
-// cc is chosen on the exact op count within a live-value budget.
+// Only x^0 (walk bits 0..cc clear) is walked; row copies are x^0 + constants
+// (seg_cx, seg_cy), and every row or node copy is kept live or formed on
+// demand inside its consumer (seg_fit's storage plan) — the same values
+// either way.  cc, the storage plan and b are chosen on the exact op count
+// within a live-value budget.
 //
-// Measured on MI355X (profiles/r1): n=40 d=0.5 bench matrix 18.2 VALU
-// instructions per Gray step (cost model 18.0; the prefix-blocked AOT walk
-// executes 46.6, the plain dense walk 81), VALU 96% busy at 2 waves/SIMD,
-// 2.05e12 steps/s.  Everything else (chunk start, lane layout, wave-chunk
-// queue, reduction order) is walk_common.hpp's, shared with the ahead-of-time
-// kernels, and the arithmetic is mirrored bit for bit by engine_cpu.cpp
-// (tree_*, seg_*) and oracle/oracle.c (kind 3).
+// Measured on MI355X (profiles/r2): n=40 d=0.5 bench matrix 12.8 VALU
+// instructions per Gray step (cost model 12.7; round 1 18.2; the prefix-
+// blocked AOT walk executes 46.6, the plain dense walk 81), VALU 94% busy at 2
+// waves/SIMD, 2.85e12 steps/s.  Everything else (chunk start, lane layout,
+// wave-chunk queue, reduction order) is walk_common.hpp's, shared with the
+// ahead-of-time kernels, and the arithmetic is mirrored bit for bit by
+// engine_cpu.cpp (tree_*, seg_*) and oracle/oracle.c (kind 3).
 //
 // Lane sum.  Two levels: acc takes the pair terms of one 2^b-pair block and
 // folds into a running total after each shared step (8.0e-12 against 2.4e-11
@@ -47,14 +51,18 @@
 //
 // Chunk skip.  Rows no walk bit touches (the outer tree's tail) are constant
 // over a wave-chunk; when their product is an exact zero in every valid lane
-// the chunk's walk is skipped (integer matrices; config 5: 60% of chunks).
+// the chunk's walk is skipped (integer matrices; the planner weighs it:
+// config 5 skips 87% of its chunks).
 //
 // Compiled code objects are cached in memory (per process, per device) and on
 // disk: $SUP_JIT_CACHE_DIR, else $XDG_CACHE_HOME/superman_amd, else
 // ~/.cache/superman_amd (SUP_JIT_CACHE_DIR="" disables the disk cache).
 // Debugging / experiment knobs: SUP_JIT_DUMP=<dir> keeps the generated source,
-// SUP_JIT_VERBOSE prints the plan's op count, live values and cached bits,
-// SUP_JIT_CC / SUP_JIT_WAVES / SUP_JIT_LDS force cached bits, occupancy, LDS.
+// SUP_JIT_VERBOSE prints the plan's op count, live values and cached bits;
+// SUP_JIT_CC / _B / _STORAGE / _STARTS / _POLISH / _REGMAX / _KP / _PF /
+// _XSTEP / _WAVES / _LDS force cached bits, pair bits, storage budget, search
+// starts, skip polish, register budget, SGPR pieces per region, prefetch,
+// cross-step regions, occupancy, dynamic LDS.
 #include <hip/hiprtc.h>
 #include <sys/stat.h>
 #include <unistd.h>
