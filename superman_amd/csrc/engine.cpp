@@ -532,7 +532,10 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   if ((rc = ensure(c->d_cols, c->cols_cap, P.cols.size()))) return rc;
   if ((rc = ensure(c->d_chunk, c->chunk_cap, (size_t)count))) return rc;
   if ((rc = ensure(c->d_scratch, c->scratch_cap, (size_t)pairwise_scratch_size(count)))) return rc;
-  const bool visited = want_visited && P.kind == kWalkSkip;
+  // walked states per chunk: SkipPer's jumps, the segmented walk's chunk skip
+  // (only where the walk leaves rows untouched)
+  const bool visited = want_visited && (P.kind == kWalkSkip || (P.kind == kWalkSeg && P.outer_tree.tail_hi >
+                                                                                           P.outer_tree.tail_lo));
   if (visited && (rc = ensure(c->d_visited, c->visited_cap, (size_t)count))) return rc;
 
   const bool seg = P.kind == kWalkSeg;

@@ -1133,6 +1133,7 @@ struct Gen {
     o << "  const uint32_t lane_par = __builtin_popcount(lane) & 1u;\n";
     o << "  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {\n";
     o << "    double keep = 0.0;\n";
+    o << "    uint32_t vkeep = 0;\n";  // per chunk: Gray steps walked per lane (0 when skipped)
     o << "    for (uint32_t j = 0; j < (uint32_t)p.group; ++j) {\n";
     o << "      const uint64_t a = (uint64_t)g * p.group + j;\n";
     o << "      if (a >= p.chunk_count) break;\n";
@@ -1167,10 +1168,12 @@ struct Gen {
     // chunk: when Ro is an exact zero in every valid lane (integer matrices),
     // every product of the chunk is zero and the walk is skipped (part = +0).
     o << "      double acc = 0.0;\n";
+    o << "      uint32_t vis = 0;\n";
     if (P.outer_tree.tail_hi > P.outer_tree.tail_lo)
       o << "      if (__builtin_amdgcn_ballot_w64(lane_valid && Ro != 0.0) != 0) {\n";
     else
       o << "      {\n";
+    o << "      vis = " << (1u << m) << "u;\n";
     tree_init(1, 0);
     tree_init(1, 1);
     for (uint32_t S : submasks(inner_root_csig()))
@@ -1229,9 +1232,13 @@ struct Gen {
     o << "      }\n";
     o << "      const double part = wave_sum(lane_valid ? acc : 0.0);\n";
     o << "      keep = (lane == j) ? part : keep;\n";
+    o << "      vkeep = (lane == j) ? vis : vkeep;\n";
     o << "    }\n";
     o << "    const uint64_t a = (uint64_t)g * p.group + lane;\n";
-    o << "    if (lane < (uint32_t)p.group && a < p.chunk_count) p.chunk_out[a] = keep;\n";
+    o << "    if (lane < (uint32_t)p.group && a < p.chunk_count) {\n";
+    o << "      p.chunk_out[a] = keep;\n";
+    o << "      if (p.visited) p.visited[a] = vkeep;\n";
+    o << "    }\n";
     o << "  }\n";
     o << "}\n";
     o << "}  // namespace sup\n";

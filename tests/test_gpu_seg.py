@@ -154,9 +154,12 @@ def test_seg_chunk_skip_gpu(sup, orc, n, d, seed):
     from conftest import seg_skip_fraction
     from test_seg import _skip_case
     a = _skip_case(sup, n, d, seed)
-    assert seg_skip_fraction(sup, a) >= 0.25
+    frac = seg_skip_fraction(sup, a, "seg")
+    assert frac >= 0.25
     got, st = sup.perman(a, algo=4, kernel="seg", return_stats=True)
     assert st["walk_kind"] == 3
+    # the kernel reports the states it walked: exactly the chunks not skipped
+    assert st["visited_steps"] == round((1.0 - frac) * 2 ** (n - 1))
     assert got == sup.perman_cpu(a, "seg", threads=8) == orc.engine_perman_as(sup, a, "seg", threads=8)
     assert rel(got, float(orc.exact_perman_crt(a))) < 1e-12
 
