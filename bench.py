@@ -295,8 +295,11 @@ def main():
                             "value": args.steps * (1 << (nb - 1)) / e2, "unit": "gray-steps/s (nominal)",
                             "ms_per_step": e2 / args.steps * 1e3, "kernel_ms_avg": kms2,
                             "walk": walk_names[st2["walk_kind"]],
-                            # products evaluated / Gray steps of this rank's shard (SkipPer skips < 1)
+                            # states evaluated / Gray steps (SkipPer's jumps and the segmented
+                            # walk's chunk skip make it < 1); SURVEY 8(d): visited steps/s beside
+                            # the nominal rate
                             "visited_frac": st2["visited_steps"] * world / float(1 << (nb - 1)),
+                            "visited_steps_per_s": args.steps * st2["visited_steps"] * world / e2,
                             "permanent": perm2})
 
     # every rank's walk-kernel time (strong-scaling diagnosis: the slowest rank sets the step)
