@@ -934,6 +934,7 @@ struct Gen {
   };
   std::vector<std::string> pieces;
   std::map<std::string, int> piece_id;
+  int next_step_id = 0;
   int piece(const std::string& load_expr) {
     auto it = piece_id.find(load_expr);
     if (it != piece_id.end()) return it->second;
@@ -951,7 +952,7 @@ struct Gen {
     auto col_piece = [&](int pc) {
       return piece("((cjdbl8*)(" + base + " + " + off + "))[" + std::to_string(pc) + "]");
     };
-    const int sid = out.empty() ? 0 : out.back().step + 1;
+    const int sid = next_step_id++;
     for (size_t i = 0; i < rows.size(); ++i) {
       const int vi = full ? rows[i] : (int)i, pc = col_piece(vi / 8);
       out.push_back({"x[" + std::to_string(rows[i]) + "] += " + pref(pc, vi % 8) + ";", {pc}, sid});
