@@ -98,7 +98,7 @@ typedef struct {
   int verbose;        /* print per-device / per-chunk timing lines like the reference        */
   int jit;            /* segmented walk specialised for the matrix pattern (hiprtc, gfx950):  */
                       /*  -1 never; 0 auto: when its cost model wins and the predicted walk  */
-                      /*  time saved exceeds 1 s (plan ~0.1-1 s + compile ~0.5 s, both once */
+                      /*  time saved exceeds 3 s (plan 0.1-2.5 s + compile ~0.5 s, both once*/
                       /*  per matrix: plans cached in memory, code objects also on disk); 1  */
                       /*  whenever its cost model wins                                       */
 } sup_opts;

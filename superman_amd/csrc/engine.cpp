@@ -255,11 +255,11 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
 // fp64 VALU lane-ops per second of one MI355X on the walk kernels (measured:
 // 46.6 ops/step at 7.98e11 steps/s on the n=40 bench), for jit's auto mode.
 static constexpr double kLaneOpsPerSec = 3.7e13;
-// The segmented walk's plan (walk-order searches, 0.1-1 s at n = 30-44) and
-// compile + load (0.4-0.7 s with hiprtc; 0 when the disk cache holds it) are
-// paid once per matrix; auto mode specialises when the predicted walk time
-// saved is larger than both.
-static constexpr double kJitMinSavingSec = 1.0;
+// The segmented walk's plan (walk-order searches, 0.1-2.5 s at n = 30-44)
+// and compile + load (0.4-0.7 s with hiprtc; 0 when the disk cache holds it)
+// are paid once per matrix; auto mode specialises when the predicted walk time
+// saved is clearly larger than both.
+static constexpr double kJitMinSavingSec = 3.0;
 
 static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit,
                              int ndev, int dev);

@@ -52,7 +52,7 @@ def test_planner_choice(sup):
     a, _, _ = sup.read_matrix(fixture_path("double__40_0.50_0"))
     assert sup.plan_info(a, "dense", jit=-1)["kind"] == "sparse"
     assert sup.plan_info(a, "dense", jit=1)["kind"] == "seg"
-    # auto: the n = 40 walk saves ~0.5 s on one GPU, below the 1 s plan + compile
+    # auto: the n = 40 walk saves ~0.5 s on one GPU, below the 3 s plan + compile
     # threshold (a one-shot call is faster on the prefix walk); n = 44 saves seconds
     assert sup.plan_info(a, "dense", jit=0)["kind"] == "sparse"
     assert sup.plan_info(a, "dense", jit=0, gpu_num=8)["kind"] == "sparse"
