@@ -154,6 +154,12 @@ double walk_cost(const Plan& P) {
   return cost + w * 16.0 * ((P.n + 7) / 8);  // tail: the rest of the walk bits, bounded
 }
 
+// ops per nominal Gray step, chunks the walk skips discounted: what the
+// planner compares walks on (the reported cost model stays per walked step)
+static double walk_cost_eff(const Plan& P) {
+  return P.kind == kWalkSeg ? walk_cost(P) * (1.0 - P.seg_skip) : walk_cost(P);
+}
+
 int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const Layout& lay, Plan& P) {
   if (n < 1 || n > SUP_MAX_N) {
     set_error("n must be in [1, 64]");
@@ -362,15 +368,15 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
       if (jit < 1 && steps * skip_cost / kLaneOpsPerSec < kJitMinSavingSec) return SUP_OK;
       Plan s;
       if (make_seg(s) != SUP_OK) return SUP_OK;
-      if (walk_cost(s) >= skip_cost) return SUP_OK;
-      if (jit < 1 && steps * (skip_cost - walk_cost(s)) / kLaneOpsPerSec < kJitMinSavingSec) return SUP_OK;
+      if (walk_cost_eff(s) >= skip_cost) return SUP_OK;
+      if (jit < 1 && steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec < kJitMinSavingSec) return SUP_OK;
       if (integral) {
         const double f = skip_visited_fraction(P, dev);
         if (f < 0.0) return SUP_OK;
         skip_cost *= f;
       }
-      const double saved = steps * (skip_cost - walk_cost(s)) / kLaneOpsPerSec;
-      if (walk_cost(s) < skip_cost && (jit >= 1 || saved >= kJitMinSavingSec)) P = std::move(s);
+      const double saved = steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec;
+      if (walk_cost_eff(s) < skip_cost && (jit >= 1 || saved >= kJitMinSavingSec)) P = std::move(s);
       return SUP_OK;
     }
     case SUP_KERNEL_DENSE_PLAIN: return make_plan(A, n, kWalkDense, false, lay, P);
@@ -400,9 +406,9 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
                         kJitMinSavingSec;  // auto mode: skip the segmented plan's search where it cannot pay
   if (jit >= 0 && n >= 8 && lay.m >= 3 && (jit >= 1 || may_save)) {
     Plan s;
-    if (make_seg(s) == SUP_OK && walk_cost(s) < walk_cost(best)) {
+    if (make_seg(s) == SUP_OK && walk_cost_eff(s) < walk_cost(best)) {
       const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
-      const double saved = steps * (walk_cost(best) - walk_cost(s)) / kLaneOpsPerSec;
+      const double saved = steps * (walk_cost(best) - walk_cost_eff(s)) / kLaneOpsPerSec;
       if (jit >= 1 || saved >= kJitMinSavingSec) best = std::move(s);
     }
   }

@@ -91,6 +91,7 @@ struct Plan {
   bool lds = false;                // kWalkDense run by the LDS-staged kernel (walk_lds.hip; same bits)
   int seg_cc = 0;                  // cached step classes: walk bits 1..seg_cc held in every state
   double seg_ops = 0.0;            // fp64 VALU ops per Gray step of the generated kernel
+  double seg_skip = 0.0;           // sampled fraction of wave-chunks the kernel skips (integer matrices)
   int seg_regs = 0;                // values live across steps (doubles), estimate
   std::vector<int> jofs;           // [m] offset (doubles) of walk bit k's + block in jtab
   std::vector<double> jtab;        // packed touched values: + block, - block (each padded to 8); then,
@@ -120,6 +121,8 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
 // rows exactly zero in every lane) for an extended walk order (m walk
 // columns, then the lane columns); integer matrices.
 double seg_skip_estimate(const double* A, int n, const std::vector<int>& order, int m, int samples);
+// The same for a built segmented plan (engine row and column order).
+double seg_skip_fraction_plan(const Plan& P, int samples);
 // Engine row order of the segmented walk for walk columns `walk`: rows in
 // first-touch order, segment 0 (the rows of walk[0]) internally ordered by
 // first touch among walk[1..], its rows no other walk column touches last.

@@ -670,6 +670,40 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
   return extend(bests[gi], count);
 }
 
+double seg_skip_fraction_plan(const Plan& P, int samples) {
+  const int n = P.n, L = P.lay.L, m = P.lay.m, nb = n - 1;
+  const int tail_lo = P.seg_start.empty() ? n : P.seg_start.back();
+  if (tail_lo >= n) return 0.0;
+  for (const double v : P.cols)
+    if (v != std::floor(v)) return 0.0;  // exact zeros need integer entries
+  const int h = nb - L - m;
+  int skipped = 0;
+  std::vector<double> base(n - tail_lo);
+  for (int s = 0; s < samples; ++s) {
+    const uint64_t a = h > 0 ? ((uint64_t)s * 0x9E3779B97F4A7C15ull) >> (64 - std::min(h, 63)) : 0;
+    const uint64_t g = a ^ (a >> 1);
+    for (int r = tail_lo; r < n; ++r) {
+      double v = P.x0[r];
+      for (int k = 0; k < h; ++k)
+        if ((g >> k) & 1u) v += P.cols[(size_t)(2 * (L + m + k)) * P.NP + r];
+      base[r - tail_lo] = v;
+    }
+    bool all = true;
+    for (unsigned lane = 0; lane < (1u << L) && all; ++lane) {
+      bool zero = false;
+      for (int r = tail_lo; r < n && !zero; ++r) {
+        double v = base[r - tail_lo];
+        for (int e = 0; e < L; ++e)
+          if ((lane >> e) & 1u) v += P.cols[(size_t)(2 * e) * P.NP + r];
+        zero = v == 0.0;
+      }
+      all = zero;
+    }
+    skipped += all;
+  }
+  return (double)skipped / samples;
+}
+
 double seg_skip_estimate(const double* A, int n, const std::vector<int>& order, int m, int samples) {
   const int nb = n - 1, L = std::min(6, nb - m);
   if ((int)order.size() < m + L) return 0.0;
@@ -1348,6 +1382,7 @@ int build_seg(Plan& P) {
     P.inner_tree = std::move(f.inner);
     P.seg_cc = f.cc;
     P.seg_ops = f.ops;
+    P.seg_skip = seg_skip_fraction_plan(P, 2048);
     P.seg_regs = f.regs;
     if (std::getenv("SUP_JIT_VERBOSE"))
       std::fprintf(stderr, "seg plan n=%d m=%d b=%d ops/step=%.4f regs=%d cc=%d (storage plans evaluated: %ld)\n", n,
