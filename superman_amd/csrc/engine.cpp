@@ -578,7 +578,11 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   const uint64_t wpb = P.lds ? 1 : kWavesPerBlock;  // waves per block
   const uint64_t resident = (uint64_t)c->cus * (uint64_t)occ;  // resident blocks
   const uint64_t res_waves = resident * wpb;
-  unsigned group = 8;
+  // chunk groups of up to 64 (one lane per partial: a 512-byte store); the
+  // largest that leaves >= 32 groups per resident wave (tail balance).  n = 40
+  // on one MI355X: 16 chunks, 128-byte stores (8 chunks: 64-byte partial-line
+  // stores, 2.5x the partials' bytes in WRITE_SIZE)
+  unsigned group = 64;
   while (group > 1 && count / ((uint64_t)group * res_waves) < 32) group >>= 1;
   const uint64_t waves_needed = (count + group - 1) / group;  // one chunk group per wave at a time
   uint64_t grid = (waves_needed + wpb - 1) / wpb;

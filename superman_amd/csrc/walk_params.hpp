@@ -34,8 +34,9 @@ struct WalkParams {
   // sparse kernels: nblk of walk bit k packed as 4-bit fields, k < 16 in nb_lo,
   // k >= 16 in nb_hi (kept in SGPRs: no memory round trip per step)
   unsigned long long nb_lo, nb_hi;
-  // wave-chunks are dequeued in groups of `group` (1, 2, 4 or 8) consecutive
-  // chunks; the group's partials leave the wave as one store of 8*group bytes.
+  // wave-chunks are dequeued in groups of `group` (1, 2, 4, ..., 64)
+  // consecutive chunks; the group's partials leave the wave as one store of
+  // 8*group bytes.
   // The host picks the largest group that still leaves >= 32 groups per
   // resident wave (tail balance beats write coalescing).
   unsigned int group;
