@@ -904,6 +904,23 @@ struct Gen {
     const ProdTree& t = tr(ti);
     return (id < t.items() ? t.item_sig[id] : t.sig[id - t.items()]) & ccm;
   }
+  // operand at the chunk start: live values by name, the rest inline (row
+  // copies read their constant with one scalar load), so only live values are
+  // held while the trees are formed
+  std::string iopnd(int ti, int v, int id, uint32_t S) {
+    const ProdTree& t = tr(ti);
+    if (id < t.items()) {
+      const int r = t.item_row[id];
+      if (r < 0) return ti == 0 ? "Ro" : (v ? "Cy" : "Cx");
+      const uint32_t s = S & rs(r);
+      if (s == 0) return v ? "y[" + std::to_string(r) + "]" : "x[" + std::to_string(r) + "]";
+      if (live(r, v)) return cname(r, s, v);
+      return "(x[" + std::to_string(r) + "] + " + kinit(r, s, v) + ")";
+    }
+    const int i = id - t.items();
+    if (nlive(ti, v, i)) return nname(ti, v, i, S);
+    return "(" + iopnd(ti, v, t.a[i], S) + " * " + iopnd(ti, v, t.b[i], S) + ")";
+  }
   std::string top(int ti, int v, uint32_t S) const {
     const ProdTree& t = tr(ti);
     return t.root() < 0 ? std::string() : opnd(ti, v, t.root(), S, nullptr);
@@ -1179,24 +1196,25 @@ struct Gen {
     o << "        cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off_const(0, 0) << ");\n";
     for (int r = 0; r < len0; ++r) o << "        y[" << r << "] = x[" << r << "] + cv[" << r / 8 << "][" << r % 8 << "];\n";
     o << "      }\n";
-    // every copy for the cached states (init: all named; on-demand ones are
-    // dead after the trees are formed)
+    // the live row copies for the cached states (y copy 0 is y[r])
     for (int r = 0; r < n; ++r)
       for (int v = 0; v < (r < len0 ? 2 : 1); ++v)
-        for (uint32_t S : submasks(rs(r))) {
-          if (S == 0) continue;
-          o << "      double " << cname(r, S, v) << " = x[" << r << "] + " << kinit(r, S, v) << ";\n";
-        }
-    // constant items (tails) and every node copy
+        if (live(r, v))
+          for (uint32_t S : submasks(rs(r))) {
+            if (S == 0) continue;
+            o << "      double " << cname(r, S, v) << " = x[" << r << "] + " << kinit(r, S, v) << ";\n";
+          }
+    // constant items (tails) and the live node copies (on-demand ones inline)
     auto tree_init = [&](int ti, int v) {
       const ProdTree& t = tr(ti);
       if (t.tail_hi > t.tail_lo)
         o << "      const double " << (ti == 0 ? "Ro" : (v ? "Cy" : "Cx")) << " = "
           << tree(t.tail_lo, t.tail_hi, v ? "y" : "x") << ";\n";
       for (int i = 0; i < t.K(); ++i)
-        for (uint32_t S : submasks(t.sig[i] & ccm))
-          o << "      double " << opnd(ti, v, t.items() + i, S, nullptr) << " = " << node(ti, v, i, S, nullptr)
-            << ";\n";
+        if (this->nlive(ti, v, i))
+          for (uint32_t S : submasks(t.sig[i] & ccm))
+            o << "      double " << nname(ti, v, i, S) << " = " << iopnd(ti, v, t.a[i], S) << " * "
+              << iopnd(ti, v, t.b[i], S) << ";\n";
     };
     tree_init(0, 0);
     // Rows no walk bit touches (the outer tree's tail, Ro) are constant over the
@@ -1211,8 +1229,12 @@ struct Gen {
     o << "      vis = " << (1u << m) << "u;\n";
     tree_init(1, 0);
     tree_init(1, 1);
-    for (uint32_t S : submasks(inner_root_csig()))
-      o << "      double " << dname(S) << " = " << top(1, 0, S) << " - " << top(1, 1, S) << ";\n";
+    if (P.inner_tree.root() >= 0)
+      for (uint32_t S : submasks(inner_root_csig()))
+        o << "      double " << dname(S) << " = " << iopnd(1, 0, P.inner_tree.root(), S) << " - "
+          << iopnd(1, 1, P.inner_tree.root(), S) << ";\n";
+    else
+      o << "      double D0 = 0.0;\n";
     {
       const std::string U = top(0, 0, 0);
       o << "      acc = " << (U.empty() ? dname(0) : dname(0) + " * " + U) << ";\n";
