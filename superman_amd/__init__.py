@@ -180,12 +180,12 @@ def partial(mat, start: int, end: int, kernel: str = "dense", gpu_num: int = 1, 
 
 
 def perman_shard(mat, shard: int, nshards: int, kernel: str = "dense", device_id: int = 0,
-                 return_stats: bool = False, jit: int = 0):
+                 return_stats: bool = False, jit: int = 0, walk_log2: int = 0):
     """Partial sum of shard `shard` of `nshards` of the engine's enumeration
     (one process per GPU): the shards add up to perm / (4(n&1)-2)."""
     a, dt, n = _mat(mat)
     lib = _lib.load()
-    o = _opts(device_id=device_id, jit=jit)
+    o = _opts(device_id=device_id, jit=jit, walk_log2=walk_log2)
     out, st = C.c_double(0.0), SupStats()
     _lib.check(lib.sup_perman_shard(a.ctypes.data, dt, n, _KERNELS[kernel], int(shard), int(nshards), C.byref(o),
                                     C.byref(out), C.byref(st)), "perman_shard")

@@ -95,6 +95,18 @@ int sup_nw_start(const void* mat, sup_dtype t, int n, double* x0, double* p0) {
   return SUP_OK;
 }
 
+// The default layout, or the walk length (m walk bits) sup_opts::walk_log2 asks for.
+static Layout layout_for(int n, const sup_opts& o) {
+  Layout lay = default_layout(n);
+  if (o.walk_log2 > 0) {
+    const int rest = n - 1 - lay.L;
+    lay.m = std::min(o.walk_log2, rest);
+    lay.h = rest - lay.m;
+    lay.fixed = true;
+  }
+  return lay;
+}
+
 int sup_perman(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched sched, const sup_opts* o_in,
                double* out, sup_stats* st) {
   auto t0 = std::chrono::steady_clock::now();
@@ -107,12 +119,7 @@ int sup_perman(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched
   if ((rc = to_double(mat, t, n, A))) return rc;
   Plan P;
   if ((rc = check_walk_opts(o))) return rc;
-  Layout lay = default_layout(n);
-  if (o.walk_log2 > 0) {
-    const int rest = n - 1 - lay.L;
-    lay.m = std::min(o.walk_log2, rest);
-    lay.h = rest - lay.m;
-  }
+  const Layout lay = layout_for(n, o);
   if ((rc = plan_for(A.data(), n, kernel, lay, P, o.jit, sched == SUP_SCHED_SINGLE ? 1 : o.gpu_num,
                      o.device_id)))
     return rc;
@@ -203,7 +210,7 @@ int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int
   std::vector<double> A;
   if ((rc = to_double(mat, t, n, A))) return rc;
   Plan P;
-  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, nshards, o.device_id))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, layout_for(n, o), P, o.jit, nshards, o.device_id))) return rc;
   const uint64_t C = P.lay.chunks();
   const uint64_t c0 = C * (uint64_t)shard / (uint64_t)nshards, c1 = C * (uint64_t)(shard + 1) / (uint64_t)nshards;
   SchedResult r;

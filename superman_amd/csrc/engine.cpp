@@ -270,6 +270,36 @@ static constexpr double kJitMinSavingSec = 3.0;
 static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit,
                              int ndev, int dev);
 
+// Chunk start of the segmented walk (start index's column sums, row copies,
+// trees of every cached state), in VALU ops per lane: ~750 fitted from config
+// 3's kernel time against its walk length (profiles/r2/probe_walklen.log).
+static constexpr double kSegStartOps = 1024.0;
+
+// The segmented walk on the default layout, or on longer wave-chunks where its
+// steps are cheap: a chunk's walk (2^m steps) should be >= 64 chunk starts.
+// Both walks are planned and the one with fewer ops per nominal step, chunk
+// start and chunk skip included, wins.  At least 2^15 chunks remain (16 per
+// resident wave of one GPU).  The layout depends only on the matrix, so every
+// GPU count sums the same chunks (bit-identical results).
+static int make_seg_plan(const double* A, int n, const Layout& lay, Plan& P) {
+  int rc = make_plan(A, n, kWalkSeg, false, lay, P);
+  if (rc || lay.fixed) return rc;
+  const int mmax = std::min(lay.m + lay.h - 15, 31);
+  int m2 = lay.m;
+  while (m2 < mmax && std::ldexp(walk_cost(P), m2) < 64.0 * kSegStartOps) ++m2;
+  if (m2 == lay.m) return SUP_OK;
+  Layout l2 = lay;
+  l2.m = m2;
+  l2.h = lay.m + lay.h - m2;
+  Plan s2;
+  if (make_plan(A, n, kWalkSeg, false, l2, s2) != SUP_OK) return SUP_OK;
+  auto eff = [](const Plan& q) {
+    return (1.0 - q.seg_skip) * (walk_cost(q) + std::ldexp(kSegStartOps, -q.lay.m));
+  };
+  if (eff(s2) < eff(P)) P = std::move(s2);
+  return SUP_OK;
+}
+
 // Plans are pure functions of (matrix, request, layout): repeated calls on the
 // same matrix (the bench's steps, a shard per rank, -p6 items, reductions
 // revisiting a leaf) reuse the plan instead of re-running the walk-order
@@ -348,7 +378,7 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
                              int ndev, int dev) {
   // candidates in preference order; the cheapest by walk_cost wins
   std::vector<WalkKind> kinds;
-  auto make_seg = [&](Plan& s) { return make_plan(A, n, kWalkSeg, false, lay, s); };
+  auto make_seg = [&](Plan& s) { return make_seg_plan(A, n, lay, s); };
   switch (kernel) {
     case SUP_KERNEL_SKIPPER: {
       // SkipPer only gains where some x_j(S) is exactly zero.  With a

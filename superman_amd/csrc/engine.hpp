@@ -31,6 +31,7 @@ struct Layout {
   int L;          // lane bits = min(6, n-1)
   int m;          // walk bits
   int h;          // high (wave-chunk) bits = n-1-L-m
+  bool fixed = false;  // m asked for by the caller (sup_opts::walk_log2): plans keep it
   uint64_t chunks() const { return 1ull << h; }
 };
 Layout default_layout(int n);

@@ -144,6 +144,26 @@ def test_seg_n40_d02_companion(sup):
     b = a.copy()
     b[7] *= 4.0
     assert sup.perman(b, algo=4, jit=1) == r_seg * 4.0
+    # cheap steps: the plan lengthens the wave-chunks (engine.cpp make_seg_plan);
+    # the shards of that layout still pair up to the full sum bit for bit
+    assert sup.plan_info(a, "dense", jit=1)["m"] > sup.layout(40)[1]
+    full = sup.perman_shard(a, 0, 1, jit=1)
+    parts = [sup.perman_shard(a, r, 8, jit=1) for r in range(8)]
+    while len(parts) > 1:
+        parts = [parts[i] + parts[i + 1] for i in range(0, len(parts), 2)]
+    assert parts[0] == full and -2 * full == r_seg
+
+
+def test_seg_config3_long_chunks(sup, golden):
+    """Config 3 (double/36_0.20_0, SortOrder, SpaRyser request): the segmented
+    walk on lengthened wave-chunks against the reference's golden, and
+    bit-identical to the same walk length asked for explicitly (walk_log2)."""
+    a = sup.sort_order(sup.read_matrix(fixture_path("double__36_0.20_0"))[0])[0]
+    info = sup.plan_info(a, "sparse", jit=1)
+    assert info["kind"] == "seg" and info["m"] > sup.layout(36)[1]
+    got = sup.perman(a, algo=4, sparse=True, jit=1)
+    assert rel(got, golden["double__36_0.20_0|sparse|r1|b0|t8"]) < 1e-9
+    assert sup.perman(a, algo=4, sparse=True, jit=1, walk_log2=info["m"]) == got
 
 
 @pytest.mark.parametrize("n,d,seed", [(24, 0.15, 4), (24, 0.15, 3)])

@@ -177,6 +177,26 @@ def test_seg_pair_bits_chosen_by_cost(sup, monkeypatch):
         assert auto["est_ops_per_step"] == pytest.approx(forced[auto["pair_bits"]], abs=1e-9)
 
 
+def test_seg_walk_length_rule(sup):
+    """Cheap segmented walks run on longer wave-chunks (engine.cpp
+    make_seg_plan): a chunk's walk should cost >= 64 chunk starts, with at
+    least 2^15 chunks left.  Measured on MI355X (profiles/r2/probe_walklen.log):
+    config 3 2.94 -> 2.12 ms at m = 14, the d = 0.2 companion 36.1 -> 33.4 ms at
+    m = 15; the bench matrix (12.7 ops per step) keeps m = 13."""
+    cases = (("double__40_0.50_0", 0, "dense", 13, 13), ("double__40_0.20_0", 0, "dense", 14, 18),
+             ("double__36_0.20_0", 1, "sparse", 13, 14), ("double__32_0.50_0", 0, "dense", 10, 10))
+    for name, prep, kernel, lo, hi in cases:
+        a = sup.read_matrix(fixture_path(name))[0]
+        if prep:
+            a = sup.sort_order(a)[0]
+        info = sup.plan_info(a, kernel, jit=1)
+        n = a.shape[0]
+        assert info["kind"] == "seg" and info["L"] == 6 and lo <= info["m"] <= hi, (name, info["m"])
+        assert n - 1 - 6 - info["m"] >= min(15, sup.layout(n)[2])
+        if info["m"] > sup.layout(n)[1]:  # the walk's own steps now dwarf a chunk start, or the chunks ran out
+            assert info["est_ops_per_step"] * 2.0 ** info["m"] >= 64 * 1024 or n - 1 - 6 - info["m"] == 15
+
+
 @pytest.mark.parametrize("n,d,seed", [(16, 0.5, 31), (18, 0.35, 32)])
 def test_cpu_seg_storage_plan_invariance(sup, orc, monkeypatch, tmp_path, n, d, seed):
     """Every value of the segmented walk is a pure function of x^0, so keeping a
