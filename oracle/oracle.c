@@ -638,6 +638,14 @@ static void e_tree_update(const etree* t, const double* a, etv* v, int c) {
     if ((t->sig[i] >> c) & 1u) v->N[i] = e_tv_id(t, a, v, t->a[i]) * e_tv_id(t, a, v, t->b[i]);
 }
 
+/* D = top_x - top_y of segment 0's tree; a root node's product fuses with the
+ * subtraction into one fma (the kernel's __builtin_fma, one rounding) */
+static double e_seg_D(const etree* t, const double* x, const etv* vx, const double* y, const etv* vy) {
+  if (t->K == 0) return e_tree_top(t, x, vx) - e_tree_top(t, y, vy);
+  int i = t->K - 1;
+  return fma(e_tv_id(t, x, vx, t->a[i]), e_tv_id(t, x, vx, t->b[i]), -vy->N[i]);
+}
+
 /* the outer tree (rows outside segment 0) and segment 0's tree */
 static void e_seg_trees(const eplan* P, etree* outer, etree* inner) {
   unsigned rsig[ORC_MAXN] = {0};
@@ -680,7 +688,7 @@ static void e_derive(const eplan* P, const double* x0, double xs[][ORC_MAXN], do
 
 /* one pair step flipping walk bit k >= 1: its rows of x0 (and their copies in
  * every cached state), then in every state the outer tree and segment 0's
- * trees over x and y with D = top_x - top_y */
+ * trees over x and y with D = top_x - top_y (e_seg_D) */
 static void e_seg_step(const eplan* P, const etree* outer, const etree* inner, double* x0, double xs[][ORC_MAXN],
                        double ys[][ORC_MAXN], etv* vo, etv* vx, etv* vy, double* D, int k, int neg) {
   const double* c = P->col[2 * (P->L + k) + neg];
@@ -699,7 +707,7 @@ static void e_seg_step(const eplan* P, const etree* outer, const etree* inner, d
     if ((e_root_sig(inner) >> cl) & 1u) {
       e_tree_update(inner, xs[S], &vx[S], cl);
       e_tree_update(inner, ys[S], &vy[S], cl);
-      D[S] = e_tree_top(inner, xs[S], &vx[S]) - e_tree_top(inner, ys[S], &vy[S]);
+      D[S] = e_seg_D(inner, xs[S], &vx[S], ys[S], &vy[S]);
     }
   }
 }
@@ -742,7 +750,7 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
           e_tree_init(&outer, xs[S], &vo[S]);
           e_tree_init(&inner, xs[S], &vx[S]);
           e_tree_init(&inner, ys[S], &vy[S]);
-          D[S] = e_tree_top(&inner, xs[S], &vx[S]) - e_tree_top(&inner, ys[S], &vy[S]);
+          D[S] = e_seg_D(&inner, xs[S], &vx[S], ys[S], &vy[S]);
         }
         acc = D[0] * e_tree_top(&outer, xs[0], &vo[0]);
         double tot = 0.0; /* two-level lane sum: acc folds into tot after pair j = 2^segb (q + 1) */

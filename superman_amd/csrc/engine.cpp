@@ -272,11 +272,12 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
 
 // Chunk start of the segmented walk (start index's column sums, row copies,
 // trees of every cached state), in VALU ops per lane: ~750 fitted from config
-// 3's kernel time against its walk length (profiles/r2/probe_walklen.log).
-static constexpr double kSegStartOps = 1024.0;
+// 3's kernel time against its walk length, ~1700 from the d = 0.2 companion's
+// (profiles/r2/probe_walklen.log).
+static constexpr double kSegStartOps = 2048.0;
 
 // The segmented walk on the default layout, or on longer wave-chunks where its
-// steps are cheap: a chunk's walk (2^m steps) should be >= 64 chunk starts.
+// steps are cheap: a chunk's walk (2^m steps) should be >= 32 chunk starts.
 // Both walks are planned and the one with fewer ops per nominal step, chunk
 // start and chunk skip included, wins.  At least 2^15 chunks remain (16 per
 // resident wave of one GPU).  The layout depends only on the matrix, so every
@@ -286,7 +287,7 @@ static int make_seg_plan(const double* A, int n, const Layout& lay, Plan& P) {
   if (rc || lay.fixed) return rc;
   const int mmax = std::min(lay.m + lay.h - 15, 31);
   int m2 = lay.m;
-  while (m2 < mmax && std::ldexp(walk_cost(P), m2) < 64.0 * kSegStartOps) ++m2;
+  while (m2 < mmax && std::ldexp(walk_cost(P), m2) < 32.0 * kSegStartOps) ++m2;
   if (m2 == lay.m) return SUP_OK;
   Layout l2 = lay;
   l2.m = m2;

@@ -122,6 +122,14 @@ inline double tree_top(const ProdTree& t, const double* a, const TreeVal& v) {
   return t.root() < 0 ? 1.0 : tree_id(t, a, v, t.root());
 }
 
+// D = top_x - top_y of segment 0's tree; a root node's product fuses with
+// the subtraction, fma(x_a, x_b, -top_y), as in the kernel (jit.cpp dexpr)
+inline double seg_D(const ProdTree& t, const double* x, const TreeVal& vx, const double* y, const TreeVal& vy) {
+  if (t.K() == 0) return tree_top(t, x, vx) - tree_top(t, y, vy);
+  const int i = t.K() - 1;
+  return std::fma(tree_id(t, x, vx, t.a[i]), tree_id(t, x, vx, t.b[i]), -vy.N[i]);
+}
+
 // Paired form: Gray steps 2j, 2j+1 differ in walk bit 0 only; segment 0 (the
 // rows walk bit 0 touches) is kept as x (bit 0 clear) and y = x + a_0, and the
 // pair adds (-1)^j (prod_seg0 x - prod_seg0 y) * U1 (U1 = outer tree over the
@@ -182,7 +190,7 @@ void seg_init(const Lane& s, SegLane& g, const Plan& P, const SegConsts& K) {
     tree_init(P.outer_tree, g.x[S], g.o[S]);
     tree_init(P.inner_tree, g.x[S], g.ix[S]);
     tree_init(P.inner_tree, g.y[S], g.iy[S]);
-    g.D[S] = tree_top(P.inner_tree, g.x[S], g.ix[S]) - tree_top(P.inner_tree, g.y[S], g.iy[S]);
+    g.D[S] = seg_D(P.inner_tree, g.x[S], g.ix[S], g.y[S], g.iy[S]);
   }
 }
 
@@ -205,7 +213,7 @@ void seg_step(SegLane& g, const Plan& P, const SegConsts& K, int k, int neg) {
     if ((P.inner_tree.root_sig() >> c) & 1u) {
       tree_update(P.inner_tree, g.x[S], g.ix[S], c);
       tree_update(P.inner_tree, g.y[S], g.iy[S], c);
-      g.D[S] = tree_top(P.inner_tree, g.x[S], g.ix[S]) - tree_top(P.inner_tree, g.y[S], g.iy[S]);
+      g.D[S] = seg_D(P.inner_tree, g.x[S], g.ix[S], g.y[S], g.iy[S]);
     }
   }
 }

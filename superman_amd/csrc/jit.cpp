@@ -37,10 +37,13 @@
 // either way.  cc, the storage plan and b are chosen on the exact op count
 // within a live-value budget.
 //
-// Measured on MI355X (profiles/r2): n=40 d=0.5 bench matrix 12.8 VALU
-// instructions per Gray step (cost model 12.7; round 1 18.2; the prefix-
-// blocked AOT walk executes 46.6, the plain dense walk 81), VALU 94% busy at 2
-// waves/SIMD, 2.85e12 steps/s.  Everything else (chunk start, lane layout,
+// D = prod_x - prod_y of segment 0 fuses the x root's product with the
+// subtraction into one fma (dexpr).
+//
+// Measured on MI355X (profiles/r2): n=40 d=0.5 bench matrix 12.3 VALU
+// instructions per Gray step (cost model 12.2; round 1 18.2; the prefix-
+// blocked AOT walk executes 46.6, the plain dense walk 81), VALU 93% busy at 2
+// waves/SIMD, 2.94e12 steps/s.  Everything else (chunk start, lane layout,
 // wave-chunk queue, reduction order) is walk_common.hpp's, shared with the
 // ahead-of-time kernels, and the arithmetic is mirrored bit for bit by
 // engine_cpu.cpp (tree_*, seg_*) and oracle/oracle.c (kind 3).
@@ -295,8 +298,8 @@ SegFit seg_fit(const SegRows& R, int cc, int budget, int budget_hi = -1, SegFit*
     int rg = 6 + R.n;  // x^0, acc, tot, loop state
     for (auto& v : V)
       if (v.live) ops += v.fr * v.F, rg += v.store;
-    if (f.inner.root() >= 0) {  // D per copy: the sub and its non-live tops
-      ops += fD * cD;
+    if (f.inner.root() >= 0) {  // D per copy: the sub (fused with a root node's mul) and its non-live tops
+      ops += f.inner.K() ? 0.0 : fD * cD;
       for (int rt : {bx + f.inner.root(), by + f.inner.root()})
         if (!V[rt].live) ops += fD * (double)cD / V[rt].cop * V[rt].F;
       rg += cD;
@@ -621,45 +624,95 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
   // final candidates are compared on ops x (1 - sampled skip fraction).
   bool integral = true;
   for (size_t i = 0; i < (size_t)n * n && integral; ++i) integral = A[i] == std::floor(A[i]);
+  // swap descent of order `bo` (b = bb) on ops x (1 - skip), kPolishSamples
+  // sampled chunks per trial (the same chunks for every trial); returns the
+  // final eff and leaves the order in bo.  512 samples overfit: on config 5
+  // the descent's best at 512 (0.176 ops per nominal step) measured 0.216.
+  constexpr int kPolishSamples = 8192;
+  auto polish = [&](std::vector<int>& bo, int bb, double beff) {
+    const int npos = std::min(count, m + std::min(6, nb - m));
+    std::vector<int> cur(bo.begin(), bo.begin() + npos);
+    double cur_ops = cost(std::vector<int>(cur.begin(), cur.begin() + m), bb);
+    for (int pass = 0; pass < 4; ++pass) {
+      bool improved = false;
+      for (int a = 0; a < npos; ++a) {
+        for (int c = 0; c < nb; ++c) {
+          if (c == cur[a]) continue;
+          std::vector<int> o = cur;
+          auto it = std::find(o.begin(), o.end(), c);
+          const bool walk_same = a >= m && (it == o.end() || it - o.begin() >= m);
+          if (it != o.end()) std::swap(o[a], *it);
+          else o[a] = c;
+          // the skip first: one swap rarely cuts the ops by 15 %, so trials
+          // that could not win even then skip the op count (a storage fit)
+          const double keep = 1.0 - seg_skip_estimate(A, n, extend(o, count), m, kPolishSamples);
+          if (cur_ops * 0.85 * keep >= beff) continue;
+          const double ops = walk_same ? cur_ops : cost(std::vector<int>(o.begin(), o.begin() + m), bb);
+          if (ops >= 1e300) continue;
+          const double eff = ops * keep;
+          if (eff < beff - 1e-12) beff = eff, cur = o, cur_ops = ops, improved = true;
+        }
+      }
+      if (!improved) break;
+    }
+    bo = extend(cur, count);
+    return beff;
+  };
   if (integral && count >= m + std::min(6, nb - m)) {
     double beff = 1e300;
     std::vector<int> bo;
     int bb = cands[gi];
+    std::vector<std::tuple<double, int, std::vector<int>>> ranked;  // (eff, b, order)
     for (size_t ci = 0; ci < cands.size(); ++ci)
       for (const auto& fc : finals[ci]) {
         if (fc.first >= 1e300) continue;
         const std::vector<int> full = extend(fc.second, count);
-        const double eff = fc.first * (1.0 - seg_skip_estimate(A, n, full, m, 2048));
+        const double eff = fc.first * (1.0 - seg_skip_estimate(A, n, full, m, kPolishSamples));
         if (std::getenv("SUP_JIT_VERBOSE"))
           std::fprintf(stderr, "  candidate b=%d ops=%.4f skip=%.3f eff=%.4f\n", cands[ci], fc.first,
                        1.0 - eff / fc.first, eff);
+        ranked.emplace_back(eff, cands[ci], full);
         if (eff < beff - 1e-12) beff = eff, bo = full, bb = cands[ci];
       }
     if (!bo.empty()) {
-      // polish: swap descent of that b on ops x (1 - skip) (512 sampled
-      // chunks per candidate; SUP_JIT_POLISH=0 skips it).  Config 5 (n = 44
-      // d = 0.15 int): 56 % of the chunks skipped -> 87 %, at 1.42 instead
-      // of 1.30 ops per step
+      // polish: swap descent on ops x (1 - skip) (SUP_JIT_POLISH=0 skips
+      // it) of the kPolish best distinct
+      // candidates, one host thread each; the best result wins.  The descent
+      // is local and its end varies a lot with the start: on config 5 (n = 44
+      // d = 0.15 int) the 8 best candidates end at 0.20-0.53 ops per nominal
+      // step (best: 86 % of the chunks skipped at 1.40 ops per step).
+      // Every walk position and the lane columns (positions m .. m+L-1) are
+      // polished: the lanes cost no ops, and with the walk columns they
+      // decide which rows stay untouched (config 5: 0.205 -> 0.201 against
+      // the first 12 walk positions only).
       const char* pe = std::getenv("SUP_JIT_POLISH");
       if (!pe || std::atoi(pe) != 0) {
-        std::vector<int> cur(bo.begin(), bo.begin() + m);
-        for (int pass = 0; pass < 4; ++pass) {
-          bool improved = false;
-          for (int a = 0; a < std::min(m, 12); ++a)
-            for (int c = 0; c < nb; ++c) {
-              if (c == cur[a]) continue;
-              std::vector<int> o = cur;
-              auto it = std::find(o.begin(), o.end(), c);
-              if (it != o.end()) std::swap(o[a], *it);
-              else o[a] = c;
-              const double ops = cost(o, bb);
-              if (ops >= 1e300 || ops * 0.1 >= beff) continue;
-              const double eff = ops * (1.0 - seg_skip_estimate(A, n, extend(o, count), m, 512));
-              if (eff < beff - 1e-12) beff = eff, cur = o, improved = true;
-            }
-          if (!improved) break;
+        constexpr int kPolish = 4;
+        std::stable_sort(ranked.begin(), ranked.end(),
+                         [](const auto& x, const auto& y) { return std::get<0>(x) < std::get<0>(y); });
+        std::vector<std::tuple<double, int, std::vector<int>>> starts;
+        for (const auto& r : ranked) {
+          bool dup = false;
+          for (const auto& q : starts) dup |= std::get<1>(q) == std::get<1>(r) && std::get<2>(q) == std::get<2>(r);
+          if (!dup) starts.push_back(r);
+          if ((int)starts.size() == kPolish) break;
         }
-        bo = extend(cur, count);
+        std::vector<double> effs(starts.size());
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < starts.size(); ++i)
+          th.emplace_back([&, i] { effs[i] = polish(std::get<2>(starts[i]), std::get<1>(starts[i]), std::get<0>(starts[i])); });
+        for (auto& t : th) t.join();
+        if (std::getenv("SUP_JIT_VERBOSE"))
+          for (size_t i = 0; i < starts.size(); ++i) {
+            const std::vector<int>& o = std::get<2>(starts[i]);
+            const double ops = cost(std::vector<int>(o.begin(), o.begin() + m), std::get<1>(starts[i]));
+            std::fprintf(stderr, "  polished #%zu b=%d eff=%.4f ops=%.4f eff@16384=%.4f\n", i, std::get<1>(starts[i]),
+                         effs[i], ops, ops * (1.0 - seg_skip_estimate(A, n, o, m, 16384)));
+          }
+        size_t bi = 0;
+        for (size_t i = 1; i < starts.size(); ++i)
+          if (effs[i] < effs[bi] - 1e-12) bi = i;
+        beff = effs[bi], bb = std::get<1>(starts[bi]), bo = std::get<2>(starts[bi]);
         if (std::getenv("SUP_JIT_VERBOSE")) std::fprintf(stderr, "  polished eff=%.4f\n", beff);
       }
       if (b_out) *b_out = bb;
@@ -724,32 +777,47 @@ double seg_skip_estimate(const double* A, int n, const std::vector<int>& order, 
   double p0;
   nw_start(A, n, x0.data(), &p0);
   const int h = (int)high.size();
-  const int S = samples;
+  // Integer entries (x0 half-integers): every sum below is exact, so tail row
+  // r is zero in lane l iff its chunk value == -(its lane columns' sum over
+  // l).  Per row: its nonzero high-column entries and the distinct lane sums
+  // with the mask of lanes holding each; a chunk is skipped when the rows'
+  // zero-lane masks cover every lane.
+  struct Row {
+    double x0;
+    std::vector<std::pair<int, double>> hi;         // (chunk bit, entry)
+    std::vector<std::pair<double, uint64_t>> lane;  // (-lane sum, lanes)
+  };
+  const uint64_t all_lanes = L >= 6 ? ~0ull : (1ull << (1u << L)) - 1ull;
+  std::vector<Row> rows(tail.size());
+  for (size_t i = 0; i < tail.size(); ++i) {
+    const double* a = A + (size_t)tail[i] * n;
+    rows[i].x0 = x0[tail[i]];
+    for (int k = 0; k < h; ++k)
+      if (a[high[k]] != 0.0) rows[i].hi.push_back({k, a[high[k]]});
+    for (unsigned l = 0; l < (1u << L); ++l) {
+      double v = 0.0;
+      for (int e = 0; e < L; ++e)
+        if ((l >> e) & 1u) v += a[order[m + e]];
+      auto it = std::find_if(rows[i].lane.begin(), rows[i].lane.end(), [&](const auto& q) { return q.first == -v; });
+      if (it == rows[i].lane.end()) rows[i].lane.push_back({-v, 1ull << l});
+      else it->second |= 1ull << l;
+    }
+  }
   int skipped = 0;
-  std::vector<double> base(tail.size());
-  for (int s = 0; s < S; ++s) {
+  for (int s = 0; s < samples; ++s) {
     const uint64_t a = h ? ((uint64_t)s * 0x9E3779B97F4A7C15ull) >> (64 - std::min(h, 63)) : 0;
     const uint64_t g = a ^ (a >> 1);
-    for (size_t i = 0; i < tail.size(); ++i) {
-      double v = x0[tail[i]];
-      for (int k = 0; k < h; ++k)
-        if ((g >> k) & 1u) v += A[(size_t)tail[i] * n + high[k]];
-      base[i] = v;
+    uint64_t zero = 0;
+    for (size_t i = 0; i < rows.size() && zero != all_lanes; ++i) {
+      double v = rows[i].x0;
+      for (const auto& q : rows[i].hi)
+        if ((g >> q.first) & 1u) v += q.second;
+      for (const auto& q : rows[i].lane)
+        if (v == q.first) zero |= q.second;
     }
-    bool all = true;
-    for (unsigned lane = 0; lane < (1u << L) && all; ++lane) {
-      bool zero = false;
-      for (size_t i = 0; i < tail.size() && !zero; ++i) {
-        double v = base[i];
-        for (int e = 0; e < L; ++e)
-          if ((lane >> e) & 1u) v += A[(size_t)tail[i] * n + order[m + e]];
-        zero = v == 0.0;
-      }
-      all = zero;
-    }
-    skipped += all;
+    skipped += zero == all_lanes;
   }
-  return (double)skipped / S;
+  return (double)skipped / samples;
 }
 
 std::vector<int> seg_row_order(const double* A, int n, const std::vector<int>& walk) {
@@ -930,6 +998,17 @@ struct Gen {
     return opnd(ti, v, t.a[i], S, ks) + " * " + opnd(ti, v, t.b[i], S, ks);
   }
   uint32_t inner_root_csig() const { return P.inner_tree.root() < 0 ? 0u : csig(1, P.inner_tree.root()); }
+  // D = top_x - top_y of segment 0's tree; with a root node, the x root's
+  // product fuses with the subtraction: fma(x_a, x_b, -top_y) (one rounding;
+  // engine_cpu.cpp seg_D, oracle.c e_seg_D)
+  template <class Op>
+  std::string dexpr(Op op) const {
+    const ProdTree& t = P.inner_tree;
+    const int rt = t.root();
+    if (rt < t.items()) return op(0, rt) + " - " + op(1, rt);
+    const int i = rt - t.items();
+    return "__builtin_fma(" + op(0, t.a[i]) + ", " + op(0, t.b[i]) + ", -" + op(1, rt) + ")";
+  }
   std::string dname(uint32_t s) const { return "D" + std::to_string(s & inner_root_csig()); }
 
   // statements of a step of class c after its x^0 adds (same for every
@@ -959,9 +1038,9 @@ struct Gen {
     if ((P.inner_tree.root_sig() >> c) & 1u) {
       upd(1, 0);
       upd(1, 1);
-      const int rt = P.inner_tree.root();
       for (uint32_t S : submasks(inner_root_csig()))
-        st.push_back({dname(S) + " = " + opnd(1, 0, rt, S, &ks) + " - " + opnd(1, 1, rt, S, &ks) + ";"});
+        st.push_back({dname(S) + " = " +
+                      dexpr([&](int v, int id) { return opnd(1, v, id, S, &ks); }) + ";"});
     }
   }
 
@@ -1231,8 +1310,8 @@ struct Gen {
     tree_init(1, 1);
     if (P.inner_tree.root() >= 0)
       for (uint32_t S : submasks(inner_root_csig()))
-        o << "      double " << dname(S) << " = " << iopnd(1, 0, P.inner_tree.root(), S) << " - "
-          << iopnd(1, 1, P.inner_tree.root(), S) << ";\n";
+        o << "      double " << dname(S) << " = " << dexpr([&](int v, int id) { return iopnd(1, v, id, S); })
+          << ";\n";
     else
       o << "      double D0 = 0.0;\n";
     {

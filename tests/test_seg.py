@@ -179,7 +179,7 @@ def test_seg_pair_bits_chosen_by_cost(sup, monkeypatch):
 
 def test_seg_walk_length_rule(sup):
     """Cheap segmented walks run on longer wave-chunks (engine.cpp
-    make_seg_plan): a chunk's walk should cost >= 64 chunk starts, with at
+    make_seg_plan): a chunk's walk should cost >= 32 chunk starts, with at
     least 2^15 chunks left.  Measured on MI355X (profiles/r2/probe_walklen.log):
     config 3 2.94 -> 2.12 ms at m = 14, the d = 0.2 companion 36.1 -> 33.4 ms at
     m = 15; the bench matrix (12.7 ops per step) keeps m = 13."""
@@ -194,7 +194,7 @@ def test_seg_walk_length_rule(sup):
         assert info["kind"] == "seg" and info["L"] == 6 and lo <= info["m"] <= hi, (name, info["m"])
         assert n - 1 - 6 - info["m"] >= min(15, sup.layout(n)[2])
         if info["m"] > sup.layout(n)[1]:  # the walk's own steps now dwarf a chunk start, or the chunks ran out
-            assert info["est_ops_per_step"] * 2.0 ** info["m"] >= 64 * 1024 or n - 1 - 6 - info["m"] == 15
+            assert info["est_ops_per_step"] * 2.0 ** info["m"] >= 32 * 2048 or n - 1 - 6 - info["m"] == 15
 
 
 @pytest.mark.parametrize("n,d,seed", [(16, 0.5, 31), (18, 0.35, 32)])
