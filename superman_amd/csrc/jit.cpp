@@ -1141,6 +1141,45 @@ struct Gen {
       rp.push_back(pcs);
       i = j;
     }
+    // Accumulates (no pieces) that close a region float into the next one:
+    // their fma chain on acc is serial, and there the scheduler can interleave
+    // it with the next step's independent adds (same statements, same order
+    // of the chain: the bits do not change).  SUP_JIT_ACCFLOAT=0 disables.
+    static const bool accfloat =
+        std::getenv("SUP_JIT_ACCFLOAT") ? std::atoi(std::getenv("SUP_JIT_ACCFLOAT")) != 0 : true;
+    std::vector<std::vector<size_t>> order(reg.size());
+    for (size_t r = 0; r < reg.size(); ++r)
+      for (size_t i = reg[r].first; i < reg[r].second; ++i) order[r].push_back(i);
+    if (accfloat)
+      for (size_t r = 0; r + 1 < reg.size(); ++r) {
+        std::vector<size_t> tail;
+        while (!order[r].empty() && items[order[r].back()].step < 0 && items[order[r].back()].pieces.empty() &&
+               order[r].size() > 1) {
+          tail.insert(tail.begin(), order[r].back());
+          order[r].pop_back();
+        }
+        if (tail.empty()) continue;
+        // spread the chain over the next region's leading x^0 adds (they
+        // write no value an accumulate reads: D and the outer root are
+        // re-formed after them), one accumulate after every `gap` of them
+        size_t lead = 0;
+        while (lead < order[r + 1].size() && items[order[r + 1][lead]].text.compare(0, 2, "x[") == 0) ++lead;
+        if (lead == 0) {  // nothing to interleave with: keep them where they were
+          order[r].insert(order[r].end(), tail.begin(), tail.end());
+          continue;
+        }
+        std::vector<size_t> nx;
+        const size_t gap = std::max<size_t>(1, lead / (tail.size() + 1));
+        size_t t = 0;
+        for (size_t i = 0; i < order[r + 1].size(); ++i) {
+          if (i == lead)
+            while (t < tail.size()) nx.push_back(tail[t++]);
+          nx.push_back(order[r + 1][i]);
+          if (i < lead && t < tail.size() && (i + 1) % gap == 0) nx.push_back(tail[t++]);
+        }
+        while (t < tail.size()) nx.push_back(tail[t++]);
+        order[r + 1] = nx;
+      }
     auto pname = [&](size_t r, int pc) { return "s" + std::to_string(pc) + "_" + std::to_string(r); };
     auto load = [&](size_t r) {
       for (int pc : rp[r]) o << ind << "  jdbl8 " << pname(r, pc) << " = " << pieces[pc] << ";\n";
@@ -1156,7 +1195,7 @@ struct Gen {
     pin(0);
     for (size_t r = 0; r < reg.size(); ++r) {
       if (pf && r + 1 < reg.size()) load(r + 1);
-      for (size_t i = reg[r].first; i < reg[r].second; ++i) {
+      for (size_t i : order[r]) {
         const std::string& t = items[i].text;
         std::string out;
         for (size_t q = 0; q < t.size(); ++q) {

@@ -36,6 +36,7 @@ for step in "$@"; do
            prof_pmc pmc_write WRITE_SIZE
            prof_pmc pmc_sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT
            prof_pmc pmc_lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY;;
+    pmcsqc) run pmc_sqc 120 rocprofv3 --pmc SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM SQ_WAVE_CYCLES --kernel-trace -d "$OUT/pmc_sqc" -o run --output-format csv -- $BENCH1;;
     probe) run probe 300 python3 tools/probe.py;;
     pmc44) for k in sparse skip; do
              run "pmc44_sq_$k" 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace -d "$OUT/pmc44_sq_$k" -o run --output-format csv -- python3 tools/run_one.py synth44_0.15_int 2 $k
