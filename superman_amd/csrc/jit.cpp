@@ -40,10 +40,10 @@
 // D = prod_x - prod_y of segment 0 fuses the x root's product with the
 // subtraction into one fma (dexpr).
 //
-// Measured on MI355X (profiles/r2): n=40 d=0.5 bench matrix 12.3 VALU
-// instructions per Gray step (cost model 12.2; round 1 18.2; the prefix-
+// Measured on MI355X (profiles/r2): n=40 d=0.5 bench matrix 12.1 VALU
+// instructions per Gray step (cost model 11.9; round 1 18.2; the prefix-
 // blocked AOT walk executes 46.6, the plain dense walk 81), VALU 93% busy at 2
-// waves/SIMD, 2.94e12 steps/s.  Everything else (chunk start, lane layout,
+// waves/SIMD, 2.99e12 steps/s.  Everything else (chunk start, lane layout,
 // wave-chunk queue, reduction order) is walk_common.hpp's, shared with the
 // ahead-of-time kernels, and the arithmetic is mirrored bit for bit by
 // engine_cpu.cpp (tree_*, seg_*) and oracle/oracle.c (kind 3).
@@ -483,13 +483,22 @@ int seg_static_bits(int m) {
 double seg_walk_cost(const Plan& P) { return P.seg_ops; }
 
 // Greedy starts the walk-order descent runs from (SUP_JIT_STARTS overrides):
-// 8 when the plain walk would take a second or more on one MI355X (2n + 1 ops
+// 32 when the plain walk would take a second or more on one MI355X (2n + 1 ops
 // per Gray step at 3.7e13 lane-ops/s: n >= 40), else 3.  More starts find
 // cheaper walks (n = 40 bench matrix: 13.05 ops per step from 3 starts, 12.66
-// from 8) for ~2x the plan time (1.3 s -> 2.3 s).
+// from 8 before the fused D; after it 12.16 from 8 or 16, 11.93 from 32 or
+// 64); the descents run on plan_threads() host threads (32 starts: 1.7 s on 8).
+// Host threads for the plan's searches: the machine's, at most OMP_NUM_THREADS
+// (the GPU box's CPU share) and 16.
+int plan_threads() {
+  int t = (int)std::max(1u, std::thread::hardware_concurrency());
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) t = std::min(t, std::max(1, std::atoi(e)));
+  return std::min(t, 16);
+}
+
 int seg_search_starts(int n) {
   if (const char* e = std::getenv("SUP_JIT_STARTS")) return std::max(1, std::atoi(e));
-  return std::ldexp(1.0, n - 1) * (2.0 * n + 1.0) / 3.7e13 >= 1.0 ? 8 : 3;
+  return std::ldexp(1.0, n - 1) * (2.0 * n + 1.0) / 3.7e13 >= 1.0 ? 32 : 3;
 }
 
 std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b_out) {
@@ -539,82 +548,74 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
   std::vector<std::vector<int>> bests(cands.size());
   std::vector<std::vector<std::pair<double, std::vector<int>>>> finals(cands.size());
   std::vector<double> bcosts(cands.size(), 1e300);
-  auto search = [&](size_t ci) {
+  // phase 1, one host thread per b: greedy continuations from every first
+  // column, ranked by cost
+  std::vector<std::vector<std::pair<double, std::vector<int>>>> starts(cands.size());
+  auto rank_starts = [&](size_t ci) {
     const int b = cands[ci];
-    // greedy continuations from every first column, the few cheapest kept
-    std::vector<std::pair<double, std::vector<int>>> starts;
     for (int f = 0; f < nb; ++f) {
       std::vector<int> o = extend({f}, m);
-      starts.push_back({cost(o, b), std::move(o)});
+      starts[ci].push_back({cost(o, b), std::move(o)});
     }
-    std::stable_sort(starts.begin(), starts.end(),
+    std::stable_sort(starts[ci].begin(), starts[ci].end(),
                      [](const std::pair<double, std::vector<int>>& x, const std::pair<double, std::vector<int>>& y) {
                        return x.first < y.first;
                      });
-    // descent from each: swap a walk position with another walk position or
-    // an unused column while the cost drops (positions whose weight 2^-(k+1)
-    // is visible); every result is a final candidate
-    const int hot = std::min(m, 12);
-    std::vector<int> best;
-    double bcost = 1e300;
-    const size_t nstart = std::min(starts.size(), (size_t)seg_search_starts(n));
-    finals[ci].clear();
-    for (size_t si = 0; si < nstart; ++si) {
-      std::vector<int> cur = starts[si].second;
-      double ccost = starts[si].first;
-      for (int pass = 0; pass < 8 && ccost < 1e300; ++pass) {
-        bool improved = false;
-        for (int a = 0; a < hot; ++a) {
-          for (int c = 0; c < nb; ++c) {
-            if (c == cur[a]) continue;
-            std::vector<int> o = cur;
-            auto it = std::find(o.begin(), o.end(), c);
-            if (it != o.end()) std::swap(o[a], *it);
-            else o[a] = c;
-            const double v = cost(o, b);
-            if (v < ccost - 1e-12) ccost = v, cur = o, improved = true;
-          }
-        }
-        if (!improved) break;
-      }
-      if (best.empty() || ccost < bcost - 1e-12) bcost = ccost, best = cur;
-      finals[ci].push_back({ccost, cur});
-    }
-    if (const char* e = std::getenv("SUP_JIT_ANNEAL")) {  // experiment: simulated annealing on the order
-      const int iters = std::atoi(e);
-      uint64_t rs = 0x9E3779B97F4A7C15ull ^ (uint64_t)b;
-      auto rnd = [&]() { rs ^= rs << 13; rs ^= rs >> 7; rs ^= rs << 17; return rs; };
-      std::vector<int> cur = best;
-      std::vector<char> inw(n, 0);
-      double ccost = bcost;
-      for (int it = 0; it < iters; ++it) {
-        const double T = 0.02 * bcost * (1.0 - (double)it / iters);
-        std::vector<int> o = cur;
-        const int a = (int)(rnd() % m);
-        if (rnd() & 1) {
-          const int c2 = (int)(rnd() % m);
-          std::swap(o[a], o[c2]);
-        } else {
-          std::fill(inw.begin(), inw.end(), 0);
-          for (int k = 0; k < m; ++k) inw[o[k]] = 1;
-          int c = (int)(rnd() % nb);
-          if (inw[c]) continue;
-          o[a] = c;
-        }
-        const double v = cost(o, b);
-        const double u = (double)(rnd() >> 11) * (1.0 / 9007199254740992.0);
-        if (v < ccost || (T > 0 && u < std::exp((ccost - v) / T))) cur = o, ccost = v;
-        if (ccost < bcost - 1e-12) bcost = ccost, best = cur;
-      }
-    }
-    bests[ci] = std::move(best);
-    bcosts[ci] = bcost;
   };
   {
     std::vector<std::thread> th;
-    for (size_t ci = 1; ci < cands.size(); ++ci) th.emplace_back(search, ci);
-    search(0);
+    for (size_t ci = 1; ci < cands.size(); ++ci) th.emplace_back(rank_starts, ci);
+    rank_starts(0);
     for (auto& t : th) t.join();
+  }
+  // phase 2: a descent from each of the seg_search_starts(n) cheapest starts
+  // of every b — swap a walk position with another walk position or an unused
+  // column while the cost drops (positions whose weight 2^-(k+1) is visible) —
+  // as independent tasks on a pool of host threads; every result is a final
+  // candidate (deterministic: gathered in (b, start) order)
+  const int hot = std::min(m, 12);
+  const size_t nstart = std::min((size_t)nb, (size_t)seg_search_starts(n));
+  std::vector<std::pair<size_t, size_t>> tasks;
+  for (size_t si = 0; si < nstart; ++si)
+    for (size_t ci = 0; ci < cands.size(); ++ci) tasks.push_back({ci, si});
+  std::vector<std::pair<double, std::vector<int>>> results(tasks.size());
+  auto descend = [&](size_t ti) {
+    const size_t ci = tasks[ti].first, si = tasks[ti].second;
+    const int b = cands[ci];
+    std::vector<int> cur = starts[ci][si].second;
+    double ccost = starts[ci][si].first;
+    for (int pass = 0; pass < 8 && ccost < 1e300; ++pass) {
+      bool improved = false;
+      for (int a = 0; a < hot; ++a) {
+        for (int c = 0; c < nb; ++c) {
+          if (c == cur[a]) continue;
+          std::vector<int> o = cur;
+          auto it = std::find(o.begin(), o.end(), c);
+          if (it != o.end()) std::swap(o[a], *it);
+          else o[a] = c;
+          const double v = cost(o, b);
+          if (v < ccost - 1e-12) ccost = v, cur = o, improved = true;
+        }
+      }
+      if (!improved) break;
+    }
+    results[ti] = {ccost, std::move(cur)};
+  };
+  {
+    std::atomic<size_t> next{0};
+    auto worker = [&]() {
+      for (size_t ti = next++; ti < tasks.size(); ti = next++) descend(ti);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < std::min<int>(plan_threads(), (int)tasks.size()); ++t) th.emplace_back(worker);
+    worker();
+    for (auto& t : th) t.join();
+  }
+  for (size_t ci = 0; ci < cands.size(); ++ci) finals[ci].clear();
+  for (size_t ti = 0; ti < tasks.size(); ++ti) {
+    const size_t ci = tasks[ti].first;
+    if (bests[ci].empty() || results[ti].first < bcosts[ci] - 1e-12) bcosts[ci] = results[ti].first, bests[ci] = results[ti].second;
+    finals[ci].push_back(results[ti]);
   }
   size_t gi = 0;
   for (size_t ci = 1; ci < cands.size(); ++ci)
@@ -629,13 +630,18 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
   // final eff and leaves the order in bo.  512 samples overfit: on config 5
   // the descent's best at 512 (0.176 ops per nominal step) measured 0.216.
   constexpr int kPolishSamples = 8192;
+  constexpr int kPolishEvals = 48;
   auto polish = [&](std::vector<int>& bo, int bb, double beff) {
     const int npos = std::min(count, m + std::min(6, nb - m));
     std::vector<int> cur(bo.begin(), bo.begin() + npos);
     double cur_ops = cost(std::vector<int>(cur.begin(), cur.begin() + m), bb);
-    for (int pass = 0; pass < 4; ++pass) {
-      bool improved = false;
-      for (int a = 0; a < npos; ++a) {
+    // best-improvement passes: every swap's skip first (2048 samples), then
+    // for the kPolishEvals most promising by the optimistic bound 0.85 x ops
+    // x (1 - skip) (one swap rarely cuts the ops by 15 %) the op count (a
+    // storage fit) and the skip on all samples
+    for (int pass = 0; pass < 16; ++pass) {
+      std::vector<std::tuple<double, bool, std::vector<int>>> trials;  // (1 - skip, walk unchanged, order)
+      for (int a = 0; a < npos; ++a)
         for (int c = 0; c < nb; ++c) {
           if (c == cur[a]) continue;
           std::vector<int> o = cur;
@@ -643,17 +649,23 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
           const bool walk_same = a >= m && (it == o.end() || it - o.begin() >= m);
           if (it != o.end()) std::swap(o[a], *it);
           else o[a] = c;
-          // the skip first: one swap rarely cuts the ops by 15 %, so trials
-          // that could not win even then skip the op count (a storage fit)
-          const double keep = 1.0 - seg_skip_estimate(A, n, extend(o, count), m, kPolishSamples);
-          if (cur_ops * 0.85 * keep >= beff) continue;
-          const double ops = walk_same ? cur_ops : cost(std::vector<int>(o.begin(), o.begin() + m), bb);
-          if (ops >= 1e300) continue;
-          const double eff = ops * keep;
-          if (eff < beff - 1e-12) beff = eff, cur = o, cur_ops = ops, improved = true;
+          trials.emplace_back(1.0 - seg_skip_estimate(A, n, extend(o, count), m, kPolishSamples / 4), walk_same,
+                              std::move(o));
         }
+      std::stable_sort(trials.begin(), trials.end(),
+                       [](const auto& x, const auto& y) { return std::get<0>(x) < std::get<0>(y); });
+      double best = beff;
+      int bi = -1;
+      double bops = cur_ops;
+      for (size_t t = 0; t < trials.size() && (int)t < kPolishEvals; ++t) {
+        if (cur_ops * 0.85 * std::get<0>(trials[t]) >= best) break;
+        const std::vector<int>& o = std::get<2>(trials[t]);
+        const double keep = 1.0 - seg_skip_estimate(A, n, extend(o, count), m, kPolishSamples);
+        const double ops = std::get<1>(trials[t]) ? cur_ops : cost(std::vector<int>(o.begin(), o.begin() + m), bb);
+        if (ops < 1e300 && ops * keep < best - 1e-12) best = ops * keep, bi = (int)t, bops = ops;
       }
-      if (!improved) break;
+      if (bi < 0) break;
+      beff = best, cur = std::get<2>(trials[bi]), cur_ops = bops;
     }
     bo = extend(cur, count);
     return beff;
@@ -679,8 +691,8 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
       // it) of the kPolish best distinct
       // candidates, one host thread each; the best result wins.  The descent
       // is local and its end varies a lot with the start: on config 5 (n = 44
-      // d = 0.15 int) the 8 best candidates end at 0.20-0.53 ops per nominal
-      // step (best: 86 % of the chunks skipped at 1.40 ops per step).
+      // d = 0.15 int) the best candidates end at 0.19-0.49 ops per nominal
+      // step (best: ~87 % of the chunks skipped at ~1.5 ops per step).
       // Every walk position and the lane columns (positions m .. m+L-1) are
       // polished: the lanes cost no ops, and with the walk columns they
       // decide which rows stay untouched (config 5: 0.205 -> 0.201 against
