@@ -91,14 +91,16 @@ typedef struct {
   int cpu_worker;     /* -c together with -g: a CPU thread also takes chunks                 */
   int grid_dim;       /* 0 = auto (resident-wave sized); reference default 2048              */
   int block_dim;      /* 0 = auto (256); the engine only supports 256                         */
-  int walk_log2;      /* 0 = auto; Gray steps walked per wave-chunk = 2^walk_log2            */
+  int walk_log2;      /* 0 = auto (the segmented walk lengthens its wave-chunks where its    */
+                      /*  steps are cheap); else each lane walks 2^walk_log2 Gray steps per  */
+                      /*  wave-chunk (sup_perman, sup_perman_shard, sup_plan_info)           */
   int chunk_log2;     /* 0 = auto; for SUP_SCHED_CHUNKS: wave-chunks per queue item = 2^x    */
   int use_rccl;       /* 1: multi-device partials combined by one RCCL all-reduce (bit-     */
                       /*    identical to the host combine); 2: also with a single device    */
   int verbose;        /* print per-device / per-chunk timing lines like the reference        */
   int jit;            /* segmented walk specialised for the matrix pattern (hiprtc, gfx950):  */
                       /*  -1 never; 0 auto: when its cost model wins and the predicted walk  */
-                      /*  time saved exceeds 3 s (plan 0.1-2.5 s + compile ~0.5 s, both once*/
+                      /*  time saved exceeds 3 s (plan 0.2-6 s + compile ~0.5 s, both once  */
                       /*  per matrix: plans cached in memory, code objects also on disk); 1  */
                       /*  whenever its cost model wins                                       */
 } sup_opts;

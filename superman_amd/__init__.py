@@ -192,7 +192,8 @@ def perman_shard(mat, shard: int, nshards: int, kernel: str = "dense", device_id
     return (out.value, st.as_dict()) if return_stats else out.value
 
 
-def plan_info(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_id: int = 0) -> dict:
+def plan_info(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_id: int = 0,
+              walk_log2: int = 0) -> dict:
     """The plan the engine runs for `kernel` (and options jit / gpu_num): walk
     kind, column map, layout, cost model (fp64 ops per Gray step), cached walk
     bits and specialised pair bits of the segmented walk.  A SkipPer
@@ -202,14 +203,15 @@ def plan_info(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device
     kind, L, m, cc, pb = C.c_int(), C.c_int(), C.c_int(), C.c_int(), C.c_int()
     ops = C.c_double(0.0)
     cm = np.zeros(max(n - 1, 1), np.int32)
-    o = _opts(gpu_num=gpu_num, device_id=device_id, jit=jit)
+    o = _opts(gpu_num=gpu_num, device_id=device_id, jit=jit, walk_log2=walk_log2)
     _lib.check(lib.sup_plan_info(a.ctypes.data, dt, n, _KERNELS[kernel], C.byref(o), C.byref(kind), cm.ctypes.data,
                                  C.byref(L), C.byref(m), C.byref(cc), C.byref(pb), C.byref(ops)), "plan_info")
     return {"kind": WALK_NAMES[kind.value], "colmap": cm[: n - 1].copy(), "L": L.value, "m": m.value,
             "cached": cc.value, "pair_bits": pb.value, "est_ops_per_step": ops.value}
 
 
-def prepare(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_id: int = 0) -> dict:
+def prepare(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_id: int = 0,
+            walk_log2: int = 0) -> dict:
     """Plan `mat` as perman / perman_shard would and compile the segmented
     walk's specialised kernel now if the plan uses it (hiprtc, no device
     needed): {"kind": walk name, "compile_ms": hiprtc time (0 when cached)}.
@@ -217,7 +219,7 @@ def prepare(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_i
     a, dt, n = _mat(mat)
     lib = _lib.load()
     kind, ms = C.c_int(), C.c_double(0.0)
-    o = _opts(gpu_num=gpu_num, device_id=device_id, jit=jit)
+    o = _opts(gpu_num=gpu_num, device_id=device_id, jit=jit, walk_log2=walk_log2)
     _lib.check(lib.sup_prepare(a.ctypes.data, dt, n, _KERNELS[kernel], C.byref(o), C.byref(kind), C.byref(ms)),
                "prepare")
     return {"kind": WALK_NAMES[kind.value], "compile_ms": ms.value}

@@ -302,7 +302,8 @@ int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const 
   if (o_in) o = *o_in;
   else sup_opts_init(&o);
   Plan P;
-  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num, o.device_id))) return rc;
+  if ((rc = check_walk_opts(o))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, layout_for(n, o), P, o.jit, o.gpu_num, o.device_id))) return rc;
   if (walk_kind) *walk_kind = P.lds ? 4 : (int)P.kind;
   if (cached_bits) *cached_bits = P.kind == kWalkSeg ? P.seg_cc : 0;
   if (pair_bits) *pair_bits = P.kind == kWalkSeg ? P.seg_b : 0;
@@ -323,7 +324,8 @@ int sup_prepare(const void* mat, sup_dtype t, int n, sup_kernel kernel, const su
   if (o_in) o = *o_in;
   else sup_opts_init(&o);
   Plan P;
-  if ((rc = plan_for(A.data(), n, kernel, default_layout(n), P, o.jit, o.gpu_num, o.device_id))) return rc;
+  if ((rc = check_walk_opts(o))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, layout_for(n, o), P, o.jit, o.gpu_num, o.device_id))) return rc;
   if (walk_kind) *walk_kind = P.lds ? 4 : (int)P.kind;
   if (compile_ms) *compile_ms = 0.0;
   if (P.kind == kWalkSeg) return jit_compile_only(P, compile_ms);
