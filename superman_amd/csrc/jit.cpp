@@ -1157,8 +1157,7 @@ struct Gen {
     // their fma chain on acc is serial, and there the scheduler can interleave
     // it with the next step's independent adds (same statements, same order
     // of the chain: the bits do not change).  SUP_JIT_ACCFLOAT=0 disables.
-    static const bool accfloat =
-        std::getenv("SUP_JIT_ACCFLOAT") ? std::atoi(std::getenv("SUP_JIT_ACCFLOAT")) != 0 : true;
+    const bool accfloat = std::getenv("SUP_JIT_ACCFLOAT") ? std::atoi(std::getenv("SUP_JIT_ACCFLOAT")) != 0 : true;
     std::vector<std::vector<size_t>> order(reg.size());
     for (size_t r = 0; r < reg.size(); ++r)
       for (size_t i = reg[r].first; i < reg[r].second; ++i) order[r].push_back(i);

@@ -229,3 +229,19 @@ def test_seg_storage_plan_invariance_gpu(sup, orc, monkeypatch):
             assert sup.perman(a, algo=4, kernel="seg") == want, (n, budget)
         monkeypatch.delenv("SUP_JIT_STORAGE")
         assert sup.perman(a, algo=4, kernel="seg") == want, n
+
+
+def test_seg_codegen_schedule_invariance_gpu(sup, orc, monkeypatch):
+    """Scheduling-only code generation choices keep every bit: accumulate chains
+    floated into the next region or not (SUP_JIT_ACCFLOAT), step regions of 1,
+    2 or 4 SGPR pieces (SUP_JIT_KP); all equal to the oracle mirror."""
+    rng = np.random.default_rng(91)
+    n = 28
+    a = np.where(rng.random((n, n)) < 0.5, rng.random((n, n)) * 5, 0.0)
+    a[np.arange(n), rng.permutation(n)] = 1.0
+    want = orc.engine_perman_as(sup, a, "seg", threads=16)
+    for knob, vals in (("SUP_JIT_ACCFLOAT", ("0", "1")), ("SUP_JIT_KP", ("1", "2", "4"))):
+        for v in vals:
+            monkeypatch.setenv(knob, v)
+            assert sup.perman(a, algo=4, kernel="seg") == want, (knob, v)
+        monkeypatch.delenv(knob)
