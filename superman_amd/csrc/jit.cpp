@@ -1435,6 +1435,15 @@ struct Gen {
 const char* const kJitOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
 constexpr int kJitNopts = 4;
 
+// hiprtc options: kJitOpts, plus the LLVM machine scheduler strategy
+// SUP_JIT_SCHED names (experiments: max-ilp, max-memory-clause, ...).
+std::vector<std::string> jit_opts() {
+  std::vector<std::string> v(kJitOpts, kJitOpts + kJitNopts);
+  if (const char* e = std::getenv("SUP_JIT_SCHED"))
+    if (*e) v.push_back("-mllvm"), v.push_back(std::string("-amdgpu-sched-strategy=") + e);
+  return v;
+}
+
 uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
   for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
   return h;
@@ -1561,7 +1570,7 @@ int build_seg(Plan& P) {
     P.jtab.insert(P.jtab.end(), t.begin(), t.end());
   }
   std::string key = P.jit_src;
-  for (int i = 0; i < kJitNopts; ++i) key += std::string("\n//") + kJitOpts[i];
+  for (const std::string& opt : jit_opts()) key += "\n//" + opt;
   key += std::string("\n//") + kWalkCommonSrc + kWalkParamsSrc;
   P.jit_key = fnv1a(key);
   return SUP_OK;
@@ -1657,7 +1666,10 @@ int compile(const Plan& P, std::shared_ptr<std::vector<char>>& code) {
       set_error("hiprtcCreateProgram failed");
       return SUP_EHIP;
     }
-    const hiprtcResult cr = hiprtcCompileProgram(prog, kJitNopts, kJitOpts);
+    const std::vector<std::string> opts = jit_opts();
+    std::vector<const char*> optp;
+    for (const std::string& x : opts) optp.push_back(x.c_str());
+    const hiprtcResult cr = hiprtcCompileProgram(prog, (int)optp.size(), optp.data());
     if (cr == HIPRTC_SUCCESS) break;
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);
