@@ -325,10 +325,13 @@ int sup_prepare(const void* mat, sup_dtype t, int n, sup_kernel kernel, const su
   else sup_opts_init(&o);
   Plan P;
   if ((rc = check_walk_opts(o))) return rc;
+  // compiles may already happen while planning (the live-value budget is
+  // checked against the compiler), so the time is taken around both
+  const double before = jit_compile_ms_total();
   if ((rc = plan_for(A.data(), n, kernel, layout_for(n, o), P, o.jit, o.gpu_num, o.device_id))) return rc;
   if (walk_kind) *walk_kind = P.lds ? 4 : (int)P.kind;
-  if (compile_ms) *compile_ms = 0.0;
-  if (P.kind == kWalkSeg) return jit_compile_only(P, compile_ms);
+  if (P.kind == kWalkSeg && (rc = jit_compile_only(P, nullptr))) return rc;
+  if (compile_ms) *compile_ms = jit_compile_ms_total() - before;
   return SUP_OK;
 }
 

@@ -148,6 +148,9 @@ int jit_occupancy(int dev, const Plan& P, int* blocks_per_cu, double* compile_ms
 int jit_launch(int dev, const Plan& P, const WalkParams& p, int grid, hipStream_t s);
 // Compile (or find in the caches) the specialised kernel of P without loading it.
 int jit_compile_only(const Plan& P, double* compile_ms);
+// Compile (or fetch) P's kernel and read its VGPR count and VGPR spill count
+// from the code object's metadata.
+int jit_code_regs(const Plan& P, int* vgprs, int* vgpr_spills);
 // Milliseconds spent compiling specialised kernels in this process (hiprtc).
 double jit_compile_ms_total();
 

@@ -82,6 +82,7 @@
 #include <mutex>
 #include <sstream>
 #include <tuple>
+#include <string_view>
 #include <thread>
 
 #include "engine.hpp"
@@ -401,16 +402,16 @@ SegFit seg_fit(const SegRows& R, int cc, int budget, int budget_hi = -1, SegFit*
 // Best number of cached classes (0 .. min(kMaxCachedBits, b-1)) within the
 // register budget.
 std::atomic<long> g_fit_calls{0};  // planning effort (SUP_JIT_VERBOSE)
-SegFit seg_best(const SegRows& R, int cc_max = kMaxCachedBits) {
+SegFit seg_best(const SegRows& R, int cc_max = kMaxCachedBits, int regs_max = kRegsMax) {
   ++g_fit_calls;
   SegFit best;
   double bscore = 1e300;
   for (int cc = 0; cc <= std::min(cc_max, std::max(0, R.b - 1)); ++cc) {
     SegFit hi;
-    SegFit lo = seg_fit(R, cc, kRegs3, kRegsMax, &hi);  // one greedy: both budgets' plans
+    SegFit lo = seg_fit(R, cc, kRegs3, regs_max, &hi);  // one greedy: both budgets' plans
     for (SegFit* f : {&lo, &hi}) {
-      if (f->regs > kRegsMax && cc > 0) continue;
-      const double score = f->ops * (f->regs <= kRegs3 ? 1.0 : kOcc2Penalty) * (f->regs > kRegsMax ? 2.0 : 1.0);
+      if (f->regs > regs_max && cc > 0) continue;
+      const double score = f->ops * (f->regs <= kRegs3 ? 1.0 : kOcc2Penalty) * (f->regs > regs_max ? 2.0 : 1.0);
       if (score < bscore) bscore = score, best = std::move(*f);
     }
   }
@@ -1525,54 +1526,104 @@ int build_seg(Plan& P) {
     for (int j = 0; j < n; ++j)
       if (in[j]) P.dyn_rows.push_back(j);
   }
-  {  // product trees and cached classes (seg_best; SUP_JIT_CC forces cc, experiments)
-    SegRows R;
-    R.n = n, R.m = m, R.touched = P.touched;
-    R.len0 = P.seg_start[1], R.s_end = P.sub_start.back(), R.r_end = P.seg_start.back();
-    seg_rows_finish(R, P.seg_b);
+  // product trees, cached classes and storage plan for a live-value budget,
+  // then the tables and the generated source
+  SegRows SR;
+  SR.n = n, SR.m = m, SR.touched = P.touched;
+  SR.len0 = P.seg_start[1], SR.s_end = P.sub_start.back(), SR.r_end = P.seg_start.back();
+  seg_rows_finish(SR, P.seg_b);
+  auto finish = [&](int budget) {
     SegFit f;
     // experiments / tests: SUP_JIT_CC forces cc; SUP_JIT_STORAGE forces the
     // storage budget of the chosen plan (same walk order and trees, other
     // live/on-demand choices: the same values, so bit-identical results)
     if (const char* e = std::getenv("SUP_JIT_CC"))
-      f = seg_fit(R, std::max(0, std::min({std::atoi(e), R.b - 1, kMaxCachedBits})), kRegsMax);
-    else f = seg_best(R);
-    if (const char* e = std::getenv("SUP_JIT_STORAGE")) f = seg_fit(R, f.cc, std::max(0, std::atoi(e)));
+      f = seg_fit(SR, std::max(0, std::min({std::atoi(e), SR.b - 1, kMaxCachedBits})), budget);
+    else f = seg_best(SR, kMaxCachedBits, budget);
+    if (const char* e = std::getenv("SUP_JIT_STORAGE")) f = seg_fit(SR, f.cc, std::max(0, std::atoi(e)));
     P.outer_tree = std::move(f.outer);
     P.inner_tree = std::move(f.inner);
     P.seg_cc = f.cc;
     P.seg_ops = f.ops;
-    P.seg_skip = seg_skip_fraction_plan(P, 2048);
     P.seg_regs = f.regs;
-    if (std::getenv("SUP_JIT_VERBOSE"))
-      std::fprintf(stderr, "seg plan n=%d m=%d b=%d ops/step=%.4f regs=%d cc=%d (storage plans evaluated: %ld)\n", n,
-                   m, P.seg_b, f.ops, f.regs, f.cc, g_fit_calls.load());
-  }
-  P.jofs.assign(m, 0);
-  P.jtab.clear();
-  for (int k = 0; k < m; ++k) {
-    const std::vector<int>& t = P.touched[k];
-    const size_t blk = (t.size() + 7) & ~(size_t)7;
-    P.jofs[k] = (int)P.jtab.size();
-    P.jtab.resize(P.jtab.size() + 2 * std::max<size_t>(blk, 8), 0.0);
-    for (size_t i = 0; i < t.size(); ++i) {
-      P.jtab[P.jofs[k] + i] = P.cols[(size_t)(2 * (L + k)) * P.NP + t[i]];
-      P.jtab[P.jofs[k] + blk + i] = P.cols[(size_t)(2 * (L + k) + 1) * P.NP + t[i]];
+    P.jofs.assign(m, 0);
+    P.jtab.clear();
+    for (int k = 0; k < m; ++k) {
+      const std::vector<int>& t = P.touched[k];
+      const size_t blk = (t.size() + 7) & ~(size_t)7;
+      P.jofs[k] = (int)P.jtab.size();
+      P.jtab.resize(P.jtab.size() + 2 * std::max<size_t>(blk, 8), 0.0);
+      for (size_t i = 0; i < t.size(); ++i) {
+        P.jtab[P.jofs[k] + i] = P.cols[(size_t)(2 * (L + k)) * P.NP + t[i]];
+        P.jtab[P.jofs[k] + blk + i] = P.cols[(size_t)(2 * (L + k) + 1) * P.NP + t[i]];
+      }
     }
+    P.seg_cbase = P.jtab.size();
+    P.seg_kp = 4;
+    if (const char* e = std::getenv("SUP_JIT_KP")) P.seg_kp = std::max(1, std::atoi(e));
+    Gen g(P);
+    P.jit_src = g.source();
+    {
+      const std::vector<double> t = g.tail();
+      P.jtab.insert(P.jtab.end(), t.begin(), t.end());
+    }
+    std::string key = P.jit_src;
+    for (const std::string& opt : jit_opts()) key += "\n//" + opt;
+    key += std::string("\n//") + kWalkCommonSrc + kWalkParamsSrc;
+    P.jit_key = fnv1a(key);
+  };
+  int budget = kRegsMax;
+  finish(budget);
+  // The live-value budget against the compiler (long walks only: up to ~5
+  // hiprtc compiles of ~0.5-1 s, cached).  The estimate is rough (at 170 the
+  // n = 40 bench kernel fits 256 VGPRs with 6 chunk-level spills, denser or
+  // larger matrices spill inside the walk loop), so the compiled code object's
+  // VGPR spill count decides: from the default, larger budgets (fewer ops)
+  // while their kernels spill at most kSpillOk VGPRs — the fewest ops wins;
+  // if the default spills more, smaller budgets until one does not.
+  // Measured (n = 40 bench matrix, profiles/r2/probe_regmax_sched.log): 170
+  // -> 11.93 ops, 188.5 ms; 190 -> 11.56, 181.8 ms; 200 -> 11.44 (17 spilled
+  // VGPRs, one scratch access in the loop), 179.0 ms; 210 -> 11.53, 183.2 ms.
+  const bool fixed = std::getenv("SUP_JIT_REGMAX") || std::getenv("SUP_JIT_STORAGE") || std::getenv("SUP_JIT_CC") ||
+                     std::getenv("SUP_JIT_NOVERIFY");
+  const double walk_s = std::ldexp(1.0, n - 1) * P.seg_ops / 3.7e13;
+  if (!fixed && walk_s >= 0.05 && P.seg_regs > kRegs3) {
+    constexpr int kSpillOk = 20;
+    auto spills = [&]() {
+      int vgpr = 0, sp = 0;
+      return jit_code_regs(P, &vgpr, &sp) == SUP_OK ? sp : 1 << 20;
+    };
+    const int s0 = spills();
+    // a kernel the register allocator gives up on (some dense n >= 46
+    // patterns): no segmented plan, callers fall back to the ahead-of-time
+    // walks.  No further compile is tried: hiprtc has crashed on the next
+    // program after such a failure.
+    if (s0 >= (1 << 20)) return SUP_EHIP;
+    int best_b = budget;
+    double best_ops = P.seg_ops;
+    if (s0 <= kSpillOk) {
+      for (int b2 = budget + 10; b2 <= budget + 40; b2 += 10) {
+        finish(b2);
+        if (P.seg_ops < best_ops - 1e-9 && spills() <= kSpillOk) best_ops = P.seg_ops, best_b = b2;
+      }
+    } else {
+      // the fewest spills if none gets under kSpillOk
+      int fewest = s0;
+      for (int b2 = budget - 20; b2 >= kRegs3 && fewest > kSpillOk; b2 -= 20) {
+        finish(b2);
+        const int sp = spills();
+        if (sp < fewest) fewest = sp, best_b = b2;
+      }
+      if (fewest >= (1 << 20)) return SUP_EHIP;
+    }
+    if (std::getenv("SUP_JIT_VERBOSE"))
+      std::fprintf(stderr, "seg budget %d: default %d spilled %d VGPRs\n", best_b, budget, s0);
+    if (best_b != budget || P.seg_ops != best_ops) finish(best_b);
   }
-  P.seg_cbase = P.jtab.size();
-  P.seg_kp = 4;
-  if (const char* e = std::getenv("SUP_JIT_KP")) P.seg_kp = std::max(1, std::atoi(e));
-  Gen g(P);
-  P.jit_src = g.source();
-  {
-    const std::vector<double> t = g.tail();
-    P.jtab.insert(P.jtab.end(), t.begin(), t.end());
-  }
-  std::string key = P.jit_src;
-  for (const std::string& opt : jit_opts()) key += "\n//" + opt;
-  key += std::string("\n//") + kWalkCommonSrc + kWalkParamsSrc;
-  P.jit_key = fnv1a(key);
+  P.seg_skip = seg_skip_fraction_plan(P, 2048);
+  if (std::getenv("SUP_JIT_VERBOSE"))
+    std::fprintf(stderr, "seg plan n=%d m=%d b=%d ops/step=%.4f regs=%d cc=%d (storage plans evaluated: %ld)\n", n, m,
+                 P.seg_b, P.seg_ops, P.seg_regs, P.seg_cc, g_fit_calls.load());
   return SUP_OK;
 }
 
@@ -1743,6 +1794,42 @@ int jit_compile_only(const Plan& P, double* compile_ms) {
   }
   if (compile_ms) *compile_ms = jit_compile_ms_total() - before;
   return rc;
+}
+
+// Unsigned msgpack value after the map key `key` in the code object's
+// metadata note (fixstr key; fixint / uint8-32 value); -1 if absent.
+static long code_meta(const std::vector<char>& co, const std::string& key) {
+  if (key.size() >= 32) return -1;
+  std::string pat(1, (char)(0xa0 | key.size()));
+  pat += key;
+  const std::string_view sv(co.data(), co.size());
+  const size_t at = sv.find(pat);
+  if (at == std::string_view::npos || at + pat.size() >= co.size()) return -1;
+  const unsigned char* v = (const unsigned char*)co.data() + at + pat.size();
+  const size_t left = co.size() - at - pat.size();
+  if (v[0] < 0x80) return v[0];
+  if (v[0] == 0xcc && left >= 2) return v[1];
+  if (v[0] == 0xcd && left >= 3) return (v[1] << 8) | v[2];
+  if (v[0] == 0xce && left >= 5) return ((long)v[1] << 24) | (v[2] << 16) | (v[3] << 8) | v[4];
+  return -1;
+}
+
+int jit_code_regs(const Plan& P, int* vgprs, int* vgpr_spills) {
+  std::shared_ptr<std::vector<char>> code;
+  int rc;
+  {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    rc = compile(P, code);
+  }
+  if (rc) return rc;
+  const long v = code_meta(*code, ".vgpr_count"), sp = code_meta(*code, ".vgpr_spill_count");
+  if (v < 0 || sp < 0) {
+    set_error("segmented walk: no register counts in the code object's metadata");
+    return SUP_EHIP;
+  }
+  if (vgprs) *vgprs = (int)v;
+  if (vgpr_spills) *vgpr_spills = (int)sp;
+  return SUP_OK;
 }
 
 int jit_occupancy(int dev, const Plan& P, int* blocks_per_cu, double* compile_ms) {

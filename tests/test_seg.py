@@ -93,7 +93,7 @@ def test_generated_kernel_compiles(sup, case, tmp_path, monkeypatch):
     info = sup.prepare(a, "seg")
     assert info["kind"] == "seg"
     assert info["compile_ms"] > 0.0
-    assert len(list(tmp_path.glob("seg_*.co"))) == 1  # disk cache written
+    assert len(list(tmp_path.glob("seg_*.co"))) >= 1  # disk cache written (one per budget the plan compiled)
     again = sup.prepare(a, "seg")
     assert again["compile_ms"] == 0.0  # in-memory cache
 
