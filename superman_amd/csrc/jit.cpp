@@ -40,10 +40,10 @@
 // D = prod_x - prod_y of segment 0 fuses the x root's product with the
 // subtraction into one fma (dexpr).
 //
-// Measured on MI355X (profiles/r2): n=40 d=0.5 bench matrix 12.1 VALU
-// instructions per Gray step (cost model 11.9; round 1 18.2; the prefix-
+// Measured on MI355X (profiles/r2): n=40 d=0.5 bench matrix 11.6 VALU
+// instructions per Gray step (cost model 11.4; round 1 18.2; the prefix-
 // blocked AOT walk executes 46.6, the plain dense walk 81), VALU 93% busy at 2
-// waves/SIMD, 2.99e12 steps/s.  Everything else (chunk start, lane layout,
+// waves/SIMD, 3.08e12 steps/s.  Everything else (chunk start, lane layout,
 // wave-chunk queue, reduction order) is walk_common.hpp's, shared with the
 // ahead-of-time kernels, and the arithmetic is mirrored bit for bit by
 // engine_cpu.cpp (tree_*, seg_*) and oracle/oracle.c (kind 3).
@@ -207,11 +207,9 @@ inline uint64_t freq(uint32_t s, int b, int cc) {
 // 102 -> 188 VGPRs, 142 -> 246 VGPRs no spill, 205 -> 175 spilled VGPRs).
 // Occupancy 2 costs ~2% against 3 on this walk (measured, n = 40), 1 ~35%.
 constexpr int kRegs3 = 90;
-// Calibrated against the compiler (round 2, storage plans): at an estimate of
-// 170 no walk loop spills VGPRs on the bench matrix or on random n = 30-64
-// matrices of density 0.1-0.9 (scratch traffic only in the chunk start); at
-// 180-200 some do.  On the bench matrix (MI355X): 142 -> 2.55e12, 160 ->
-// 2.80e12, 180 -> 2.81e12 Gray steps/s.  SUP_JIT_REGMAX overrides (experiments).
+// The default; long walks check it against the compiler (build_seg: larger
+// or smaller budgets by the code object's VGPR spill count).  SUP_JIT_REGMAX
+// fixes it (experiments).
 static const int kRegsMax = std::getenv("SUP_JIT_REGMAX") ? std::atoi(std::getenv("SUP_JIT_REGMAX")) : 170;
 constexpr double kOcc2Penalty = 1.02;
 
@@ -1622,8 +1620,8 @@ int build_seg(Plan& P) {
   }
   P.seg_skip = seg_skip_fraction_plan(P, 2048);
   if (std::getenv("SUP_JIT_VERBOSE"))
-    std::fprintf(stderr, "seg plan n=%d m=%d b=%d ops/step=%.4f regs=%d cc=%d (storage plans evaluated: %ld)\n", n, m,
-                 P.seg_b, P.seg_ops, P.seg_regs, P.seg_cc, g_fit_calls.load());
+    std::fprintf(stderr, "seg plan n=%d m=%d b=%d ops/step=%.4f regs=%d cc=%d key=%016llx (storage plans evaluated: %ld)\n",
+                 n, m, P.seg_b, P.seg_ops, P.seg_regs, P.seg_cc, (unsigned long long)P.jit_key, g_fit_calls.load());
   return SUP_OK;
 }
 
