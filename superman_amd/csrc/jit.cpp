@@ -1572,8 +1572,8 @@ int build_seg(Plan& P) {
   };
   int budget = kRegsMax;
   finish(budget);
-  // The live-value budget against the compiler (long walks only: up to ~5
-  // hiprtc compiles of ~0.5-1 s, cached).  The estimate is rough (at 170 the
+  // The live-value budget against the compiler (walks of 10 ms or more: up to
+  // ~5 hiprtc compiles of ~0.5-1 s, cached).  The estimate is rough (at 170 the
   // n = 40 bench kernel fits 256 VGPRs with 6 chunk-level spills, denser or
   // larger matrices spill inside the walk loop), so the compiled code object's
   // VGPR spill count decides: from the default, larger budgets (fewer ops)
@@ -1585,7 +1585,7 @@ int build_seg(Plan& P) {
   const bool fixed = std::getenv("SUP_JIT_REGMAX") || std::getenv("SUP_JIT_STORAGE") || std::getenv("SUP_JIT_CC") ||
                      std::getenv("SUP_JIT_NOVERIFY");
   const double walk_s = std::ldexp(1.0, n - 1) * P.seg_ops / 3.7e13;
-  if (!fixed && walk_s >= 0.05 && P.seg_regs > kRegs3) {
+  if (!fixed && walk_s >= 0.01 && P.seg_regs > kRegs3) {
     constexpr int kSpillOk = 20;
     auto spills = [&]() {
       int vgpr = 0, sp = 0;

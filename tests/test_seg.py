@@ -230,3 +230,20 @@ def test_seg_skip_aware_plan(sup, monkeypatch):
             info = sup.plan_info(a, "seg")
             eff[polish] = info["est_ops_per_step"] * (1.0 - seg_skip_fraction(sup, a, "seg"))
         assert eff["1"] <= eff["0"] * 1.05 + 1e-12, (n, eff)
+
+
+def test_seg_uncompilable_pattern_falls_back(sup, tmp_path, monkeypatch):
+    """A dense n = 60 pattern whose generated kernel hiprtc's register
+    allocator gives up on ("maximum depth for recoloring"): the plan check
+    (jit.cpp build_seg) refuses the segmented walk, a dense request runs the
+    ahead-of-time walk instead, an explicit segmented request fails loudly,
+    and later kernels still compile in the same process."""
+    monkeypatch.setenv("SUP_JIT_CACHE_DIR", str(tmp_path))
+    rng = np.random.default_rng(1029)
+    n = 60
+    a = np.where(rng.random((n, n)) < 0.9, rng.random((n, n)) * 5, 0.0)
+    a[np.arange(n), rng.permutation(n)] = 1.0
+    assert sup.plan_info(a, "dense", jit=1)["kind"] in ("dense", "sparse")
+    with pytest.raises(sup.SupError):
+        sup.plan_info(a, "seg", jit=1)
+    assert sup.prepare(_rand(24, 0.5, 11), "seg")["kind"] == "seg"
