@@ -1600,9 +1600,15 @@ int build_seg(Plan& P) {
     int best_b = budget;
     double best_ops = P.seg_ops;
     if (s0 <= kSpillOk) {
+      // (bench matrix: 180/190/200/210 -> 11.73/11.63/11.45/11.37 ops with
+      // 5/0/7/9 spilled VGPRs; from 220 on 11.28-11.29 ops, 21-27 spills)
       for (int b2 = budget + 10; b2 <= budget + 40; b2 += 10) {
         finish(b2);
-        if (P.seg_ops < best_ops - 1e-9 && spills() <= kSpillOk) best_ops = P.seg_ops, best_b = b2;
+        if (P.seg_ops < best_ops - 1e-9) {
+          const int sp = spills();
+          if (std::getenv("SUP_JIT_VERBOSE")) std::fprintf(stderr, "  budget %d: ops %.4f spills %d\n", b2, P.seg_ops, sp);
+          if (sp <= kSpillOk) best_ops = P.seg_ops, best_b = b2;
+        }
       }
     } else {
       // the fewest spills if none gets under kSpillOk
