@@ -195,9 +195,13 @@ int sup_perman_cpu(const void* mat, sup_dtype t, int n, sup_kernel kernel, int t
  * the residues are joined by CRT (walk_exact.hip, exact.cpp), with a built-in
  * divisibility self-check.  *out receives the signed decimal integer,
  * NUL-terminated (520 bytes always suffice).  o->gpu_num devices from
- * o->device_id split the work statically; on_cpu = 1 runs o->threads host
- * threads instead.  st (optional): kernel_ms (max over devices), wall_ms,
- * devices_used, gray_steps. */
+ * o->device_id take power-of-two items of wave-chunks from a queue
+ * (o->chunk_log2 wave-chunks each, 0 = ~16 items per taker; one device alone
+ * walks its whole range), and with o->cpu_worker a CPU thread (o->threads
+ * host threads) takes items too; on_cpu = 1 runs o->threads host threads
+ * instead.  The result never depends on who took which item (residue sums).
+ * st (optional): kernel_ms (max over devices), wall_ms, devices_used,
+ * gray_steps, chunks_done_cpu. */
 int sup_perman_exact(const void* mat, sup_dtype t, int n, const sup_opts* o, int on_cpu, char* out,
                      size_t out_len, sup_stats* st);
 

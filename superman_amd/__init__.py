@@ -152,13 +152,15 @@ def perman_cpu(mat, kernel: str = "dense", threads: int = 16, return_stats: bool
 
 
 def perman_exact(mat, gpu_num: int = 1, device_id: int = 0, cpu: bool = False, threads: int = 16,
-                 return_stats: bool = False):
+                 return_stats: bool = False, cpu_worker: bool = False, chunk_log2: int = 0):
     """Exact permanent (Python int) of an integer matrix: the Ryser / Gray walk
     of 2A in residue arithmetic modulo primes, joined by CRT (sup_perman_exact).
-    The reference's int / -b path is fp64; this one is exact."""
+    The reference's int / -b path is fp64; this one is exact.  ``cpu`` runs on
+    host threads only; ``cpu_worker`` adds a host worker to the devices' chunk
+    queue (items of 2^chunk_log2 wave-chunks, 0 = automatic)."""
     a, dt, n = _mat(mat)
     lib = _lib.load()
-    o = _opts(gpu_num=gpu_num, device_id=device_id, threads=threads)
+    o = _opts(gpu_num=gpu_num, device_id=device_id, threads=threads, cpu=cpu_worker, chunk_log2=chunk_log2)
     buf = C.create_string_buffer(1024)
     st = SupStats()
     _lib.check(lib.sup_perman_exact(a.ctypes.data, dt, n, C.byref(o), int(bool(cpu)), buf, len(buf), C.byref(st)),

@@ -236,8 +236,8 @@ int sup_perman_exact(const void* mat, sup_dtype t, int n, const sup_opts* o_in, 
   else sup_opts_init(&o);
   std::string s;
   double kms = 0.0;
-  int used = 0;
-  if ((rc = exact_perman(A.data(), n, o, on_cpu != 0, s, &kms, &used))) return rc;
+  int used = 0, cpu_items = 0;
+  if ((rc = exact_perman(A.data(), n, o, on_cpu != 0, s, &kms, &used, &cpu_items))) return rc;
   if (s.size() + 1 > out_len) {
     set_error("sup_perman_exact: output buffer too small");
     return SUP_EINVAL;
@@ -250,6 +250,7 @@ int sup_perman_exact(const void* mat, sup_dtype t, int n, const sup_opts* o_in, 
     st->gray_steps = 1ull << (n - 1);
     st->visited_steps = st->gray_steps;
     st->devices_used = used;
+    st->chunks_done_cpu = cpu_items;
     st->walk_kind = (int)kWalkDense;
     st->leaves = 1;
   }

@@ -218,8 +218,10 @@ int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1,
 void cpu_exact_range(const Plan& P, uint64_t c0, uint64_t c1, const std::vector<double>& primes, int threads,
                      std::vector<uint64_t>& res);
 // Exact permanent of integer-valued A as a decimal string (sup_perman_exact).
+// Several devices or o.cpu_worker: a queue of chunk items; *cpu_items = items
+// the CPU worker took.
 int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::string& out, double* kernel_ms,
-                 int* devices_used);
+                 int* devices_used, int* cpu_items = nullptr);
 // The same after the -o reductions (sup_perman_reduced_exact): exact leaves, big-integer sum.
 int exact_perman_reduced(const double* A, int n, const sup_opts& o, bool on_cpu, const sup_reduce_opts& r,
                          std::string& out, double* kernel_ms, int* leaves);

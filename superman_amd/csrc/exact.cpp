@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <atomic>
 #include <thread>
 
 #include "engine.hpp"
@@ -149,7 +150,7 @@ struct Big {
 }  // namespace
 
 int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::string& out, double* kernel_ms,
-                 int* devices_used) {
+                 int* devices_used, int* cpu_items) {
   // integrality and size
   double maxrow = 0.0, logT = n - 1;
   for (int j = 0; j < n; ++j) {
@@ -166,6 +167,7 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
       out = "0";
       if (kernel_ms) *kernel_ms = 0.0;
       if (devices_used) *devices_used = 0;
+      if (cpu_items) *cpu_items = 0;
       return SUP_OK;
     }
     maxrow = std::max(maxrow, ra);
@@ -205,48 +207,87 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
   if (rc) return rc;
   const uint64_t C = P.lay.chunks();
 
-  // residues of T, per prime; devices split the chunks statically, kMaxPrimes per launch
+  // residues of T, per prime.  One device: its whole range, kMaxPrimes per
+  // launch.  Several devices, or the CPU worker (-c with -g): a queue of
+  // power-of-two items of wave-chunks (o.chunk_log2, else ~16 per taker) that
+  // one host thread per device, and the CPU worker on o.threads host threads,
+  // take in turn (as the fp64 -p6 queue, gpu_exact_dense.cu:776-904).  Residue
+  // sums are exact, so who took which item never changes the result.
   std::vector<uint64_t> res(np, 0);
   double kms = 0.0;
-  int used = 0;
+  int used = 0, cpu_done = 0;
   if (on_cpu) {
     cpu_exact_range(P, 0, C, primes, std::max(o.threads, 1), res);
   } else {
     int ndev = 0;
     if ((rc = device_count(&ndev))) return rc;
-    const int G = std::max(1, std::min(o.gpu_num, ndev - o.device_id));
     if (o.device_id < 0 || o.device_id >= ndev) {
       set_error("sup_perman_exact: device_id out of range");
       return SUP_EINVAL;
     }
-    std::vector<std::vector<uint64_t>> dres(G, std::vector<uint64_t>(np, 0));
-    std::vector<double> dms(G, 0.0);
-    std::vector<int> drc(G, SUP_OK);
-    std::vector<std::string> derr(G);
-    std::vector<std::thread> th;
-    for (int g = 0; g < G; ++g)
-      th.emplace_back([&, g]() {
-        const uint64_t c0 = C * g / G, c1 = C * (g + 1) / G;
-        for (int q0 = 0; q0 < np && drc[g] == SUP_OK; q0 += kMaxPrimes) {
-          const std::vector<double> pr(primes.begin() + q0, primes.begin() + std::min(np, q0 + kMaxPrimes));
+    const int G = std::max(1, std::min(o.gpu_num, ndev - o.device_id));
+    const bool cpu = o.cpu_worker != 0;
+    const int takers = G + (cpu ? 1 : 0);
+    uint64_t item = C;
+    if (takers > 1) {
+      if (o.chunk_log2 > 0) {
+        item = std::min<uint64_t>(C, 1ull << std::min(o.chunk_log2, 62));
+      } else {
+        item = 1;
+        while (item * 2 <= C && C / (item * 2) >= (uint64_t)takers * 16) item <<= 1;
+      }
+    }
+    const uint64_t nitems = (C + item - 1) / item;
+    std::vector<std::vector<uint64_t>> dres(takers, std::vector<uint64_t>(np, 0));
+    std::vector<double> dms(takers, 0.0);
+    std::vector<int> drc(takers, SUP_OK), dtook(takers, 0);
+    std::vector<std::string> derr(takers);  // g_err is thread_local: carry worker messages back
+    std::atomic<uint64_t> next{0};
+    std::atomic<bool> failed{false};
+    auto add = [&](int g, const std::vector<uint64_t>& r, int q0) {
+      for (size_t i = 0; i < r.size(); ++i) dres[g][q0 + i] = (dres[g][q0 + i] + r[i]) % (uint64_t)primes[q0 + i];
+    };
+    auto worker = [&](int g) {
+      for (;;) {
+        if (failed.load()) return;
+        const uint64_t it = next.fetch_add(1);
+        if (it >= nitems) return;
+        const uint64_t a = it * item, b = std::min(C, a + item);
+        if (g == G) {  // the CPU worker: every prime in one pass
           std::vector<uint64_t> r;
-          double ms = 0.0;
-          drc[g] = run_range_exact(o.device_id + g, P, group, c0, c1, pr, r, &ms);
-          if (drc[g]) derr[g] = last_error();
-          for (size_t i = 0; i < r.size(); ++i) dres[g][q0 + i] = r[i];
-          dms[g] += ms;
+          cpu_exact_range(P, a, b, primes, std::max(o.threads, 1), r);
+          add(g, r, 0);
+        } else {
+          for (int q0 = 0; q0 < np; q0 += kMaxPrimes) {
+            const std::vector<double> pr(primes.begin() + q0, primes.begin() + std::min(np, q0 + kMaxPrimes));
+            std::vector<uint64_t> r;
+            double ms = 0.0;
+            if ((drc[g] = run_range_exact(o.device_id + g, P, group, a, b, pr, r, &ms))) {
+              derr[g] = last_error();
+              failed.store(true);
+              return;
+            }
+            add(g, r, q0);
+            dms[g] += ms;
+          }
         }
-      });
+        ++dtook[g];
+      }
+    };
+    std::vector<std::thread> th;
+    for (int g = 1; g < takers; ++g) th.emplace_back(worker, g);
+    worker(0);
     for (auto& t : th) t.join();
-    for (int g = 0; g < G; ++g)
+    for (int g = 0; g < takers; ++g)
       if (drc[g]) {
         set_error(derr[g]);
         return drc[g];
       }
     for (int q = 0; q < np; ++q)
-      for (int g = 0; g < G; ++g) res[q] = (res[q] + dres[g][q]) % (uint64_t)primes[q];
-    kms = *std::max_element(dms.begin(), dms.end());
+      for (int g = 0; g < takers; ++g) res[q] = (res[q] + dres[g][q]) % (uint64_t)primes[q];
+    kms = *std::max_element(dms.begin(), dms.begin() + G);
     used = G;
+    cpu_done = cpu ? dtook[G] : 0;
   }
 
   // Garner: mixed-radix digits v_i, then T = sum v_i prod_{j<i} p_j in [0, M)
@@ -287,6 +328,7 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
   out = (neg && !T.zero() ? "-" : "") + T.dec();
   if (kernel_ms) *kernel_ms = kms;
   if (devices_used) *devices_used = used;
+  if (cpu_items) *cpu_items = cpu_done;
   return SUP_OK;
 }
 

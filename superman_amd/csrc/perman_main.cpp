@@ -223,6 +223,7 @@ int main(int argc, char** argv) {
       return 1;
     }
     if (c.gpu && c.perman_algo != 5 && c.perman_algo != 6 && c.perman_algo != 8) o.gpu_num = 1;
+    if (c.perman_algo != 6 && c.perman_algo != 8) o.cpu_worker = 0;  // the hybrid worker joins the queues only
     static char buf[1 << 16];
     sup_stats st;
     int rc = SUP_OK;
@@ -238,7 +239,8 @@ int main(int argc, char** argv) {
               << " in " << sec << std::endl;
     std::printf("Permanent: %s\n", buf);
     if (c.verbose)
-      std::printf("Stats: devices %d kernel_ms %.3f wall_ms %.3f\n", st.devices_used, st.kernel_ms, st.wall_ms);
+      std::printf("Stats: devices %d kernel_ms %.3f wall_ms %.3f cpu_items %d\n", st.devices_used, st.kernel_ms,
+                  st.wall_ms, st.chunks_done_cpu);
     return 0;
   }
 

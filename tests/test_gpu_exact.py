@@ -34,6 +34,22 @@ def test_gpu_exact_vs_cpu_and_oracle(sup, orc, n, d, lo, hi, seed):
     assert got == orc.exact_perman_crt(a, 16)
 
 
+@pytest.mark.parametrize("chunk_log2", [0, 1, 4])
+def test_gpu_exact_queue_with_cpu_worker(sup, chunk_log2):
+    """The chunk queue (gpu_exact_dense.cu:776-904 semantics) on every visible
+    device plus the hybrid CPU worker: residue sums are exact, so the integer is
+    the single device's whatever the item size and whoever took which item."""
+    a = _rand(26, 0.5, 11, -2, 5)
+    want = sup.perman_exact(a)
+    got, st = sup.perman_exact(a, gpu_num=sup.device_count(), cpu_worker=True, threads=8,
+                               chunk_log2=chunk_log2, return_stats=True)
+    assert got == want
+    assert st["devices_used"] == sup.device_count()
+    assert 0 <= st["chunks_done_cpu"]
+    if chunk_log2 == 1:  # 2^12 items of 2 wave-chunks: the host worker surely takes some
+        assert st["chunks_done_cpu"] > 0
+
+
 def test_gpu_exact_known(sup):
     import math
     for n in (10, 21, 26):
