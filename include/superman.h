@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SUP_ABI_VERSION 3
+#define SUP_ABI_VERSION 4
 
 /* ---- error codes ------------------------------------------------------ */
 #define SUP_OK            0
@@ -204,6 +204,20 @@ int sup_perman_cpu(const void* mat, sup_dtype t, int n, sup_kernel kernel, int t
  * gray_steps, chunks_done_cpu. */
 int sup_perman_exact(const void* mat, sup_dtype t, int n, const sup_opts* o, int on_cpu, char* out,
                      size_t out_len, sup_stats* st);
+
+/* The permanent in double-double (~106-bit significand): the MI355X form of
+ * the reference's quad-precision calculation (v2 `-q`,
+ * revised_perman/main.cpp:141-142 -> parallel_perman64<__float128,S>,
+ * cpu_algos.hpp:761-873, CPU only).  The dense Ryser / Gray walk of
+ * sup_perman (default layout, same wave-chunks) with every value a
+ * double-double (walk_dd.hip); perm = *out_hi + *out_lo (out_lo may be NULL).
+ * o->gpu_num devices from o->device_id split the wave-chunks statically;
+ * on_cpu = 1 runs the same operations on o->threads host threads.  Chunk
+ * partials are combined in one fixed pairwise order, so the result is
+ * bit-identical for any device or thread count.  ~8x the fp64 walk's work
+ * (16n + 13 fp64 ops per Gray step). */
+int sup_perman_quad(const void* mat, sup_dtype t, int n, const sup_opts* o, int on_cpu, double* out_hi,
+                    double* out_lo, sup_stats* st);
 
 /* Nijenhuis-Wilf prologue (gpu_exact_dense.cu:642-652): x0[j] = a[j][n-1] - rowsum_j/2,
  * p0 = prod x0.  Host-only helper, exported for the test harness. */

@@ -169,6 +169,21 @@ def perman_exact(mat, gpu_num: int = 1, device_id: int = 0, cpu: bool = False, t
     return (v, st.as_dict()) if return_stats else v
 
 
+def perman_quad(mat, gpu_num: int = 1, device_id: int = 0, cpu: bool = False, threads: int = 16,
+                return_stats: bool = False):
+    """The permanent in double-double (~106 bits; the reference's `-q` quad
+    calculation, revised_perman/main.cpp:141-142) as (hi, lo), perm = hi + lo:
+    the dense walk with double-double values (walk_dd.hip), on gpu_num devices
+    or (cpu=True) on host threads — bit-identical either way."""
+    a, dt, n = _mat(mat)
+    lib = _lib.load()
+    o = _opts(gpu_num=gpu_num, device_id=device_id, threads=threads)
+    hi, lo, st = C.c_double(0.0), C.c_double(0.0), SupStats()
+    _lib.check(lib.sup_perman_quad(a.ctypes.data, dt, n, C.byref(o), int(bool(cpu)), C.byref(hi), C.byref(lo),
+                                   C.byref(st)), "perman_quad")
+    return ((hi.value, lo.value), st.as_dict()) if return_stats else (hi.value, lo.value)
+
+
 def partial(mat, start: int, end: int, kernel: str = "dense", gpu_num: int = 1, device_id: int = 0,
             walk_log2: int = 0, return_stats: bool = False):
     """GPU partial Ryser sum over reference Gray indices [start, end) (index 0 = p0 term)."""

@@ -34,7 +34,7 @@ SCHED_SINGLE, SCHED_STATIC, SCHED_CHUNKS = 0, 1, 2
 EXPORTS = [
     "sup_opts_init", "sup_abi_version", "sup_last_error", "sup_device_count",
     "sup_perman", "sup_partial", "sup_perman_cpu", "sup_nw_start", "sup_perman_shard", "sup_plan_info",
-    "sup_prepare", "sup_perman_exact", "sup_perman_reduced_exact",
+    "sup_prepare", "sup_perman_exact", "sup_perman_reduced_exact", "sup_perman_quad",
     "sup_gpu_perman64_xshared_coalescing_mshared",
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpu",
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks",
@@ -126,7 +126,7 @@ def load() -> C.CDLL:
             build()
         lib = C.CDLL(LIB_PATH)
         _declare(lib)
-        if lib.sup_abi_version() != 3:
+        if lib.sup_abi_version() != 4:
             raise RuntimeError("libsuperman_hip.so ABI version mismatch")
         _lib = lib
         return lib
@@ -144,6 +144,7 @@ def _declare(lib: C.CDLL) -> None:
                                 C.POINTER(SupStats)]
     lib.sup_perman_cpu.argtypes = [P, I, I, I, I, C.POINTER(D), C.POINTER(SupStats)]
     lib.sup_perman_exact.argtypes = [P, I, I, C.POINTER(SupOpts), I, C.c_char_p, C.c_size_t, C.POINTER(SupStats)]
+    lib.sup_perman_quad.argtypes = [P, I, I, C.POINTER(SupOpts), I, C.POINTER(D), C.POINTER(D), C.POINTER(SupStats)]
     lib.sup_perman_shard.argtypes = [P, I, I, I, I, I, C.POINTER(SupOpts), C.POINTER(D), C.POINTER(SupStats)]
     lib.sup_plan_info.argtypes = [P, I, I, I, C.POINTER(SupOpts), C.POINTER(I), P, C.POINTER(I), C.POINTER(I),
                                   C.POINTER(I), C.POINTER(I), C.POINTER(D)]

@@ -257,6 +257,38 @@ int sup_perman_exact(const void* mat, sup_dtype t, int n, const sup_opts* o_in, 
   return SUP_OK;
 }
 
+int sup_perman_quad(const void* mat, sup_dtype t, int n, const sup_opts* o_in, int on_cpu, double* out_hi,
+                    double* out_lo, sup_stats* st) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!out_hi) {
+    set_error("sup_perman_quad: out_hi missing");
+    return SUP_EINVAL;
+  }
+  std::vector<double> A;
+  int rc = to_double(mat, t, n, A);
+  if (rc) return rc;
+  sup_opts o;
+  if (o_in) o = *o_in;
+  else sup_opts_init(&o);
+  double hi = 0.0, lo = 0.0, kms = 0.0;
+  int used = 0;
+  if ((rc = quad_perman(A.data(), n, o, on_cpu != 0, &hi, &lo, &kms, &used))) return rc;
+  *out_hi = hi;
+  if (out_lo) *out_lo = lo;
+  if (st) {
+    std::memset(st, 0, sizeof(*st));
+    st->kernel_ms = kms;
+    st->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    st->gray_steps = 1ull << (n - 1);
+    st->visited_steps = st->gray_steps;
+    st->devices_used = used;
+    st->walk_kind = (int)kWalkDense;
+    st->leaves = 1;
+    st->est_ops_per_step = 16.0 * n + 13.0;
+  }
+  return SUP_OK;
+}
+
 int sup_perman_reduced_exact(const void* mat, sup_dtype t, int n, const sup_opts* o_in, int on_cpu,
                              const sup_reduce_opts* r_in, char* out, size_t out_len, sup_stats* st) {
   auto t0 = std::chrono::steady_clock::now();

@@ -482,6 +482,8 @@ struct DeviceCtx {
   unsigned* d_visited = nullptr;
   double* d_wave = nullptr;   // exact path: per-wave residues
   size_t wave_cap = 0;
+  double* d_x0dd = nullptr;   // double-double walk: start vector (hi, lo)
+  size_t x0dd_cap = 0;
   size_t visited_cap = 0;
   unsigned* d_counter = nullptr;
   double* d_result = nullptr;
@@ -742,6 +744,57 @@ int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1,
     for (size_t i = 0; i < waves; ++i) acc = (acc + (uint64_t)w[i * kMaxPrimes + q]) % pq;
     res[q] = acc;
   }
+  return SUP_OK;
+}
+
+int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64_t c0, uint64_t c1,
+                 double* parts, double* kernel_ms) {
+  if (kernel_ms) *kernel_ms = 0.0;
+  if (c1 <= c0) return SUP_OK;
+  if (P.kind != kWalkDense || c1 > P.lay.chunks() || x0dd.size() != 2 * (size_t)P.NP) {
+    set_error("run_range_dd: bad request");
+    return SUP_EINVAL;
+  }
+  DeviceCtx* c = nullptr;
+  int rc = get_ctx(dev, &c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(c->mu);
+  SUP_HIP(hipSetDevice(dev));
+  int occ = 0;
+  SUP_HIP(dd_occupancy(P.n, &occ));
+  if (occ < 1) occ = 1;
+  const uint64_t count = c1 - c0;
+  uint64_t grid = (uint64_t)c->cus * (uint64_t)occ;
+  const uint64_t need_blocks = (count + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (grid > need_blocks) grid = need_blocks;
+  if (grid < 1) grid = 1;
+  if ((rc = ensure(c->d_cols, c->cols_cap, P.cols.size()))) return rc;
+  if ((rc = ensure(c->d_x0dd, c->x0dd_cap, x0dd.size()))) return rc;
+  if ((rc = ensure(c->d_chunk, c->chunk_cap, (size_t)(2 * count)))) return rc;
+  hipStream_t s = c->stream;
+  c->tables_uid = 0;  // the walk's own tables replace the cached plan's
+  SUP_HIP(hipMemcpyAsync(c->d_cols, P.cols.data(), P.cols.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  SUP_HIP(hipMemcpyAsync(c->d_x0dd, x0dd.data(), x0dd.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
+  WalkParams p{};
+  p.cols = c->d_cols;
+  p.x0 = c->d_x0dd;
+  p.chunk_begin = c0;
+  p.chunk_count = count;
+  p.L = P.lay.L;
+  p.m = P.lay.m;
+  p.n = P.n;
+  p.chunk_out = c->d_chunk;
+  p.counter = c->d_counter;
+  p.group = 1;
+  SUP_HIP(hipEventRecord(c->ev0, s));
+  SUP_HIP(launch_dd(P.n, p, (int)grid, s));
+  SUP_HIP(hipEventRecord(c->ev1, s));
+  SUP_HIP(hipMemcpyAsync(parts, c->d_chunk, 2 * count * sizeof(double), hipMemcpyDeviceToHost, s));
+  SUP_HIP(hipStreamSynchronize(s));
+  float ms = 0.f;
+  SUP_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  if (kernel_ms) *kernel_ms = ms;
   return SUP_OK;
 }
 

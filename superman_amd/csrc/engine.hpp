@@ -226,4 +226,16 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
 int exact_perman_reduced(const double* A, int n, const sup_opts& o, bool on_cpu, const sup_reduce_opts& r,
                          std::string& out, double* kernel_ms, int* leaves);
 
+// ---- double-double walk (quad.cpp, walk_dd.hip) ----
+// Wave-chunk partials (hi, lo) of chunks [c0, c1) of the dense identity plan
+// P with the double-double start vector x0dd (2 NP: hi block, lo block) into
+// parts[2 (c - c0) + {0, 1}]: on device `dev`, or on host threads (bit-identical).
+int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64_t c0, uint64_t c1,
+                 double* parts, double* kernel_ms);
+void cpu_dd_range(const Plan& P, const std::vector<double>& x0dd, uint64_t c0, uint64_t c1, int threads,
+                  double* parts);
+// Permanent in double-double (sup_perman_quad): *hi + *lo.
+int quad_perman(const double* A, int n, const sup_opts& o, bool on_cpu, double* hi, double* lo, double* kernel_ms,
+                int* devices_used);
+
 }  // namespace sup

@@ -32,6 +32,14 @@ SUP_DECL_EXACT(17)
 SUP_DECL_EXACT(33)
 SUP_DECL_EXACT(49)
 #undef SUP_DECL_EXACT
+#define SUP_DECL_DD(LO)                                                               \
+  hipError_t launch_dd_##LO(int n, const WalkParams& p, int grid, hipStream_t s);    \
+  hipError_t occupancy_dd_##LO(int n, int* blocks_per_cu);
+SUP_DECL_DD(1)
+SUP_DECL_DD(17)
+SUP_DECL_DD(33)
+SUP_DECL_DD(49)
+#undef SUP_DECL_DD
 #define SUP_DECL_LDS(LO)                                                                   \
   hipError_t launch_lds_##LO(int n, const WalkParams& p, int grid, hipStream_t s);        \
   hipError_t occupancy_lds_##LO(int n, int m, int* blocks_per_cu);
@@ -58,6 +66,11 @@ hipError_t lds_occupancy(int n, int m, int* blocks_per_cu);
 // multiplied in exact groups of g (1, 2 or 4) before the residue chain.
 hipError_t launch_exact(int n, int g, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s);
 hipError_t exact_occupancy(int n, int g, int* blocks_per_cu);
+
+// Double-double dense walk (walk_dd.hip): p.x0 = 2 NP doubles (hi, lo),
+// p.chunk_out = 2 doubles (hi, lo) per wave-chunk.
+hipError_t launch_dd(int n, const WalkParams& p, int grid, hipStream_t s);
+hipError_t dd_occupancy(int n, int* blocks_per_cu);
 
 // Fixed-order pairwise reduction of `count` doubles into *out (64-way passes,
 // zero padded; mirrored by oracle/oracle.c orc_pairwise_reduce).  `scratch`

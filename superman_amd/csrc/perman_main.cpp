@@ -14,7 +14,9 @@
 // its cost model wins); --exact (-E) the exact integer permanent of an int /
 // -b (binary) matrix (sup_perman_exact: residue walk + CRT; the reference's
 // int path is fp64): on -g with -p5/-p6 it uses -d devices, with -c alone
-// the -t host threads.
+// the -t host threads.  -q (v2's quad calculation, main.cpp:141-142): the
+// dense walk in double-double (sup_perman_quad), -d devices with -p5/-p6,
+// -t host threads with -c; prints hi and the hi + lo pair.
 #include <getopt.h>
 
 #include <chrono>
@@ -31,7 +33,7 @@ namespace {
 
 struct Cli {
   bool generic = true, dense = true, approximation = false, gpu = false, cpu = false, grid_graph = false;
-  bool rccl = false, verbose = false, compression = false, exact = false;
+  bool rccl = false, verbose = false, compression = false, exact = false, quad = false;
   int gpu_num = 2, threads = 16, perman_algo = 1, preprocessing = 0, device = 0, reps = 1;
   double scaling = -1.0;
   long number_of_times = 100000;  // main.cu:338-344 defaults
@@ -122,7 +124,7 @@ int run_approx(const Cli& c) {
 
 int main(int argc, char** argv) {
   Cli c;
-  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rvou:S:J:E";
+  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rvou:S:J:Eq";
   const struct option long_options[] = {{"binary", 0, NULL, 'b'},       {"sparse", 0, NULL, 's'},
                                         {"preprocessing", 1, NULL, 'r'}, {"threads", 1, NULL, 't'},
                                         {"file", 1, NULL, 'f'},          {"gpu", 0, NULL, 'g'},
@@ -135,7 +137,8 @@ int main(int argc, char** argv) {
                                         {"rccl", 0, NULL, 'R'},          {"verbose", 0, NULL, 'v'},
                                         {"compression", 0, NULL, 'o'},   {"scaling", 1, NULL, 'u'},
                                         {"seed", 1, NULL, 'S'},          {"jit", 1, NULL, 'J'},
-                                        {"exact", 0, NULL, 'E'},         {NULL, 0, NULL, 0}};
+                                        {"exact", 0, NULL, 'E'},         {"quad", 0, NULL, 'q'},
+                                        {NULL, 0, NULL, 0}};
   int opt;
   auto need_arg = [&](char o) -> bool {
     if (optarg[0] == '-') {
@@ -168,6 +171,7 @@ int main(int argc, char** argv) {
       case 'k': if (!need_arg('k')) return 1; c.reps = std::max(1, std::atoi(optarg)); break;
       case 'R': c.rccl = true; break;
       case 'E': c.exact = true; break;
+      case 'q': c.quad = true; break;
       case 'v': c.verbose = true; break;
       case 'o': c.compression = true; break;  // revised_perman/main.cpp:1462
       case 'u':                                // main.cpp:1465 (atoi)
@@ -241,6 +245,32 @@ int main(int argc, char** argv) {
     if (c.verbose)
       std::printf("Stats: devices %d kernel_ms %.3f wall_ms %.3f cpu_items %d\n", st.devices_used, st.kernel_ms,
                   st.wall_ms, st.chunks_done_cpu);
+    return 0;
+  }
+
+  if (c.quad) {  // double-double dense walk (any -p: the sum does not depend on the kernel)
+    if (reduce) {
+      std::fprintf(stderr, "perman: -q does not combine with -o / -u\n");
+      sup_free(mat);
+      return 1;
+    }
+    if (c.gpu && c.perman_algo != 5 && c.perman_algo != 6 && c.perman_algo != 8) o.gpu_num = 1;
+    double hi = 0.0, lo = 0.0;
+    sup_stats st;
+    int rc = SUP_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int rep = 0; rep < c.reps && rc == SUP_OK; ++rep)
+      rc = sup_perman_quad(mat, t, n, &o, c.gpu ? 0 : 1, &hi, &lo, &st);
+    const double sec =
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / (double)c.reps;
+    sup_free(mat);
+    if (rc != SUP_OK) return fail("double-double permanent");
+    std::cout << "Result: " << (c.gpu ? "gpu_perman64_quad" : "cpu_perman64_quad") << " " << hi << " in " << sec
+              << std::endl;
+    std::printf("Permanent: %.17e\n", hi);
+    std::printf("Permanent (double-double): %.17e %+.17e\n", hi, lo);
+    if (c.verbose)
+      std::printf("Stats: devices %d kernel_ms %.3f wall_ms %.3f\n", st.devices_used, st.kernel_ms, st.wall_ms);
     return 0;
   }
 

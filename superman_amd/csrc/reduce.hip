@@ -94,6 +94,16 @@ hipError_t launch_exact(int n, int g, const WalkParams& p, const ExactParams& e,
   SUP_DISPATCH(exact, launch, n, g, p, e, grid, s)
 }
 
+hipError_t launch_dd(int n, const WalkParams& p, int grid, hipStream_t s) {
+  if (n < 1 || n > 64) return hipErrorInvalidValue;
+  SUP_DISPATCH(dd, launch, n, p, grid, s)
+}
+
+hipError_t dd_occupancy(int n, int* blocks_per_cu) {
+  if (n < 1 || n > 64) return hipErrorInvalidValue;
+  SUP_DISPATCH(dd, occupancy, n, blocks_per_cu)
+}
+
 hipError_t exact_occupancy(int n, int g, int* blocks_per_cu) {
   if (n < 1 || n > 64) return hipErrorInvalidValue;
   SUP_DISPATCH(exact, occupancy, n, g, blocks_per_cu)

@@ -1,0 +1,69 @@
+"""Double-double permanent (sup_perman_quad) on host threads — the host twin
+of walk_dd.hip, the MI355X form of the reference's quad-precision calculation
+(v2 `-q`, revised_perman/main.cpp:141-142 -> parallel_perman64<__float128,S>).
+
+Pinned against the reference itself: every `dense_q` golden (the reference's
+__float128 Ryser, compiled from its sources, tests/golden/make_golden.py) up
+to n = 22 equals hi bit for bit once rounded to fp64; on integer matrices
+hi + lo is the exact integer (checked against the exact residue path)."""
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+from conftest import fixture_path
+
+QUAD_MAX_N_CPU = 22
+
+
+def _quad_goldens(golden, max_n):
+    out = []
+    for k, q in sorted(golden.items()):
+        if "|dense_q|" not in k or k.endswith("seconds"):
+            continue
+        out.append((k.split("|")[0], q))
+    return out
+
+
+def test_quad_host_matches_reference_quad_goldens(sup, golden):
+    checked = 0
+    for nm, q in _quad_goldens(golden, QUAD_MAX_N_CPU):
+        a = sup.read_matrix(fixture_path(nm))[0]
+        if a.shape[0] > QUAD_MAX_N_CPU:
+            continue
+        hi, lo = sup.perman_quad(a, cpu=True, threads=8)
+        assert hi == q, (nm, hi, q)  # the reference's __float128 result, rounded once to fp64
+        assert abs(lo) <= abs(hi) * 2.0 ** -52, nm  # normalised pair
+        checked += 1
+    assert checked >= 40
+
+
+@pytest.mark.parametrize("n,lo_v,hi_v,seed", [(9, -3, 4, 1), (14, 1, 6, 2), (18, 0, 2, 3), (21, -5, 6, 4)])
+def test_quad_host_int_is_exact(sup, n, lo_v, hi_v, seed):
+    rng = np.random.default_rng(seed)
+    a = rng.integers(lo_v, hi_v, (n, n)).astype(np.int32)
+    hi, lo = sup.perman_quad(a, cpu=True, threads=8)
+    e = sup.perman_exact(a, cpu=True, threads=8)
+    if abs(e) < 2 ** 100:
+        assert Fraction(hi) + Fraction(lo) == e
+    else:
+        assert abs(Fraction(hi) + Fraction(lo) - e) <= abs(e) * Fraction(1, 2 ** 100)
+
+
+def test_quad_host_thread_invariance(sup):
+    a = sup.read_matrix(fixture_path("synth/20_0.50_double"))[0]
+    r1 = sup.perman_quad(a, cpu=True, threads=1)
+    assert r1 == sup.perman_quad(a, cpu=True, threads=7) == sup.perman_quad(a, cpu=True, threads=16)
+
+
+def test_quad_tiny_and_degenerate(sup):
+    assert sup.perman_quad(np.array([[2.5]]), cpu=True) == (2.5, 0.0)
+    assert sup.perman_quad(np.array([[1.0, 2.0], [3.0, 4.0]]), cpu=True)[0] == 10.0
+    z = np.ones((6, 6))
+    z[3] = 0.0
+    assert sup.perman_quad(z, cpu=True)[0] == 0.0
+    # 0.1 is not representable: the double-double start vector keeps the digits the fp64 one rounds away
+    a = np.full((12, 12), 0.1)
+    hi, lo = sup.perman_quad(a, cpu=True)
+    want = Fraction(479001600) * Fraction(0.1) ** 12
+    assert abs(Fraction(hi) + Fraction(lo) - want) <= want * Fraction(1, 2 ** 95)
