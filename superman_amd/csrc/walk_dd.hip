@@ -73,8 +73,12 @@ __device__ __forceinline__ dd dd_wave_sum(dd v) {
 
 // p.x0: 2 NP doubles (hi block, then lo block); p.chunk_out: 2 doubles per
 // wave-chunk (hi, lo).
+// Occupancy: 4n VGPRs hold x.  Up to n = 40 the kernel is asked for 2 waves
+// per SIMD (256 VGPRs): without the request LLVM allocates 266-282 VGPRs at
+// n = 26-29 and 258 at n = 40, i.e. 1 wave; with it 173-191 and 256 (2 spilled
+// VGPRs at n = 40).  Above 40 the request would spill 8-580 VGPRs: 1 wave.
 template <int N>
-__global__ __launch_bounds__(kBlock) void walk_dd(WalkParams p) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N <= 40 ? 2 : 1))) void walk_dd(WalkParams p) {
   constexpr int NP = pad8(N);
   const uint32_t lane = threadIdx.x & 63u;
   const bool lane_valid = lane < (1u << p.L);
