@@ -417,6 +417,21 @@ def perman_reduced_exact(mat, cpu: bool = False, threads: int = 16, device_id: i
     return (v, st.as_dict()) if return_stats else v
 
 
+def perman_reduced_quad(mat, compress: bool = True, scale=None, cpu: bool = False, threads: int = 16,
+                        device_id: int = 0, gpu_num: int = 1, min_n: int = 30, max_deg: int = 5,
+                        return_stats: bool = False):
+    """-o / -u with double-double leaves and combine (sup_perman_reduced_quad):
+    (hi, lo), perm = hi + lo."""
+    a, dt, n = _mat(mat, 4096)
+    lib = _lib.load()
+    o = _opts(gpu_num, device_id, threads)
+    r = _reduce_opts(compress, scale, min_n, max_deg)
+    hi, lo, st = C.c_double(0.0), C.c_double(0.0), SupStats()
+    _lib.check(lib.sup_perman_reduced_quad(a.ctypes.data, dt, n, C.byref(o), int(bool(cpu)), C.byref(r),
+                                           C.byref(hi), C.byref(lo), C.byref(st)), "perman_reduced_quad")
+    return ((hi.value, lo.value), st.as_dict()) if return_stats else (hi.value, lo.value)
+
+
 def read_mtx(path: str, binary: bool = False) -> tuple[np.ndarray, str, int]:
     """MatrixMarket coordinate file -> (matrix, type name, nz lines) (read_matrix.hpp:11-157)."""
     lib = _lib.load()

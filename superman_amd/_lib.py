@@ -35,6 +35,7 @@ EXPORTS = [
     "sup_opts_init", "sup_abi_version", "sup_last_error", "sup_device_count",
     "sup_perman", "sup_partial", "sup_perman_cpu", "sup_nw_start", "sup_perman_shard", "sup_plan_info",
     "sup_prepare", "sup_perman_exact", "sup_perman_reduced_exact", "sup_perman_quad",
+    "sup_perman_reduced_quad",
     "sup_gpu_perman64_xshared_coalescing_mshared",
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpu",
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks",
@@ -166,6 +167,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.sup_decompose.argtypes = [P, I, I, C.POINTER(SupReduceOpts), LEAF_FN, P, C.POINTER(D), C.POINTER(I)]
     lib.sup_perman_reduced_exact.argtypes = [P, I, I, C.POINTER(SupOpts), I, C.POINTER(SupReduceOpts), C.c_char_p,
                                              C.c_size_t, C.POINTER(SupStats)]
+    lib.sup_perman_reduced_quad.argtypes = [P, I, I, C.POINTER(SupOpts), I, C.POINTER(SupReduceOpts), C.POINTER(D),
+                                            C.POINTER(D), C.POINTER(SupStats)]
     lib.sup_perman_reduced.argtypes = [P, I, I, I, I, C.POINTER(SupOpts), I, C.POINTER(SupReduceOpts),
                                        C.POINTER(D), C.POINTER(SupStats)]
     for name in EXPORTS:

@@ -2,6 +2,7 @@
 #include <chrono>
 #include <cstring>
 
+#include "dd.hpp"
 #include "engine.hpp"
 
 using namespace sup;
@@ -460,6 +461,50 @@ int engine_leaf(const double* a, int n, void* user, double* out) {
   return SUP_OK;
 }
 }  // namespace
+
+int sup_perman_reduced_quad(const void* mat, sup_dtype t, int n, const sup_opts* o_in, int on_cpu,
+                            const sup_reduce_opts* r_in, double* out_hi, double* out_lo, sup_stats* st) {
+  auto t0 = std::chrono::steady_clock::now();
+  if (!mat || !out_hi || n < 1 || n > SUP_MAX_READ_N) {
+    set_error("sup_perman_reduced_quad: bad argument");
+    return SUP_EINVAL;
+  }
+  std::vector<double> A((size_t)n * n);
+  for (size_t i = 0; i < A.size(); ++i)
+    A[i] = t == SUP_INT32 ? (double)((const int32_t*)mat)[i]
+           : t == SUP_FLOAT32 ? (double)((const float*)mat)[i] : ((const double*)mat)[i];
+  sup_opts o;
+  if (o_in) o = *o_in;
+  else sup_opts_init(&o);
+  sup_reduce_opts r;
+  if (r_in) r = *r_in;
+  else sup_reduce_opts_init(&r);
+  double kms = 0.0;
+  int used = 0;
+  auto leaf = [&](const double* a, int k, dd* v) {
+    double ms = 0.0;
+    int u = 0;
+    const int rc = quad_perman(a, k, o, on_cpu != 0, &v->hi, &v->lo, &ms, &u);
+    kms += ms;
+    used = std::max(used, u);
+    return rc;
+  };
+  dd v{0.0, 0.0};
+  int leaves = 0;
+  const int rc = decompose_dd(A.data(), n, r, leaf, &v, &leaves);
+  if (rc) return rc;
+  *out_hi = v.hi;
+  if (out_lo) *out_lo = v.lo;
+  if (st) {
+    std::memset(st, 0, sizeof(*st));
+    st->kernel_ms = kms;
+    st->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    st->devices_used = used;
+    st->walk_kind = (int)kWalkDense;
+    st->leaves = leaves;
+  }
+  return SUP_OK;
+}
 
 int sup_perman_reduced(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched sched, const sup_opts* o_in,
                        int on_cpu, const sup_reduce_opts* r_in, double* out, sup_stats* st) {

@@ -64,4 +64,13 @@ SUP_DD_FN dd dd_mul(dd a, dd b) {
   return dd_fast_two_sum(p, e);
 }
 
+// a / d, d a double: quotient, exact remainder by fma, corrected quotient.
+SUP_DD_FN dd dd_div_d(dd a, double d) {
+  const double q1 = a.hi / d;
+  const double p = q1 * d;
+  const double e = __builtin_fma(q1, d, -p);
+  const double rem = ((a.hi - p) - e) + a.lo;
+  return dd_fast_two_sum(q1, rem / d);
+}
+
 }  // namespace sup

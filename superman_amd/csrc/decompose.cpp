@@ -23,9 +23,11 @@
 //   * an empty row/column after singleton removal returns 0 (the reference
 //     prints "Perman is 0" and exits, main.cpp:1089-1093).
 #include <cmath>
+#include <functional>
 #include <string>
 #include <vector>
 
+#include "dd.hpp"
 #include "engine.hpp"
 
 namespace sup {
@@ -237,24 +239,40 @@ Mat scaled(const Mat& m, const std::vector<double>& rv, const std::vector<double
   return o;
 }
 
+// Leaf values and their combine: fp64 (sup_decompose's callback) or
+// double-double (decompose_dd: -o / -u with -q leaves).
+struct DblOps {
+  typedef double V;
+  static V zero() { return 0.0; }
+  static V add(V a, V b) { return a + b; }
+  static V div(V a, double d) { return a / d; }
+};
+struct DdOps {
+  typedef dd V;
+  static V zero() { return dd{0.0, 0.0}; }
+  static V add(V a, V b) { return dd_add(a, b); }
+  static V div(V a, double d) { return dd_div_d(a, d); }
+};
+
+template <class Ops>
 struct Decomposer {
+  typedef typename Ops::V V;
   sup_reduce_opts r;
-  sup_leaf_fn fn;
-  void* user;
+  std::function<int(const double*, int, V*)> fn;
   int leaves = 0;
   int rc = SUP_OK;
 
-  double leaf(const Mat& m) {
-    if (rc) return 0.0;
+  V leaf(const Mat& m) {
+    if (rc) return Ops::zero();
     if (m.n > SUP_MAX_N) {
       set_error("a leaf of order " + std::to_string(m.n) + " remains after the reductions (the engine takes n <= " +
                 std::to_string(SUP_MAX_N) + "; try -o)");
       rc = SUP_EUNSUPPORTED;
-      return 0.0;
+      return Ops::zero();
     }
     ++leaves;
-    double v = 0.0;
-    const int e = fn(m.a.data(), m.n, user, &v);
+    V v = Ops::zero();
+    const int e = fn(m.a.data(), m.n, &v);
     if (e) {
       rc = e;
       if (std::string(sup_last_error()).empty()) set_error("leaf permanent failed");
@@ -263,23 +281,23 @@ struct Decomposer {
   }
 
   // main.cpp:1127-1259 scale_and_calculate: perm(A) = perm(D_r A D_c) / prod(cv) / prod(rv).
-  double scale_then(const Mat& m, bool then_compress) {
+  V scale_then(const Mat& m, bool then_compress) {
     std::vector<double> rv, cv;
-    if (rc) return 0.0;
-    if ((rc = scalesk(m, r.scale_threshold, rv, cv))) return 0.0;
+    if (rc) return Ops::zero();
+    if ((rc = scalesk(m, r.scale_threshold, rv, cv))) return Ops::zero();
     Mat s = scaled(m, rv, cv);
-    double v = then_compress ? singletons(s) : leaf(s);
-    for (int i = 0; i < m.n; ++i) v /= cv[i];
-    for (int i = 0; i < m.n; ++i) v /= rv[i];
+    V v = then_compress ? singletons(s) : leaf(s);
+    for (int i = 0; i < m.n; ++i) v = Ops::div(v, cv[i]);
+    for (int i = 0; i < m.n; ++i) v = Ops::div(v, rv[i]);
     return v;
   }
 
   // main.cpp:993-1063 compress_and_calculate_recursive
-  double recurse(Mat& m) {
-    if (rc) return 0.0;
+  V recurse(Mat& m) {
+    if (rc) return Ops::zero();
     const int md = min_deg(m);
     if (md < r.max_deg && m.n > r.min_n) {
-      if (md == 0) return 0.0;  // an empty row or column
+      if (md == 0) return Ops::zero();  // an empty row or column
       if (md == 1) {
         d1(m);
         return recurse(m);
@@ -290,24 +308,60 @@ struct Decomposer {
       }
       Mat m2;
       d34(m, m2, md);
-      const double left = recurse(m);
-      return left + recurse(m2);
+      const V left = recurse(m);
+      return Ops::add(left, recurse(m2));
     }
     return r.scale_threshold > 0.0 ? scale_then(m, false) : leaf(m);
   }
 
   // main.cpp:1065-1100 compress_singleton_and_then_recurse
-  double singletons(Mat& m) {
+  V singletons(Mat& m) {
     bool comp = true;
     while (comp && m.n > 1) {
       comp = d1(m) || d2(m);
-      if (comp && has_empty(m)) return 0.0;  // rank deficient: perm = 0
+      if (comp && has_empty(m)) return Ops::zero();  // rank deficient: perm = 0
     }
     return recurse(m);
   }
+
+  // the whole request: main.cpp:1640-1660 (-u scales the whole matrix first,
+  // then -o compresses it and scales each leaf again; -o alone compresses;
+  // neither = one leaf)
+  V run(Mat& m) { return r.scale_threshold > 0.0 ? scale_then(m, r.compress != 0) : r.compress ? singletons(m) : leaf(m); }
 };
 
+// d34 splits a row of degree 3 or 4 (main.cpp:1007 hard-codes minDeg < 5), and
+// needs a zero column and two surviving merges (order >= 5): larger max_deg
+// would split a degree-5+ row on its first four nonzeros, a smaller min_n
+// would recurse into n = 0 leaves
+int check_reduce_opts(const sup_reduce_opts& r, const char* who) {
+  if (r.max_deg < 1 || r.max_deg > 5 || r.min_n < 4) {
+    set_error(std::string(who) + ": need 1 <= max_deg <= 5 and min_n >= 4 (got max_deg " + std::to_string(r.max_deg) +
+              ", min_n " + std::to_string(r.min_n) + ")");
+    return SUP_EINVAL;
+  }
+  return SUP_OK;
+}
+
 }  // namespace
+
+int decompose_dd(const double* A, int n, const sup_reduce_opts& r,
+                 const std::function<int(const double*, int, dd*)>& leaf, dd* out, int* n_leaves) {
+  set_error("");
+  if (int rc = check_reduce_opts(r, "sup_perman_reduced_quad")) return rc;
+  Decomposer<DdOps> d;
+  d.r = r;
+  d.fn = leaf;
+  Mat m;
+  m.n = n;
+  m.a.assign(A, A + (size_t)n * n);
+  const dd v = d.run(m);
+  if (d.rc) return d.rc;
+  *out = v;
+  if (n_leaves) *n_leaves = d.leaves;
+  return SUP_OK;
+}
+
 }  // namespace sup
 
 using namespace sup;
@@ -330,32 +384,18 @@ int sup_decompose(const void* mat, sup_dtype t, int n, const sup_reduce_opts* r_
     return SUP_EINVAL;
   }
   set_error("");
-  Decomposer d;
+  Decomposer<DblOps> d;
   if (r_in) d.r = *r_in;
   else sup_reduce_opts_init(&d.r);
-  // d34 splits a row of degree 3 or 4 (main.cpp:1007 hard-codes minDeg < 5), and
-  // needs a zero column and two surviving merges (order >= 5): larger max_deg
-  // would split a degree-5+ row on its first four nonzeros, a smaller min_n
-  // would recurse into n = 0 leaves
-  if (d.r.max_deg < 1 || d.r.max_deg > 5 || d.r.min_n < 4) {
-    set_error("sup_decompose: need 1 <= max_deg <= 5 and min_n >= 4 (got max_deg " + std::to_string(d.r.max_deg) +
-              ", min_n " + std::to_string(d.r.min_n) + ")");
-    return SUP_EINVAL;
-  }
-  d.fn = fn;
-  d.user = user;
+  if (int rc = check_reduce_opts(d.r, "sup_decompose")) return rc;
+  d.fn = [fn, user](const double* a, int k, double* v) { return fn(a, k, user, v); };
   Mat m;
   m.n = n;
   m.a.resize((size_t)n * n);
   for (size_t i = 0; i < m.a.size(); ++i)
     m.a[i] = t == SUP_INT32 ? (double)((const int32_t*)mat)[i]
              : t == SUP_FLOAT32 ? (double)((const float*)mat)[i] : ((const double*)mat)[i];
-  double v;
-  // main.cpp:1640-1660: -u scales the whole matrix first (then -o compresses
-  // it and scales each leaf again); -o alone compresses; neither = one leaf
-  if (d.r.scale_threshold > 0.0) v = d.scale_then(m, d.r.compress != 0);
-  else if (d.r.compress) v = d.singletons(m);
-  else v = d.leaf(m);
+  const double v = d.run(m);
   if (d.rc) return d.rc;
   *out = v;
   if (n_leaves) *n_leaves = d.leaves;

@@ -5,6 +5,7 @@
 // on the host on every call.
 #pragma once
 #include <stdint.h>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -234,6 +235,11 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
                  double* parts, double* kernel_ms);
 void cpu_dd_range(const Plan& P, const std::vector<double>& x0dd, uint64_t c0, uint64_t c1, int threads,
                   double* parts);
+// -o / -u reductions with double-double leaves and combine
+// (sup_perman_reduced_quad); leaf(a, n, &v) computes one leaf.
+struct dd;
+int decompose_dd(const double* A, int n, const sup_reduce_opts& r,
+                 const std::function<int(const double*, int, dd*)>& leaf, dd* out, int* n_leaves);
 // Permanent in double-double (sup_perman_quad): *hi + *lo.
 int quad_perman(const double* A, int n, const sup_opts& o, bool on_cpu, double* hi, double* lo, double* kernel_ms,
                 int* devices_used);

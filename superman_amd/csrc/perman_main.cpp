@@ -16,7 +16,8 @@
 // int path is fp64): on -g with -p5/-p6 it uses -d devices, with -c alone
 // the -t host threads.  -q (v2's quad calculation, main.cpp:141-142): the
 // dense walk in double-double (sup_perman_quad), -d devices with -p5/-p6,
-// -t host threads with -c; prints hi and the hi + lo pair.
+// -t host threads with -c; with -o / -u every leaf and the combine in
+// double-double (sup_perman_reduced_quad); prints hi and the hi + lo pair.
 #include <getopt.h>
 
 #include <chrono>
@@ -249,18 +250,14 @@ int main(int argc, char** argv) {
   }
 
   if (c.quad) {  // double-double dense walk (any -p: the sum does not depend on the kernel)
-    if (reduce) {
-      std::fprintf(stderr, "perman: -q does not combine with -o / -u\n");
-      sup_free(mat);
-      return 1;
-    }
     if (c.gpu && c.perman_algo != 5 && c.perman_algo != 6 && c.perman_algo != 8) o.gpu_num = 1;
     double hi = 0.0, lo = 0.0;
     sup_stats st;
     int rc = SUP_OK;
     const auto t0 = std::chrono::steady_clock::now();
     for (int rep = 0; rep < c.reps && rc == SUP_OK; ++rep)
-      rc = sup_perman_quad(mat, t, n, &o, c.gpu ? 0 : 1, &hi, &lo, &st);
+      rc = reduce ? sup_perman_reduced_quad(mat, t, n, &o, c.gpu ? 0 : 1, &ro, &hi, &lo, &st)
+                  : sup_perman_quad(mat, t, n, &o, c.gpu ? 0 : 1, &hi, &lo, &st);
     const double sec =
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() / (double)c.reps;
     sup_free(mat);

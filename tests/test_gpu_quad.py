@@ -77,3 +77,18 @@ def test_cli_quad_gpu(sup):
     hi = float([l for l in out.splitlines() if l.startswith("Permanent:")][0].split()[1])
     assert hi == sup.perman_quad(sup.read_matrix(fixture_path("synth/20_0.50_double"))[0], cpu=True)[0]
     assert "gpu_perman64_quad" in out
+
+
+def test_gpu_chesapeake_reduced_quad(sup):
+    """chesapeake (n = 39 pattern matrix): its exact permanent is 13173481190272
+    (two independent exact GPU computations, test_gpu_exact.py).  The fp64 -o
+    reduction loses every digit to the fp64 walk's cancellation in its merged
+    leaves (the reference's own -o gives -2.6e24); with
+    double-double leaves and combine, and the integer merges exact, -o -q gives
+    the exact value."""
+    a = sup.read_matrix(fixture_path("mtx/chesapeake.mtx"))[0]
+    (hi, lo), st = sup.perman_reduced_quad(a, min_n=30, return_stats=True)
+    assert st["leaves"] > 100
+    assert Fraction(hi) + Fraction(lo) == 13173481190272
+    (dh, dl) = sup.perman_quad(a)
+    assert Fraction(dh) + Fraction(dl) == 13173481190272

@@ -67,3 +67,25 @@ def test_quad_tiny_and_degenerate(sup):
     hi, lo = sup.perman_quad(a, cpu=True)
     want = Fraction(479001600) * Fraction(0.1) ** 12
     assert abs(Fraction(hi) + Fraction(lo) - want) <= want * Fraction(1, 2 ** 95)
+
+
+def test_reduced_quad_int_is_exact(sup):
+    """-o with double-double leaves and combine: on an integer matrix the d1/d2/d34
+    leaves are integer matrices, so hi + lo is the exact permanent."""
+    rng = np.random.default_rng(3)
+    n = 26
+    a = np.where(rng.random((n, n)) < 0.12, rng.integers(1, 4, (n, n)), 0).astype(np.int32)
+    a[np.arange(n), rng.permutation(n)] = 1
+    (hi, lo), st = sup.perman_reduced_quad(a, cpu=True, threads=8, min_n=12, return_stats=True)
+    assert st["leaves"] > 10
+    assert Fraction(hi) + Fraction(lo) == sup.perman_reduced_exact(a, cpu=True, threads=8, min_n=12)
+
+
+def test_reduced_quad_scaled_vs_direct(sup):
+    """-o -u: leaves scaled (scalesk) in fp64, factors divided out in double-double."""
+    a = sup.read_matrix(fixture_path("mtx/can_24_ps.mtx"))[0]
+    hi, lo = sup.perman_quad(a, cpu=True, threads=8)
+    for scale in (None, 4):
+        (rh, rl), st = sup.perman_reduced_quad(a, scale=scale, cpu=True, threads=8, min_n=20, return_stats=True)
+        assert st["leaves"] >= 1
+        assert abs(rh - hi) <= 1e-13 * abs(hi), (scale, rh, hi)
