@@ -150,15 +150,6 @@ ProdTree make_tree(const std::vector<int>& rows, const std::vector<uint32_t>& rs
   return t;
 }
 
-// Signature of node i's parent (-1 for the root): a node dirty exactly when
-// its parent is need not stay live between steps.
-int parent_sig(const ProdTree& t, int i) {
-  const int id = t.items() + i;
-  for (int j = i + 1; j < t.K(); ++j)
-    if (t.a[j] == id || t.b[j] == id) return (int)t.sig[j];
-  return -1;
-}
-
 // The segmented walk's structure in engine rows (rows in seg_row_order):
 // touched[k] = rows walk bit k touches; segment 0 = rows [0, len0) (walk bit
 // 0's rows; [0, s_end) touched by some walk bit >= 1, [s_end, len0) not);
