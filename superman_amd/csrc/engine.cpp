@@ -188,8 +188,29 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
     for (int k = 0; k < m; ++k) P.colmap[L + k] = order[k], used[order[k]] = 1;
     for (int e = 0; e < L; ++e) P.colmap[e] = order[m + e], used[order[m + e]] = 1;
     int e = L + m;
-    for (int c = 0; c < nb; ++c)
-      if (!used[c]) P.colmap[e++] = c;
+    // High bits (the wave-chunk index).  The segmented walk on an integer
+    // matrix skips the wave-chunks whose rows untouched by the walk columns are
+    // exactly zero in every lane; a high column with no nonzero in those rows
+    // never changes that, so those columns take the top bits: contiguous
+    // shards (sup_perman_shard, -p5) then see the same skip pattern.  (Config
+    // 5 before: the top chunk bit alone decided skipping, half the shards had
+    // nothing to walk at 2, 4 and 8 GPUs.)  Otherwise matrix order.
+    std::vector<char> top(n, 0);
+    if (kind == kWalkSeg) {
+      bool integral = true;
+      for (size_t i = 0; i < (size_t)n * n && integral; ++i) integral = A[i] == std::floor(A[i]);
+      std::vector<char> wrow(n, 0);
+      for (int k = 0; k < m; ++k)
+        for (int i = 0; i < n; ++i) wrow[i] |= A[(size_t)i * n + order[k]] != 0.0;
+      for (int c = 0; c < nb && integral; ++c) {
+        top[c] = 1;
+        for (int i = 0; i < n; ++i)
+          if (!wrow[i] && A[(size_t)i * n + c] != 0.0) top[c] = 0;
+      }
+    }
+    for (int pass = 0; pass < 2; ++pass)
+      for (int c = 0; c < nb; ++c)
+        if (!used[c] && top[c] == pass) P.colmap[e++] = c;
   }
 
   // ---- engine row order

@@ -54,13 +54,18 @@ def seg_skip_fraction(sup, a, kernel="sparse"):
     chunks the generated kernel skips; restated from the plan's column map in
     numpy (x0 = a[:, n-1] - rowsum / 2, chunk-start Gray state of the lane and
     chunk bits)."""
+    return float(seg_skipped_chunks(sup, a, kernel).mean())
+
+
+def seg_skipped_chunks(sup, a, kernel="sparse"):
+    """Per wave-chunk (index order): True when the segmented kernel skips it."""
     n = a.shape[0]
     info = sup.plan_info(a, kernel, jit=1)
     cm, L, m = [int(c) for c in info["colmap"]], info["L"], info["m"]
     x0 = a[:, n - 1] - a.sum(1) / 2
     rest = [j for j in range(n) if not a[j, cm[L:L + m]].any()]
     if not rest:
-        return 0.0
+        return np.zeros(1 << (n - 1 - L - m), bool)
     cols = cm[:L] + cm[L + m:]
     h = len(cols) - L
     allz = np.ones(1 << h, bool)
@@ -71,4 +76,4 @@ def seg_skip_fraction(sup, a, kernel="sparse"):
         for k, c in enumerate(cols):
             x += ((g >> k) & 1)[:, None] * a[rest][:, c][None, :]
         allz &= (x == 0).any(1)
-    return float(allz.mean())
+    return allz

@@ -245,3 +245,22 @@ def test_seg_codegen_schedule_invariance_gpu(sup, orc, monkeypatch):
             monkeypatch.setenv(knob, v)
             assert sup.perman(a, algo=4, kernel="seg") == want, (knob, v)
         monkeypatch.delenv(knob)
+
+
+def test_seg_config5_shards_balanced_gpu(sup):
+    """Config 5 (n = 44 d = 0.15 int, -p8 -s -r2): with the skip-neutral high
+    columns on the top chunk bits, the 8 contiguous shards of the engine's walk
+    visit the same number of states (sup_stats.visited_steps), and they fold to
+    the one-GPU sum bit for bit."""
+    a = sup.skip_order(sup.read_matrix(fixture_path("synth44_0.15_int"))[0])[0]
+    full, st = sup.perman_shard(a, 0, 1, kernel="skip", jit=1, return_stats=True)
+    assert st["walk_kind"] == 3 and 0 < st["visited_steps"] < st["gray_steps"] // 2
+    parts, vis = [], []
+    for r in range(8):
+        p, s = sup.perman_shard(a, r, 8, kernel="skip", jit=1, return_stats=True)
+        parts.append(p)
+        vis.append(s["visited_steps"])
+    assert max(vis) == min(vis) and sum(vis) == st["visited_steps"]
+    while len(parts) > 1:
+        parts = [parts[i] + parts[i + 1] for i in range(0, len(parts), 2)]
+    assert parts[0] == full

@@ -247,3 +247,20 @@ def test_seg_uncompilable_pattern_falls_back(sup, tmp_path, monkeypatch):
     with pytest.raises(sup.SupError):
         sup.plan_info(a, "seg", jit=1)
     assert sup.prepare(_rand(24, 0.5, 11), "seg")["kind"] == "seg"
+
+
+def test_seg_shards_balanced_under_chunk_skip(sup):
+    """Config 5 (n = 44 d = 0.15 int, SkipOrder): the segmented walk skips 87 %
+    of its wave-chunks.  The high columns that touch no walk-untouched row never
+    change a skip, and the planner puts them on the top chunk bits, so the
+    contiguous shards of sup_perman_shard / -p5 walk equal chunk counts at 2, 4
+    and 8 GPUs (before: the top bit alone decided, half the shards were empty).
+    Restated in numpy from the plan's column map (conftest.seg_skipped_chunks)."""
+    from conftest import seg_skipped_chunks
+    a = sup.skip_order(sup.read_matrix(fixture_path("synth44_0.15_int"))[0])[0]
+    walked = ~seg_skipped_chunks(sup, a, "sparse")
+    assert 0.05 < walked.mean() < 0.5
+    C = walked.size
+    for world in (2, 4, 8):
+        w = [int(walked[C * r // world:C * (r + 1) // world].sum()) for r in range(world)]
+        assert max(w) == min(w), (world, w)
