@@ -27,5 +27,8 @@ struct ApproxParams {
 // words: 1, 2, 4, 8 or 16 (n <= 64 * words).
 hipError_t launch_approx(int words, const ApproxParams& p, int grid, hipStream_t s);
 hipError_t approx_occupancy(int words, int method, int* blocks_per_cu);
+// Cooperative form (one wave per sample, factors in LDS; same bits).
+hipError_t launch_approx_coop(int words, const ApproxParams& p, int grid, hipStream_t s);
+hipError_t approx_coop_occupancy(int words, int method, int n, int* blocks_per_cu);
 
 }  // namespace sup

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -147,6 +148,7 @@ void cpu_item(const Job& J, uint64_t b0, uint64_t b1, int threads, double out[3]
 // One device: its own buffers, items taken from the shared queue.
 struct DevWorker {
   int dev = 0, cus = 0, grid = 0;
+  bool coop = false;  // one wave per sample (approx.hip approx_coop), same bits
   hipStream_t st = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   uint64_t *d_row = nullptr, *d_col = nullptr;
@@ -161,8 +163,14 @@ struct DevWorker {
     hipDeviceProp_t prop;
     AHIP(hipGetDeviceProperties(&prop, dev));
     cus = prop.multiProcessorCount;
+    // The cooperative form for large n: the scaling estimator from n > 64 (its
+    // per-lane factors live in an HBM scratch), Rasmussen from n > 256;
+    // SUP_APPROX_COOP=0/1 forces the form (same bits either way).
+    coop = (J.method == 1 && J.P->W >= 2) || J.P->W >= 8;
+    if (const char* e = std::getenv("SUP_APPROX_COOP")) coop = std::atoi(e) != 0;
     int occ = 1;
-    AHIP(approx_occupancy(J.P->W, J.method, &occ));
+    if (coop) AHIP(approx_coop_occupancy(J.P->W, J.method, J.P->n, &occ));
+    else AHIP(approx_occupancy(J.P->W, J.method, &occ));
     grid = std::max(1, cus * std::max(1, occ));
     grid = (int)std::min<uint64_t>((uint64_t)grid, (item + 3) / 4);
     AHIP(hipStreamCreate(&st));
@@ -177,7 +185,7 @@ struct DevWorker {
     AHIP(hipMalloc(&d_scr, (pairwise_scratch_size(item) + 1) * sizeof(double)));
     AHIP(hipMalloc(&d_out, 3 * sizeof(double)));
     AHIP(hipMalloc(&d_cnt, sizeof(unsigned)));
-    if (J.method == 1) AHIP(hipMalloc(&d_dr, 2ull * J.P->n * (size_t)grid * kBlock * sizeof(float)));
+    if (J.method == 1 && !coop) AHIP(hipMalloc(&d_dr, 2ull * J.P->n * (size_t)grid * kBlock * sizeof(float)));
     return SUP_OK;
   }
   int run(const Job& J, uint64_t b0, uint64_t nb, double out[3]) {
@@ -198,7 +206,8 @@ struct DevWorker {
     p.lanes_total = (uint32_t)grid * kBlock;
     AHIP(hipMemsetAsync(d_cnt, 0, sizeof(unsigned), st));
     AHIP(hipEventRecord(e0, st));
-    AHIP(launch_approx(J.P->W, p, grid, st));
+    if (coop) AHIP(launch_approx_coop(J.P->W, p, grid, st));
+    else AHIP(launch_approx(J.P->W, p, grid, st));
     AHIP(hipEventRecord(e1, st));
     for (int k = 0; k < 3; ++k) AHIP(launch_pairwise_reduce(d_part + k * nb, nb, d_scr, d_out + k, st));
     AHIP(hipMemcpyAsync(out, d_out, 3 * sizeof(double), hipMemcpyDeviceToHost, st));

@@ -68,12 +68,24 @@ def seg_skipped_chunks(sup, a, kernel="sparse"):
         return np.zeros(1 << (n - 1 - L - m), bool)
     cols = cm[:L] + cm[L + m:]
     h = len(cols) - L
+    # x = x0 + sum_k bit_k(gray(p)) a[:, cols[k]] with p = (chunk << L) | lane:
+    # bits >= L are gray(chunk), bits < L depend on the lane and chunk & 1
+    # (integer matrices: every sum is exact, so the split does not change a bit)
+    ar = a[rest].astype(np.float64)
+    ch = np.arange(1 << h, dtype=np.int64)
+    gc = ch ^ (ch >> 1)
+    xc = np.tile(x0[rest].astype(np.float64), (1 << h, 1))
+    for k in range(h):
+        xc += ((gc >> k) & 1)[:, None] * ar[:, cols[L + k]][None, :]
     allz = np.ones(1 << h, bool)
-    for lane in range(1 << L):
-        p = (np.arange(1 << h, dtype=np.int64) << L) | lane
-        g = p ^ (p >> 1)
-        x = np.tile(x0[rest], (1 << h, 1))
-        for k, c in enumerate(cols):
-            x += ((g >> k) & 1)[:, None] * a[rest][:, c][None, :]
-        allz &= (x == 0).any(1)
+    for par in (0, 1):
+        sel = (ch & 1) == par
+        xp = xc[sel]
+        az = np.ones(len(xp), bool)
+        for lane in range(1 << L):
+            pl = lane | (par << L)
+            gl = pl ^ (pl >> 1)
+            xl = sum(((gl >> k) & 1) * ar[:, cols[k]] for k in range(L)) if L else 0.0
+            az &= ((xp + xl) == 0).any(1)
+        allz[sel] = az
     return allz

@@ -52,3 +52,16 @@ def test_gpu_unbiased_grid(sup):
         est, st = sup.approx(g, algo, samples=1 << 22, seed=23, return_stats=True)
         assert abs(est - t) < 5 * st["std_error"], (algo, est, t, st["std_error"])
         assert st["std_error"] < 0.01 * t
+
+
+@pytest.mark.parametrize("algo", [1, 2])
+def test_gpu_coop_equals_per_lane(sup, monkeypatch, algo):
+    """The cooperative form (one wave per sample, factors in LDS; approx.hip
+    approx_coop) gives every block sum of the per-lane form bit for bit."""
+    for g, samples in ((sup.grid_graph(10, 13), 4096), (sup.grid_graph(16, 16), 2048), (sup.grid_graph(36, 36), 256)):
+        got = {}
+        for form in ("0", "1"):
+            monkeypatch.setenv("SUP_APPROX_COOP", form)
+            got[form] = sup.approx(g, algo, samples=samples, seed=29, return_stats=True)
+        assert got["0"][0] == got["1"][0]
+        assert got["0"][1]["std_error"] == got["1"][1]["std_error"]
