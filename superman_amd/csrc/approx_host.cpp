@@ -163,10 +163,12 @@ struct DevWorker {
     hipDeviceProp_t prop;
     AHIP(hipGetDeviceProperties(&prop, dev));
     cus = prop.multiProcessorCount;
-    // The cooperative form for large n: the scaling estimator from n > 64 (its
-    // per-lane factors live in an HBM scratch), Rasmussen from n > 256;
-    // SUP_APPROX_COOP=0/1 forces the form (same bits either way).
-    coop = (J.method == 1 && J.P->W >= 2) || J.P->W >= 8;
+    // The cooperative form for large n (tools/probe_approx_coop.py,
+    // profiles/r2/probe_approx_coop.log): the scaling estimator from n > 96
+    // (its per-lane factors live in an HBM scratch: 0.81x at n = 72, 2.5x at
+    // 128, 110x at 288 and 648), Rasmussen from n > 128 (0.35x at 128, 4.6x at
+    // 288, 5x at 648); SUP_APPROX_COOP=0/1 forces the form (same bits).
+    coop = (J.method == 1 && J.P->n > 96) || J.P->n > 128;
     if (const char* e = std::getenv("SUP_APPROX_COOP")) coop = std::atoi(e) != 0;
     int occ = 1;
     if (coop) AHIP(approx_coop_occupancy(J.P->W, J.method, J.P->n, &occ));

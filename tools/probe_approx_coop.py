@@ -6,7 +6,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import superman_amd as S  # noqa: E402
 
-for (m, n) in ((8, 8), (12, 12), (16, 16), (24, 24), (36, 36)):
+for (m, n) in ((8, 8), (12, 12), (14, 14), (16, 16), (20, 20), (24, 24), (36, 36)):
     g = S.grid_graph(m, n)
     for algo in (1, 2):
         res = {}
