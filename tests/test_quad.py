@@ -89,3 +89,28 @@ def test_reduced_quad_scaled_vs_direct(sup):
         (rh, rl), st = sup.perman_reduced_quad(a, scale=scale, cpu=True, threads=8, min_n=20, return_stats=True)
         assert st["leaves"] >= 1
         assert abs(rh - hi) <= 1e-13 * abs(hi), (scale, rh, hi)
+
+
+def test_cli_quad_cpu(sup, tmp_path):
+    """perman -c -q (and with -o): the double-double lines of the CLI."""
+    import os
+    import subprocess
+    rng = np.random.default_rng(5)
+    n = 16
+    a = np.where(rng.random((n, n)) < 0.3, rng.integers(1, 4, (n, n)), 0).astype(np.int32)
+    a[np.arange(n), rng.permutation(n)] = 1
+    path = tmp_path / "m16"
+    nz = np.argwhere(a != 0)
+    with open(path, "w") as f:
+        f.write(f"{n} {len(nz)} int\n")
+        for i, j in nz:
+            f.write(f"{i} {j} {a[i, j]}\n")
+    exe = os.path.join(os.path.dirname(sup.__file__), "bin", "perman")
+    e = sup.perman_exact(a, cpu=True)
+    for extra in ([], ["-o"]):
+        out = subprocess.run([exe, "-f", str(path), "-c", "-q", "-t", "4"] + extra, capture_output=True, text=True,
+                             check=True).stdout
+        assert "cpu_perman64_quad" in out
+        hi, lo = [float(v) for v in [l for l in out.splitlines() if l.startswith("Permanent (double-double)")][0]
+                  .split(":")[1].split()]
+        assert Fraction(hi) + Fraction(lo) == e
