@@ -351,7 +351,7 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
   const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0};
   for (const char* knob :
        {"SUP_JIT_CC", "SUP_JIT_B", "SUP_JIT_STORAGE", "SUP_JIT_POLISH", "SUP_JIT_STARTS", "SUP_JIT_KP", "SUP_JIT_ACCFLOAT",
-        "SUP_JIT_SCHED", "SUP_JIT_NOVERIFY"})
+        "SUP_JIT_SCHED", "SUP_JIT_NOVERIFY", "SUP_JIT_PHASE"})
     if (std::getenv(knob)) return plan_for_uncached(A, n, kernel, lay, P, jit, ndev, dev);  // experiment knobs: never cached
   {
     std::lock_guard<std::mutex> g(g_plan_mu);

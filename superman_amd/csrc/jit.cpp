@@ -1302,6 +1302,11 @@ struct Gen {
     o << "  const uint32_t lane = threadIdx.x & 63u;\n";
     o << "  const bool lane_valid = lane < " << (1u << L) << "u;\n";
     o << "  const uint32_t lane_par = __builtin_popcount(lane) & 1u;\n";
+    // experiment (SUP_JIT_PHASE=k): odd workgroups start 64 k cycles late, so
+    // the two waves sharing a SIMD (one per workgroup) are out of phase
+    if (const char* e = std::getenv("SUP_JIT_PHASE"))
+      if (std::atoi(e) > 0)
+        o << "  if (blockIdx.x & 1u) __builtin_amdgcn_s_sleep(" << std::min(127, std::atoi(e)) << ");\n";
     o << "  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {\n";
     o << "    double keep = 0.0;\n";
     o << "    uint32_t vkeep = 0;\n";  // per chunk: Gray steps walked per lane (0 when skipped)
