@@ -208,6 +208,7 @@ int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int
   sup_opts o;
   if (o_in) o = *o_in;
   else sup_opts_init(&o);
+  if ((rc = check_walk_opts(o))) return rc;
   std::vector<double> A;
   if ((rc = to_double(mat, t, n, A))) return rc;
   Plan P;
@@ -361,11 +362,11 @@ int sup_prepare(const void* mat, sup_dtype t, int n, sup_kernel kernel, const su
   if ((rc = check_walk_opts(o))) return rc;
   // compiles may already happen while planning (the live-value budget is
   // checked against the compiler), so the time is taken around both
-  const double before = jit_compile_ms_total();
+  const double before = jit_compile_ms_thread();
   if ((rc = plan_for(A.data(), n, kernel, layout_for(n, o), P, o.jit, o.gpu_num, o.device_id))) return rc;
   if (walk_kind) *walk_kind = P.lds ? 4 : (int)P.kind;
   if (P.kind == kWalkSeg && (rc = jit_compile_only(P, nullptr))) return rc;
-  if (compile_ms) *compile_ms = jit_compile_ms_total() - before;
+  if (compile_ms) *compile_ms = jit_compile_ms_thread() - before;
   return SUP_OK;
 }
 

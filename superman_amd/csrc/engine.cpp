@@ -17,6 +17,8 @@
 #include <thread>
 #include <tuple>
 
+#include <unistd.h>  // environ
+
 namespace sup {
 
 // ---------------------------------------------------------------- errors --
@@ -330,13 +332,32 @@ namespace {
 struct PlanKey {
   uint64_t hash;
   int n, kernel, L, m, jit, ndev;
+  bool fixed;      // walk length asked for (sup_opts::walk_log2): make_seg_plan keeps it
+  uint64_t knobs;  // SUP_JIT_* experiment settings the planner and code generator read
   bool operator<(const PlanKey& o) const {
-    return std::tie(hash, n, kernel, L, m, jit, ndev) < std::tie(o.hash, o.n, o.kernel, o.L, o.m, o.jit, o.ndev);
+    return std::tie(hash, n, kernel, L, m, jit, ndev, fixed, knobs) <
+           std::tie(o.hash, o.n, o.kernel, o.L, o.m, o.jit, o.ndev, o.fixed, o.knobs);
   }
 };
 std::mutex g_plan_mu;
 std::map<PlanKey, std::pair<std::vector<double>, Plan>> g_plans;
 constexpr size_t kPlanCacheMax = 32;
+
+// Hash of every SUP_JIT_* variable that shapes a plan or its generated source
+// (experiment knobs), so a process that changes one gets a fresh plan; the
+// cache location, source dumps and log verbosity do not change a plan.
+uint64_t knob_hash() {
+  uint64_t h = 1469598103934665603ull;
+  for (char** e = environ; e && *e; ++e) {
+    const char* v = *e;
+    if (std::strncmp(v, "SUP_JIT_", 8) != 0 || !std::strncmp(v, "SUP_JIT_CACHE_DIR=", 18) ||
+        !std::strncmp(v, "SUP_JIT_DUMP=", 13) || !std::strncmp(v, "SUP_JIT_VERBOSE=", 16))
+      continue;
+    for (const char* c = v; *c; ++c) h = (h ^ (unsigned char)*c) * 1099511628211ull;
+    h = (h ^ 0xffu) * 1099511628211ull;
+  }
+  return h;
+}
 }  // namespace
 
 int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit, int ndev, int dev) {
@@ -348,11 +369,7 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
     h = (h ^ b) * 1099511628211ull;
   }
   // ndev only feeds auto mode's compile-or-not decision
-  const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0};
-  for (const char* knob :
-       {"SUP_JIT_CC", "SUP_JIT_B", "SUP_JIT_STORAGE", "SUP_JIT_POLISH", "SUP_JIT_STARTS", "SUP_JIT_KP", "SUP_JIT_ACCFLOAT",
-        "SUP_JIT_SCHED", "SUP_JIT_NOVERIFY", "SUP_JIT_PHASE"})
-    if (std::getenv(knob)) return plan_for_uncached(A, n, kernel, lay, P, jit, ndev, dev);  // experiment knobs: never cached
+  const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0, lay.fixed, knob_hash()};
   {
     std::lock_guard<std::mutex> g(g_plan_mu);
     auto it = g_plans.find(key);
@@ -881,11 +898,15 @@ int rccl_allreduce_partials(const std::vector<int>& devs, const std::vector<std:
 int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uint64_t c1,
              SchedResult& out) {
   out = SchedResult();
-  struct JitClock {  // hiprtc time spent while this schedule ran
+  // hiprtc time spent while this schedule ran: on the calling thread, or the
+  // most any device worker thread spent (they compile concurrently)
+  double worker_jit_ms = 0.0;
+  struct JitClock {
     SchedResult& o;
-    double t0 = jit_compile_ms_total();
-    ~JitClock() { o.compile_ms = jit_compile_ms_total() - t0; }
-  } jit_clock{out};
+    const double& workers;
+    double t0 = jit_compile_ms_thread();
+    ~JitClock() { o.compile_ms = std::max(jit_compile_ms_thread() - t0, workers); }
+  } jit_clock{out, worker_jit_ms};
   int ndev = 0;
   int rc = device_count(&ndev);
   if (rc) return rc;
@@ -934,6 +955,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
       }
     out.dev_partials.resize(G);
     for (int g = 0; g < G; ++g) {
+      worker_jit_ms = std::max(worker_jit_ms, rr[g].compile_ms);
       out.dev_partials[g] = rr[g].partial;
       out.kernel_ms = std::max(out.kernel_ms, rr[g].kernel_ms);
       out.visited += rr[g].visited;
@@ -967,7 +989,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   const uint64_t nitems = (total + item - 1) / item;
   std::vector<double> ipart(nitems, 0.0);
   std::vector<int> owner(nitems, 0);
-  std::vector<double> dev_ms(G + 1, 0.0);
+  std::vector<double> dev_ms(G + 1, 0.0), dev_jit(G, 0.0);
   std::vector<uint64_t> dev_vis(G + 1, 0);
   std::vector<int> dev_grid(G + 1, 0);
   std::vector<int> rcs(G + 1, SUP_OK);
@@ -1000,6 +1022,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
       owner[it] = g;
       dev_sum[g] += r.partial;
       dev_ms[g] += r.kernel_ms;
+      dev_jit[g] += r.compile_ms;
       dev_vis[g] += r.visited;
       dev_grid[g] = std::max(dev_grid[g], r.grid);
     }
@@ -1032,6 +1055,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     }
   out.devices = G;
   out.cpu_items = cpu_items.load();
+  for (int g = 0; g < G; ++g) worker_jit_ms = std::max(worker_jit_ms, dev_jit[g]);
   for (int g = 0; g <= G; ++g) {
     out.kernel_ms = std::max(out.kernel_ms, dev_ms[g]);
     out.visited += dev_vis[g];

@@ -95,6 +95,7 @@ struct Plan {
   double seg_ops = 0.0;            // fp64 VALU ops per Gray step of the generated kernel
   double seg_skip = 0.0;           // sampled fraction of wave-chunks the kernel skips (integer matrices)
   int seg_regs = 0;                // values live across steps (doubles), estimate
+  int seg_budget = 0;              // live-value budget the storage plan was fitted to
   std::vector<int> jofs;           // [m] offset (doubles) of walk bit k's + block in jtab
   std::vector<double> jtab;        // packed touched values: + block, - block (each padded to 8); then,
                                    // from seg_cbase, the row-copy constants (jit.cpp Gen::tail)
@@ -149,11 +150,22 @@ int jit_occupancy(int dev, const Plan& P, int* blocks_per_cu, double* compile_ms
 int jit_launch(int dev, const Plan& P, const WalkParams& p, int grid, hipStream_t s);
 // Compile (or find in the caches) the specialised kernel of P without loading it.
 int jit_compile_only(const Plan& P, double* compile_ms);
-// Compile (or fetch) P's kernel and read its VGPR count and VGPR spill count
-// from the code object's metadata.
-int jit_code_regs(const Plan& P, int* vgprs, int* vgpr_spills);
-// Milliseconds spent compiling specialised kernels in this process (hiprtc).
-double jit_compile_ms_total();
+// What a compiled kernel does with registers and scratch (codescan.cpp):
+// metadata counts, and the scratch instructions inside its walk loop (the
+// natural loop with the most fp64 VALU work that holds no inner loop with half
+// of it), found by disassembling the code object.
+struct CodeScan {
+  int vgprs = -1, vgpr_spills = -1, scratch_bytes = -1;  // .vgpr_count, .vgpr_spill_count, private segment
+  int insts = 0, scratch_insts = 0, loops = 0;           // whole kernel
+  int loop_scratch = -1, loop_f64 = 0, loop_insts = 0;   // the walk loop (-1: none found)
+};
+int scan_code_object(const std::vector<char>& code, const char* kernel, CodeScan* out);
+// Compile (or fetch) P's kernel and scan it.
+int jit_code_scan(const Plan& P, CodeScan* out);
+// Milliseconds this thread spent compiling specialised kernels (hiprtc; a batch
+// compiled on helper threads counts its wall time here).  Per thread, so
+// concurrent callers do not count each other's compiles.
+double jit_compile_ms_thread();
 
 // Estimated fp64 VALU ops per Gray step of a plan (dense: 2n+1; prefix kernels:
 // sum_k 2^-(k+1) (16 nblk_k + 1)).

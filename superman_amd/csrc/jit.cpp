@@ -62,10 +62,11 @@
 // ~/.cache/superman_amd (SUP_JIT_CACHE_DIR="" disables the disk cache).
 // Debugging / experiment knobs: SUP_JIT_DUMP=<dir> keeps the generated source,
 // SUP_JIT_VERBOSE prints the plan's op count, live values and cached bits;
-// SUP_JIT_CC / _B / _STORAGE / _STARTS / _POLISH / _REGMAX / _KP / _PF /
-// _XSTEP / _WAVES / _LDS force cached bits, pair bits, storage budget, search
-// starts, skip polish, register budget, SGPR pieces per region, prefetch,
-// cross-step regions, occupancy, dynamic LDS.
+// SUP_JIT_CC / _B / _STORAGE / _BUDGET / _STARTS / _POLISH / _REGMAX / _KP /
+// _PF / _XSTEP / _WAVES / _LDS force cached bits, pair bits, storage budget,
+// live-value budget (no compiler check), search starts, skip polish, register
+// budget, SGPR pieces per region, prefetch, cross-step regions, occupancy,
+// dynamic LDS.
 #include <hip/hiprtc.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -91,6 +92,22 @@ namespace sup {
 
 namespace {
 #include "jit_headers.inc"  // kWalkCommonSrc, kWalkParamsSrc (generated from the headers by the Makefile)
+
+// hiprtc time spent by this thread (and the wall time of compile batches it
+// ran on helper threads): per call, not process-wide, so concurrent callers
+// do not count each other's compiles
+thread_local double t_compile_ms = 0.0;
+// Set when hiprtc fails on a segmented walk (an error, or a register
+// allocator that gives up, "maximum depth for recoloring").  Such a failure
+// next to concurrent compiles has crashed the process (LLVM's error path is
+// not thread-safe; sequential compiles after it are fine, test_seg.py), so
+// from then on this process compiles one kernel at a time.
+std::atomic<bool> g_jit_failed{false};
+// Budget candidates compiled at once (host threads) by the compiler check.
+constexpr size_t kMaxParallelCompiles = 8;
+// A kernel with no scratch at all is preferred over one whose spills stay in
+// the chunk start unless that one saves more than this fraction of the ops.
+constexpr double kScratchTolerance = 0.01;
 
 // ---------------------------------------------------------------- planning --
 
@@ -484,6 +501,19 @@ int plan_threads() {
   int t = (int)std::max(1u, std::thread::hardware_concurrency());
   if (const char* e = std::getenv("OMP_NUM_THREADS")) t = std::min(t, std::max(1, std::atoi(e)));
   return std::min(t, 16);
+}
+
+// Run fn(0..count-1) on up to plan_threads() host threads (the caller's
+// included); results are gathered by index, so they do not depend on timing.
+void parallel_tasks(size_t count, const std::function<void(size_t)>& fn, int max_threads = 1 << 20) {
+  std::atomic<size_t> next{0};
+  auto worker = [&]() {
+    for (size_t i = next++; i < count; i = next++) fn(i);
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < std::min({plan_threads(), (int)count, max_threads}); ++t) th.emplace_back(worker);
+  worker();
+  for (auto& t : th) t.join();
 }
 
 int seg_search_starts(int n) {
@@ -1444,6 +1474,24 @@ uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
   return h;
 }
 
+// hiprtc's own version: part of the code-object key, so a disk cache written
+// by another ROCm release is not reused
+std::string hiprtc_version() {
+  int major = 0, minor = 0;
+  if (hiprtcVersion(&major, &minor) != HIPRTC_SUCCESS) return "hiprtc ?";
+  return "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + " hip " + std::to_string(HIP_VERSION);
+}
+
+// Code-object key of a generated source: the source, the compile options, the
+// embedded headers and the compiler's version.
+uint64_t jit_source_key(const std::string& src) {
+  std::string key = src;
+  for (const std::string& opt : jit_opts()) key += "\n//" + opt;
+  key += std::string("\n//") + kWalkCommonSrc + kWalkParamsSrc;
+  key += "\n//" + hiprtc_version();
+  return fnv1a(key);
+}
+
 }  // namespace
 
 int build_seg(Plan& P) {
@@ -1526,7 +1574,9 @@ int build_seg(Plan& P) {
   SR.n = n, SR.m = m, SR.touched = P.touched;
   SR.len0 = P.seg_start[1], SR.s_end = P.sub_start.back(), SR.r_end = P.seg_start.back();
   seg_rows_finish(SR, P.seg_b);
-  auto finish = [&](int budget) {
+  // trees, cached classes and storage plan for live-value budget `budget`,
+  // then the tables and the generated source (Q starts as a copy of P)
+  auto finish = [&SR, n, L, m](Plan& Q, int budget) {
     SegFit f;
     // experiments / tests: SUP_JIT_CC forces cc; SUP_JIT_STORAGE forces the
     // storage budget of the chosen plan (same walk order and trees, other
@@ -1535,90 +1585,132 @@ int build_seg(Plan& P) {
       f = seg_fit(SR, std::max(0, std::min({std::atoi(e), SR.b - 1, kMaxCachedBits})), budget);
     else f = seg_best(SR, kMaxCachedBits, budget);
     if (const char* e = std::getenv("SUP_JIT_STORAGE")) f = seg_fit(SR, f.cc, std::max(0, std::atoi(e)));
-    P.outer_tree = std::move(f.outer);
-    P.inner_tree = std::move(f.inner);
-    P.seg_cc = f.cc;
-    P.seg_ops = f.ops;
-    P.seg_regs = f.regs;
-    P.jofs.assign(m, 0);
-    P.jtab.clear();
+    Q.outer_tree = std::move(f.outer);
+    Q.inner_tree = std::move(f.inner);
+    Q.seg_cc = f.cc;
+    Q.seg_ops = f.ops;
+    Q.seg_regs = f.regs;
+    Q.seg_budget = budget;
+    Q.jofs.assign(m, 0);
+    Q.jtab.clear();
     for (int k = 0; k < m; ++k) {
-      const std::vector<int>& t = P.touched[k];
+      const std::vector<int>& t = Q.touched[k];
       const size_t blk = (t.size() + 7) & ~(size_t)7;
-      P.jofs[k] = (int)P.jtab.size();
-      P.jtab.resize(P.jtab.size() + 2 * std::max<size_t>(blk, 8), 0.0);
+      Q.jofs[k] = (int)Q.jtab.size();
+      Q.jtab.resize(Q.jtab.size() + 2 * std::max<size_t>(blk, 8), 0.0);
       for (size_t i = 0; i < t.size(); ++i) {
-        P.jtab[P.jofs[k] + i] = P.cols[(size_t)(2 * (L + k)) * P.NP + t[i]];
-        P.jtab[P.jofs[k] + blk + i] = P.cols[(size_t)(2 * (L + k) + 1) * P.NP + t[i]];
+        Q.jtab[Q.jofs[k] + i] = Q.cols[(size_t)(2 * (L + k)) * Q.NP + t[i]];
+        Q.jtab[Q.jofs[k] + blk + i] = Q.cols[(size_t)(2 * (L + k) + 1) * Q.NP + t[i]];
       }
     }
-    P.seg_cbase = P.jtab.size();
-    P.seg_kp = 4;
-    if (const char* e = std::getenv("SUP_JIT_KP")) P.seg_kp = std::max(1, std::atoi(e));
-    Gen g(P);
-    P.jit_src = g.source();
+    Q.seg_cbase = Q.jtab.size();
+    Q.seg_kp = 4;
+    if (const char* e = std::getenv("SUP_JIT_KP")) Q.seg_kp = std::max(1, std::atoi(e));
+    Gen g(Q);
+    Q.jit_src = g.source();
     {
       const std::vector<double> t = g.tail();
-      P.jtab.insert(P.jtab.end(), t.begin(), t.end());
+      Q.jtab.insert(Q.jtab.end(), t.begin(), t.end());
     }
-    std::string key = P.jit_src;
-    for (const std::string& opt : jit_opts()) key += "\n//" + opt;
-    key += std::string("\n//") + kWalkCommonSrc + kWalkParamsSrc;
-    P.jit_key = fnv1a(key);
+    Q.jit_key = jit_source_key(Q.jit_src);
+    (void)n;
   };
-  int budget = kRegsMax;
-  finish(budget);
-  // The live-value budget against the compiler (walks of 10 ms or more: up to
-  // ~5 hiprtc compiles of ~0.5-1 s, cached).  The estimate is rough (at 170 the
-  // n = 40 bench kernel fits 256 VGPRs with 6 chunk-level spills, denser or
-  // larger matrices spill inside the walk loop), so the compiled code object's
-  // VGPR spill count decides: from the default, larger budgets (fewer ops)
-  // while their kernels spill at most kSpillOk VGPRs — the fewest ops wins;
-  // if the default spills more, smaller budgets until one does not.
-  // Measured (n = 40 bench matrix, profiles/r2/probe_regmax_sched.log): 170
-  // -> 11.93 ops, 188.5 ms; 190 -> 11.56, 181.8 ms; 200 -> 11.44 (17 spilled
-  // VGPRs, one scratch access in the loop), 179.0 ms; 210 -> 11.53, 183.2 ms.
-  const bool fixed = std::getenv("SUP_JIT_REGMAX") || std::getenv("SUP_JIT_STORAGE") || std::getenv("SUP_JIT_CC") ||
-                     std::getenv("SUP_JIT_NOVERIFY");
+  // SUP_JIT_BUDGET (experiments): this budget, no compiler check
+  const char* fixed_budget = std::getenv("SUP_JIT_BUDGET");
+  finish(P, fixed_budget ? std::max(1, std::atoi(fixed_budget)) : kRegsMax);
+  // The live-value budget against the compiler (walks of 10 ms or more).  The
+  // estimate is rough: on the n = 40 bench matrix budgets up to 192 compile
+  // without a spill, 194-216 spill 5-13 VGPRs, 218+ 17-27; denser or larger
+  // matrices spill inside the walk loop at the default.  So a ladder of
+  // budgets is planned (host threads), the distinct kernels are compiled in
+  // ascending op count, kMaxParallelCompiles at a time (hiprtc on host
+  // threads), and each code object is disassembled (codescan.cpp): the one
+  // with the fewest ops whose walk loop touches no scratch wins, a kernel with
+  // no scratch at all preferred unless the other saves more than
+  // kScratchTolerance of the ops (spills in the chunk start cost HBM writes
+  // and next to no time).  Where every kernel the compiler accepts scratches
+  // inside the walk loop, or hiprtc's register allocator gives up (some dense
+  // n >= 46 patterns), there is no segmented plan and the engine runs the
+  // ahead-of-time walk.
+  const bool fixed = fixed_budget || std::getenv("SUP_JIT_REGMAX") || std::getenv("SUP_JIT_STORAGE") ||
+                     std::getenv("SUP_JIT_CC") || std::getenv("SUP_JIT_NOVERIFY");
   const double walk_s = std::ldexp(1.0, n - 1) * P.seg_ops / 3.7e13;
   if (!fixed && walk_s >= 0.01 && P.seg_regs > kRegs3) {
-    constexpr int kSpillOk = 20;
-    auto spills = [&]() {
-      int vgpr = 0, sp = 0;
-      return jit_code_regs(P, &vgpr, &sp) == SUP_OK ? sp : 1 << 20;
-    };
-    const int s0 = spills();
-    // a kernel the register allocator gives up on (some dense n >= 46
-    // patterns): no segmented plan, callers fall back to the ahead-of-time
-    // walks.  No further compile is tried: hiprtc has crashed on the next
-    // program after such a failure.
-    if (s0 >= (1 << 20)) return SUP_EHIP;
-    int best_b = budget;
-    double best_ops = P.seg_ops;
-    if (s0 <= kSpillOk) {
-      // (bench matrix: 180/190/200/210 -> 11.73/11.63/11.45/11.37 ops with
-      // 5/0/7/9 spilled VGPRs; from 220 on 11.28-11.29 ops, 21-27 spills)
-      for (int b2 = budget + 10; b2 <= budget + 40; b2 += 10) {
-        finish(b2);
-        if (P.seg_ops < best_ops - 1e-9) {
-          const int sp = spills();
-          if (std::getenv("SUP_JIT_VERBOSE")) std::fprintf(stderr, "  budget %d: ops %.4f spills %d\n", b2, P.seg_ops, sp);
-          if (sp <= kSpillOk) best_ops = P.seg_ops, best_b = b2;
-        }
-      }
-    } else {
-      // the fewest spills if none gets under kSpillOk
-      int fewest = s0;
-      for (int b2 = budget - 20; b2 >= kRegs3 && fewest > kSpillOk; b2 -= 20) {
-        finish(b2);
-        const int sp = spills();
-        if (sp < fewest) fewest = sp, best_b = b2;
-      }
-      if (fewest >= (1 << 20)) return SUP_EHIP;
+    // the ladder of budgets, one candidate plan per budget (host threads)
+    std::vector<int> budgets;
+    for (int b2 = kRegs3 + 20; b2 <= kRegsMax + 60; b2 += 8) budgets.push_back(b2);
+    std::vector<Plan> cand(budgets.size(), P);
+    parallel_tasks(budgets.size(), [&](size_t i) { finish(cand[i], budgets[i]); });
+    // distinct kernels in budget order
+    std::vector<size_t> idx;
+    for (size_t i = 0; i < cand.size(); ++i) {
+      bool dup = false;
+      for (size_t j : idx) dup = dup || cand[j].jit_key == cand[i].jit_key;
+      if (!dup) idx.push_back(i);
     }
+    std::vector<CodeScan> scans(cand.size());
+    std::vector<int> src(cand.size(), SUP_EHIP);
+    std::vector<char> done(cand.size(), 0);
+    auto run_batch = [&](const std::vector<size_t>& which) {
+      const auto t0 = std::chrono::steady_clock::now();
+      const double own = t_compile_ms;  // the batch's wall time counts for this call
+      parallel_tasks(which.size(), [&](size_t k) { src[which[k]] = jit_code_scan(cand[which[k]], &scans[which[k]]); },
+                     g_jit_failed.load() ? 1 : (int)kMaxParallelCompiles);
+      t_compile_ms = own + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      for (size_t i : which) done[i] = 1;
+    };
+    auto clean = [&](size_t i) { return done[i] && src[i] == SUP_OK && scans[i].loop_scratch == 0; };
+    // Probe: the default budget's kernel alone.  hiprtc's register allocator
+    // gives up on some dense n >= 46 patterns ("maximum depth for
+    // recoloring"), and such a failure next to concurrent compiles has crashed
+    // the process (LLVM's error path is not thread-safe): a failing pattern
+    // stops here, before any concurrent compile.
+    size_t probe = idx[0];
+    for (size_t i : idx)
+      if (budgets[i] <= kRegsMax) probe = i;
+    run_batch({probe});
+    if (src[probe] != SUP_OK) return SUP_EHIP;
+    // Then batches of up to kMaxParallelCompiles budgets, concurrently: upwards
+    // from the probe while its walk loop is clean (fewer ops, until a kernel
+    // scratches in the loop), downwards while it is not (until one is clean).
+    auto pick = [&]() {
+      int c = -1, bare = -1;
+      for (size_t i : idx) {
+        if (!clean(i)) continue;
+        if (c < 0 || cand[i].seg_ops < cand[c].seg_ops) c = (int)i;
+        if (scans[i].scratch_bytes == 0 && (bare < 0 || cand[i].seg_ops < cand[bare].seg_ops)) bare = (int)i;
+      }
+      return (bare >= 0 && c >= 0 && cand[bare].seg_ops <= cand[c].seg_ops * (1.0 + kScratchTolerance)) ? bare : c;
+    };
+    const bool up = clean(probe);
+    for (;;) {
+      std::vector<size_t> batch;
+      if (up) {
+        for (size_t i : idx)
+          if (!done[i] && budgets[i] > budgets[probe] && batch.size() < kMaxParallelCompiles) batch.push_back(i);
+      } else {
+        for (auto it = idx.rbegin(); it != idx.rend(); ++it)
+          if (!done[*it] && budgets[*it] < budgets[probe] && batch.size() < kMaxParallelCompiles) batch.push_back(*it);
+      }
+      if (batch.empty()) break;
+      run_batch(batch);
+      bool stop = false;
+      for (size_t i : batch) stop = stop || (up ? !clean(i) : clean(i));
+      if (stop) break;
+    }
+    const int best = pick();
     if (std::getenv("SUP_JIT_VERBOSE"))
-      std::fprintf(stderr, "seg budget %d: default %d spilled %d VGPRs\n", best_b, budget, s0);
-    if (best_b != budget || P.seg_ops != best_ops) finish(best_b);
+      for (size_t i : idx)
+        if (done[i])
+          std::fprintf(stderr, "  budget %d: ops %.4f rc %d vgprs %d spills %d scratch %dB (loop %d of %d insts)%s\n",
+                       budgets[i], cand[i].seg_ops, src[i], scans[i].vgprs, scans[i].vgpr_spills,
+                       scans[i].scratch_bytes, scans[i].loop_scratch, scans[i].loop_insts,
+                       (int)i == best ? "  <- chosen" : "");
+    if (best < 0) {
+      set_error("segmented walk: every budget's kernel touches scratch inside its walk loop (or fails to compile)");
+      return SUP_EHIP;
+    }
+    P = std::move(cand[best]);
   }
   P.seg_skip = seg_skip_fraction_plan(P, 2048);
   if (std::getenv("SUP_JIT_VERBOSE"))
@@ -1634,8 +1726,6 @@ std::mutex g_jit_mu;
 std::map<uint64_t, std::shared_ptr<std::vector<char>>> g_code;        // key -> code object
 std::map<std::pair<int, uint64_t>, hipFunction_t> g_fn;               // (device, key) -> kernel
 std::map<std::pair<int, uint64_t>, int> g_occ;
-double g_compile_ms = 0.0;
-
 // SUP_JIT_LDS (experiments): dynamic LDS bytes per block, to cap residency
 // and measure the walk's sensitivity to occupancy.
 unsigned jit_lds_bytes() {
@@ -1685,20 +1775,28 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
   else std::remove(tmp.c_str());
 }
 
+// Code object of P's kernel: from memory, the disk cache, or hiprtc.  Safe to
+// call from several threads at once (the budget check compiles its candidates
+// concurrently); g_jit_mu guards the maps only, not the compile.
 int compile(const Plan& P, std::shared_ptr<std::vector<char>>& code) {
-  auto it = g_code.find(P.jit_key);
-  if (it != g_code.end()) {
-    code = it->second;
-    return SUP_OK;
+  {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    auto it = g_code.find(P.jit_key);
+    if (it != g_code.end()) {
+      code = it->second;
+      return SUP_OK;
+    }
   }
   const std::string dir = cache_dir();
   const std::string name = "seg_" + key_hex(P.jit_key) + ".co";
   auto co = std::make_shared<std::vector<char>>();
-  if (!dir.empty() && read_file(dir + "/" + name, *co)) {
-    g_code[P.jit_key] = co;
-    code = co;
+  auto publish = [&]() {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    auto ins = g_code.emplace(P.jit_key, co);  // a concurrent compile of the same key may have won
+    code = ins.first->second;
     return SUP_OK;
-  }
+  };
+  if (!dir.empty() && read_file(dir + "/" + name, *co)) return publish();
   if (const char* d = std::getenv("SUP_JIT_DUMP")) {  // debugging: keep the generated source
     FILE* f = std::fopen((std::string(d) + "/seg_" + key_hex(P.jit_key) + ".hip").c_str(), "w");
     if (f) std::fputs(P.jit_src.c_str(), f), std::fclose(f);
@@ -1733,6 +1831,7 @@ int compile(const Plan& P, std::shared_ptr<std::vector<char>>& code) {
       src = Gen(Q).source();
       continue;
     }
+    g_jit_failed.store(true);
     set_error(std::string("hiprtc compile of the segmented walk failed: ") + hiprtcGetErrorString(cr) + "\n" +
               log.substr(0, 2000));
     return SUP_EHIP;
@@ -1742,11 +1841,9 @@ int compile(const Plan& P, std::shared_ptr<std::vector<char>>& code) {
   co->resize(cs);
   hiprtcGetCode(prog, co->data());
   hiprtcDestroyProgram(&prog);
-  g_compile_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  t_compile_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (!dir.empty()) write_file_atomic(dir, name, *co);
-  g_code[P.jit_key] = co;
-  code = co;
-  return SUP_OK;
+  return publish();
 }
 
 int resolve(int dev, const Plan& P, hipFunction_t* fn) {
@@ -1754,16 +1851,24 @@ int resolve(int dev, const Plan& P, hipFunction_t* fn) {
     set_error("plan has no segmented-walk kernel");
     return SUP_EINVAL;
   }
-  std::lock_guard<std::mutex> g(g_jit_mu);
   auto k = std::make_pair(dev, P.jit_key);
+  {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    auto it = g_fn.find(k);
+    if (it != g_fn.end()) {
+      *fn = it->second;
+      return SUP_OK;
+    }
+  }
+  std::shared_ptr<std::vector<char>> code;
+  int rc = compile(P, code);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(g_jit_mu);
   auto it = g_fn.find(k);
   if (it != g_fn.end()) {
     *fn = it->second;
     return SUP_OK;
   }
-  std::shared_ptr<std::vector<char>> code;
-  int rc = compile(P, code);
-  if (rc) return rc;
   hipModule_t mod;
   hipError_t e = hipModuleLoadData(&mod, code->data());
   if (e != hipSuccess) {
@@ -1785,59 +1890,26 @@ int jit_compile_only(const Plan& P, double* compile_ms) {
     set_error("plan has no segmented-walk kernel");
     return SUP_EINVAL;
   }
-  const double before = jit_compile_ms_total();
+  const double before = jit_compile_ms_thread();
   std::shared_ptr<std::vector<char>> code;
-  int rc;
-  {
-    std::lock_guard<std::mutex> g(g_jit_mu);
-    rc = compile(P, code);
-  }
-  if (compile_ms) *compile_ms = jit_compile_ms_total() - before;
+  const int rc = compile(P, code);
+  if (compile_ms) *compile_ms = jit_compile_ms_thread() - before;
   return rc;
 }
 
-// Unsigned msgpack value after the map key `key` in the code object's
-// metadata note (fixstr key; fixint / uint8-32 value); -1 if absent.
-static long code_meta(const std::vector<char>& co, const std::string& key) {
-  if (key.size() >= 32) return -1;
-  std::string pat(1, (char)(0xa0 | key.size()));
-  pat += key;
-  const std::string_view sv(co.data(), co.size());
-  const size_t at = sv.find(pat);
-  if (at == std::string_view::npos || at + pat.size() >= co.size()) return -1;
-  const unsigned char* v = (const unsigned char*)co.data() + at + pat.size();
-  const size_t left = co.size() - at - pat.size();
-  if (v[0] < 0x80) return v[0];
-  if (v[0] == 0xcc && left >= 2) return v[1];
-  if (v[0] == 0xcd && left >= 3) return (v[1] << 8) | v[2];
-  if (v[0] == 0xce && left >= 5) return ((long)v[1] << 24) | (v[2] << 16) | (v[3] << 8) | v[4];
-  return -1;
-}
-
-int jit_code_regs(const Plan& P, int* vgprs, int* vgpr_spills) {
+int jit_code_scan(const Plan& P, CodeScan* out) {
   std::shared_ptr<std::vector<char>> code;
-  int rc;
-  {
-    std::lock_guard<std::mutex> g(g_jit_mu);
-    rc = compile(P, code);
-  }
+  const int rc = compile(P, code);
   if (rc) return rc;
-  const long v = code_meta(*code, ".vgpr_count"), sp = code_meta(*code, ".vgpr_spill_count");
-  if (v < 0 || sp < 0) {
-    set_error("segmented walk: no register counts in the code object's metadata");
-    return SUP_EHIP;
-  }
-  if (vgprs) *vgprs = (int)v;
-  if (vgpr_spills) *vgpr_spills = (int)sp;
-  return SUP_OK;
+  return scan_code_object(*code, "sup_walk_seg", out);
 }
 
 int jit_occupancy(int dev, const Plan& P, int* blocks_per_cu, double* compile_ms) {
-  const double before = jit_compile_ms_total();
+  const double before = jit_compile_ms_thread();
   hipFunction_t fn;
   int rc = resolve(dev, P, &fn);
   if (rc) return rc;
-  if (compile_ms) *compile_ms = jit_compile_ms_total() - before;
+  if (compile_ms) *compile_ms = jit_compile_ms_thread() - before;
   std::lock_guard<std::mutex> g(g_jit_mu);
   auto k = std::make_pair(dev, P.jit_key);
   auto it = g_occ.find(k);
@@ -1870,9 +1942,6 @@ int jit_launch(int dev, const Plan& P, const WalkParams& p, int grid, hipStream_
   return SUP_OK;
 }
 
-double jit_compile_ms_total() {
-  std::lock_guard<std::mutex> g(g_jit_mu);
-  return g_compile_ms;
-}
+double jit_compile_ms_thread() { return t_compile_ms; }
 
 }  // namespace sup
