@@ -105,6 +105,25 @@ def combine(part: float, rank: int, world: int, device) -> float:
     return pairwise(v.cpu().tolist())
 
 
+def check_plans_agree(key: int, rank: int, world: int, device) -> list:
+    """Every rank plans on its own (plan + compile before the warmup); the
+    shards add up to the permanent only if all ranks walk the same plan.
+    All-gather each rank's plan fingerprint (sup_plan_key: walk kind, layout,
+    column map, tables, kernel source) and abort on any mismatch."""
+    if world == 1:
+        return [key]
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([key - (1 << 64) if key >= (1 << 63) else key], dtype=torch.int64, device=device)
+    got = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(got, t)
+    keys = [int(x.item()) & ((1 << 64) - 1) for x in got]
+    if len(set(keys)) != 1:
+        raise RuntimeError(f"rank {rank}: ranks planned different walks, their shards would not sum to one "
+                           f"permanent: plan keys {[hex(k) for k in keys]}")
+    return keys
+
+
 def pmc_record(n: int, kernel: str):
     """The committed rocprofv3 PMC summary of this walk kernel at this n
     (tools/pmc_summary.py: HBM bytes per launch, achieved occupancy, LDS bank
@@ -219,6 +238,7 @@ def main():
         # plan + (segmented walk) hiprtc compile, once, before the timed region;
         # gpu_num = world so that --jit 0 decides as the N-rank plan would
         prep = S.prepare(a, kernel, jit=jit, gpu_num=world, device_id=dev)
+        check_plans_agree(S.plan_key(a, kernel, jit=jit, gpu_num=world, device_id=dev), rank, world, tdev)
 
         def step():
             part, st = S.perman_shard(a, rank, world, kernel=kernel, device_id=dev, return_stats=True,

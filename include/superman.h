@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SUP_ABI_VERSION 4
+#define SUP_ABI_VERSION 5
 
 /* ---- error codes ------------------------------------------------------ */
 #define SUP_OK            0
@@ -80,8 +80,12 @@ typedef enum {
 typedef enum {
   SUP_SCHED_SINGLE = 0,   /* one device           (-p4; gpu_exact_dense.cu:640-699)            */
   SUP_SCHED_STATIC = 1,   /* static split         (-p5; gpu_exact_dense.cu:701-774)            */
-  SUP_SCHED_CHUNKS = 2    /* dynamic chunk queue  (-p6/-p8; gpu_exact_dense.cu:776-904,
+  SUP_SCHED_CHUNKS = 2,   /* dynamic chunk queue  (-p6/-p8; gpu_exact_dense.cu:776-904,
                                                    gpu_exact_sparse.cu:1192-1324)            */
+  SUP_SCHED_MANUAL = 3    /* manual distribution  (-p66; gpu_exact_dense.cu:913-990,
+                             gpu_exact_sparse.cu:1328-1400): 3/8, 3/8, 1/8, 1/8 of the space
+                             on devices 0-3 (gpu_num 4, as main.cu:71 passes; with fewer
+                             devices the pieces wrap round modulo gpu_num)             */
 } sup_sched;
 
 typedef struct {
@@ -173,6 +177,15 @@ int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const 
                   int* colmap, int* lane_bits, int* walk_bits, int* cached_bits, int* pair_bits,
                   double* est_ops_per_step);
 
+/* 64-bit fingerprint of the plan sup_perman / sup_perman_shard would run
+ * with options `o` (walk kind, layout, engine column map, signed column
+ * table, start vector, the segmented walk's cached / pair bits, budget and
+ * kernel source).  One process per GPU: every rank plans on its own, and the
+ * shards add up to the permanent only if all ranks walk the same plan —
+ * all-gather the keys before summing (bench.py does, and aborts on a
+ * mismatch). */
+int sup_plan_key(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o, uint64_t* key);
+
 /* Build the plan sup_perman would run and, if it is the segmented walk,
  * compile its kernel now (hiprtc; no device needed) into the in-memory and
  * disk caches, so a later sup_perman does not pay the compile.  (A SkipPer
@@ -251,6 +264,13 @@ int sup_gpu_perman64_xshared_coalescing_mshared_multigpu_sparse(const void* mat,
 int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_sparse(const void* mat,
     const int* cptrs, const int* rows, const void* cvals, sup_dtype t, int nov, int gpu_num,
     int cpu, int threads, int grid_dim, int block_dim, double* out);
+/* gpu_exact_dense.cu:914 ..._multigpu_manual_distribution (-p66): 3/8, 3/8, 1/8, 1/8 on 4 devices */
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpu_manual_distribution(const void* mat, sup_dtype t,
+    int nov, int gpu_num, int grid_dim, int block_dim, double* out);
+/* gpu_exact_sparse.cu:1328 ..._multigpu_sparse_manual_distribution (-p66 -s) */
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpu_sparse_manual_distribution(const void* mat,
+    const int* cptrs, const int* rows, const void* cvals, sup_dtype t, int nov, int gpu_num, int grid_dim,
+    int block_dim, double* out);
 /* gpu_exact_sparse.cu:1124 ..._skipper (-p7 -s) */
 int sup_gpu_perman64_xshared_coalescing_mshared_skipper(const void* mat, const int* rptrs,
     const int* cols, const int* cptrs, const int* rows, const void* cvals, sup_dtype t, int nov,

@@ -15,11 +15,11 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import (KERNEL_DENSE, KERNEL_SKIPPER, KERNEL_SPARYSER, LEAF_FN, SCHED_CHUNKS, SCHED_SINGLE,
+from ._lib import (KERNEL_DENSE, KERNEL_SKIPPER, KERNEL_SPARYSER, LEAF_FN, SCHED_CHUNKS, SCHED_MANUAL, SCHED_SINGLE,
                    SCHED_STATIC, SupApproxResult, SupError, SupOpts, SupReduceOpts, SupStats)
 
 __all__ = [
-    "perman", "perman_cpu", "partial", "perman_shard", "plan_info", "prepare", "read_matrix", "read_mtx", "sort_order",
+    "perman", "perman_cpu", "partial", "perman_shard", "plan_info", "plan_key", "prepare", "read_matrix", "read_mtx", "sort_order",
     "skip_order", "compress", "decompose", "perman_reduced", "approx", "grid_graph", "ALGOS_APPROX",
     "nw_start", "device_count", "layout", "SupError", "ALGOS_DENSE", "ALGOS_SPARSE",
     "gpu_perman64_xshared_coalescing_mshared",
@@ -46,7 +46,7 @@ ALGOS_DENSE = {
     4: ("gpu_perman64_xshared_coalescing_mshared", KERNEL_DENSE, SCHED_SINGLE),
     5: ("gpu_perman64_xshared_coalescing_mshared_multigpu", KERNEL_DENSE, SCHED_STATIC),
     6: ("gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks", KERNEL_DENSE, SCHED_CHUNKS),
-    66: ("gpu_perman64_xshared_coalescing_mshared_multigpu_manual_distribution", KERNEL_DENSE, SCHED_STATIC),
+    66: ("gpu_perman64_xshared_coalescing_mshared_multigpu_manual_distribution", KERNEL_DENSE, SCHED_MANUAL),
 }
 ALGOS_SPARSE = {
     1: ("gpu_perman64_xlocal_sparse", KERNEL_SPARYSER, SCHED_SINGLE),
@@ -58,7 +58,7 @@ ALGOS_SPARSE = {
     7: ("gpu_perman64_xshared_coalescing_mshared_skipper", KERNEL_SKIPPER, SCHED_SINGLE),
     8: ("gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper", KERNEL_SKIPPER, SCHED_CHUNKS),
     66: ("gpu_perman64_xshared_coalescing_mshared_multigpu_sparse_manual_distribution", KERNEL_SPARYSER,
-         SCHED_STATIC),
+         SCHED_MANUAL),
 }
 _KERNELS = {"dense": KERNEL_DENSE, "sparse": KERNEL_SPARYSER, "spa": KERNEL_SPARYSER,
             "skipper": KERNEL_SKIPPER, "skip": KERNEL_SKIPPER, "dense_plain": _lib.KERNEL_DENSE_PLAIN,
@@ -128,8 +128,8 @@ def perman(mat, algo: int = 4, sparse: bool = False, gpu_num: int = 1, cpu: bool
     _, kern, sched = table[algo]
     if kernel is not None:
         kern = _KERNELS[kernel]
-    if algo == 66:
-        gpu_num = 4
+    if algo == 66 and gpu_num == 1:
+        gpu_num = 4  # main.cu:71,150 pass 4 devices; the pieces wrap round a smaller gpu_num
     if sched == SCHED_SINGLE:
         gpu_num = 1
     a, dt, n = _mat(mat)
@@ -225,6 +225,19 @@ def plan_info(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device
                                  C.byref(L), C.byref(m), C.byref(cc), C.byref(pb), C.byref(ops)), "plan_info")
     return {"kind": WALK_NAMES[kind.value], "colmap": cm[: n - 1].copy(), "L": L.value, "m": m.value,
             "cached": cc.value, "pair_bits": pb.value, "est_ops_per_step": ops.value}
+
+
+def plan_key(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_id: int = 0,
+             walk_log2: int = 0) -> int:
+    """64-bit fingerprint of the plan perman / perman_shard would run
+    (sup_plan_key): ranks that plan on their own must agree on it before their
+    shards are summed."""
+    a, dt, n = _mat(mat)
+    lib = _lib.load()
+    key = C.c_uint64(0)
+    o = _opts(gpu_num=gpu_num, device_id=device_id, jit=jit, walk_log2=walk_log2)
+    _lib.check(lib.sup_plan_key(a.ctypes.data, dt, n, _KERNELS[kernel], C.byref(o), C.byref(key)), "plan_key")
+    return key.value
 
 
 def prepare(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_id: int = 0,

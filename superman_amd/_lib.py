@@ -28,17 +28,19 @@ ERRORS = {
 }
 SUP_INT32, SUP_FLOAT32, SUP_FLOAT64 = 0, 1, 2
 KERNEL_DENSE, KERNEL_SPARYSER, KERNEL_SKIPPER, KERNEL_DENSE_PLAIN, KERNEL_SEGMENTED, KERNEL_DENSE_LDS = 0, 1, 2, 3, 4, 5
-SCHED_SINGLE, SCHED_STATIC, SCHED_CHUNKS = 0, 1, 2
+SCHED_SINGLE, SCHED_STATIC, SCHED_CHUNKS, SCHED_MANUAL = 0, 1, 2, 3
 
 # Every symbol include/superman.h declares (checked by tests/test_capi.py).
 EXPORTS = [
     "sup_opts_init", "sup_abi_version", "sup_last_error", "sup_device_count",
     "sup_perman", "sup_partial", "sup_perman_cpu", "sup_nw_start", "sup_perman_shard", "sup_plan_info",
-    "sup_prepare", "sup_perman_exact", "sup_perman_reduced_exact", "sup_perman_quad",
+    "sup_prepare", "sup_plan_key", "sup_perman_exact", "sup_perman_reduced_exact", "sup_perman_quad",
     "sup_perman_reduced_quad",
     "sup_gpu_perman64_xshared_coalescing_mshared",
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpu",
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks",
+    "sup_gpu_perman64_xshared_coalescing_mshared_multigpu_manual_distribution",
+    "sup_gpu_perman64_xshared_coalescing_mshared_multigpu_sparse_manual_distribution",
     "sup_gpu_perman64_xshared_coalescing_mshared_sparse",
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpu_sparse",
     "sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_sparse",
@@ -127,7 +129,7 @@ def load() -> C.CDLL:
             build()
         lib = C.CDLL(LIB_PATH)
         _declare(lib)
-        if lib.sup_abi_version() != 4:
+        if lib.sup_abi_version() != 5:
             raise RuntimeError("libsuperman_hip.so ABI version mismatch")
         _lib = lib
         return lib
@@ -150,6 +152,7 @@ def _declare(lib: C.CDLL) -> None:
     lib.sup_plan_info.argtypes = [P, I, I, I, C.POINTER(SupOpts), C.POINTER(I), P, C.POINTER(I), C.POINTER(I),
                                   C.POINTER(I), C.POINTER(I), C.POINTER(D)]
     lib.sup_prepare.argtypes = [P, I, I, I, C.POINTER(SupOpts), C.POINTER(I), C.POINTER(C.c_double)]
+    lib.sup_plan_key.argtypes = [P, I, I, I, C.POINTER(SupOpts), C.POINTER(C.c_uint64)]
     lib.sup_nw_start.argtypes = [P, I, I, C.POINTER(D), C.POINTER(D)]
     lib.sup_read_matrix.argtypes = [C.c_char_p, I, C.POINTER(P), C.POINTER(I), C.POINTER(I), C.POINTER(I)]
     lib.sup_free.argtypes = [P]

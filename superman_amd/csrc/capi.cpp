@@ -350,6 +350,40 @@ int sup_plan_info(const void* mat, sup_dtype t, int n, sup_kernel kernel, const 
   return SUP_OK;
 }
 
+int sup_plan_key(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o_in, uint64_t* key) {
+  if (!key) {
+    set_error("sup_plan_key: key pointer missing");
+    return SUP_EINVAL;
+  }
+  std::vector<double> A;
+  int rc = to_double(mat, t, n, A);
+  if (rc) return rc;
+  sup_opts o;
+  if (o_in) o = *o_in;
+  else sup_opts_init(&o);
+  Plan P;
+  if ((rc = check_walk_opts(o))) return rc;
+  if ((rc = plan_for(A.data(), n, kernel, layout_for(n, o), P, o.jit, o.gpu_num, o.device_id))) return rc;
+  // everything that decides which wave-chunk sums which subsets, in what
+  // order and with which operations: walk kind, layout, column map, the
+  // signed column table, the segmented walk's choices and its kernel source
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&h](const void* p, size_t bytes) {
+    const unsigned char* c = (const unsigned char*)p;
+    for (size_t i = 0; i < bytes; ++i) h = (h ^ c[i]) * 1099511628211ull;
+  };
+  const int32_t head[] = {P.n, (int32_t)P.kind, (int32_t)P.lds, P.lay.L, P.lay.m, P.lay.h, P.seg_cc, P.seg_b,
+                          P.seg_budget, P.seg_kp};
+  mix(head, sizeof head);
+  mix(P.colmap.data(), P.colmap.size() * sizeof(int));
+  mix(P.cols.data(), P.cols.size() * sizeof(double));
+  mix(P.x0.data(), P.x0.size() * sizeof(double));
+  mix(&P.jit_key, sizeof P.jit_key);
+  mix(P.jtab.data(), P.jtab.size() * sizeof(double));
+  *key = h;
+  return SUP_OK;
+}
+
 int sup_prepare(const void* mat, sup_dtype t, int n, sup_kernel kernel, const sup_opts* o_in, int* walk_kind,
                 double* compile_ms) {
   std::vector<double> A;
@@ -371,6 +405,67 @@ int sup_prepare(const void* mat, sup_dtype t, int n, sup_kernel kernel, const su
 }
 
 // ---- reference-signature wrappers ------------------------------------------
+// The reference's sparse wrappers take the caller's CSC (cptrs, rows, cvals)
+// and, for SkipPer, CSR (rptrs, cols) next to the dense matrix (built by
+// matrix2compressed*, util.h:522-551).  The engine derives its own structure
+// from `mat` (touched rows per column, SkipOrder masks), so these arrays must
+// describe exactly mat's nonzeros: each column's rows ascending with their
+// values, each row's columns ascending.  They are checked, never silently
+// ignored: an array built with the reference's `> 0` test (util.h:537,542),
+// which drops negative entries, is refused with SUP_EINVAL.
+static double entry(const void* mat, sup_dtype t, size_t i) {
+  return t == SUP_INT32 ? (double)((const int32_t*)mat)[i]
+         : t == SUP_FLOAT32 ? (double)((const float*)mat)[i] : ((const double*)mat)[i];
+}
+
+static int check_compressed(const void* mat, sup_dtype t, int n, const int* cptrs, const int* rows,
+                            const void* cvals, const int* rptrs, const int* cols) {
+  if (!mat || n < 1 || n > SUP_MAX_N) {
+    set_error("reference wrapper: null matrix or n outside [1, 64]");
+    return SUP_EINVAL;
+  }
+  if (!cptrs || !rows || !cvals) {
+    set_error("reference wrapper: CSC arrays (cptrs, rows, cvals) missing");
+    return SUP_EINVAL;
+  }
+  auto bad = [](const std::string& m) {
+    set_error("reference wrapper: " + m + " (build CSR/CSC with sup_compress: nonzero test != 0)");
+    return SUP_EINVAL;
+  };
+  if (cptrs[0] != 0) return bad("cptrs[0] != 0");
+  for (int c = 0; c < n; ++c) {
+    if (cptrs[c + 1] < cptrs[c]) return bad("cptrs not ascending");
+    int want = 0;
+    for (int r = 0; r < n; ++r) want += entry(mat, t, (size_t)r * n + c) != 0.0;
+    if (cptrs[c + 1] - cptrs[c] != want)
+      return bad("column " + std::to_string(c) + " lists " + std::to_string(cptrs[c + 1] - cptrs[c]) +
+                 " entries, the matrix has " + std::to_string(want) + " nonzeros");
+    for (int k = cptrs[c]; k < cptrs[c + 1]; ++k) {
+      const int r = rows[k];
+      if (r < 0 || r >= n || (k > cptrs[c] && r <= rows[k - 1])) return bad("CSC rows out of range or order");
+      const double v = entry(mat, t, (size_t)r * n + c);
+      if (v == 0.0 || entry(cvals, t, (size_t)k) != v)
+        return bad("CSC value at (" + std::to_string(r) + ", " + std::to_string(c) + ") differs from the matrix");
+    }
+  }
+  if (rptrs || cols) {
+    if (!rptrs || !cols) return bad("CSR arrays incomplete");
+    if (rptrs[0] != 0) return bad("rptrs[0] != 0");
+    for (int r = 0; r < n; ++r) {
+      if (rptrs[r + 1] < rptrs[r]) return bad("rptrs not ascending");
+      int want = 0;
+      for (int c = 0; c < n; ++c) want += entry(mat, t, (size_t)r * n + c) != 0.0;
+      if (rptrs[r + 1] - rptrs[r] != want) return bad("row " + std::to_string(r) + " nonzero count differs");
+      for (int k = rptrs[r]; k < rptrs[r + 1]; ++k) {
+        const int c = cols[k];
+        if (c < 0 || c >= n || (k > rptrs[r] && c <= cols[k - 1]) || entry(mat, t, (size_t)r * n + c) == 0.0)
+          return bad("CSR columns out of range, order or pattern");
+      }
+    }
+  }
+  return SUP_OK;
+}
+
 static int run_ref(const void* mat, sup_dtype t, int nov, sup_kernel k, sup_sched s, int gpu_num, int cpu,
                    int threads, double* out) {
   sup_opts o;
@@ -393,32 +488,49 @@ int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks(const void* m
                                                                    double* out) {
   return run_ref(mat, t, nov, SUP_KERNEL_DENSE, SUP_SCHED_CHUNKS, gpu_num, cpu, threads, out);
 }
-int sup_gpu_perman64_xshared_coalescing_mshared_sparse(const void* mat, const int*, const int*, const void*,
-                                                       sup_dtype t, int nov, int, int, double* out) {
-  return run_ref(mat, t, nov, SUP_KERNEL_SPARYSER, SUP_SCHED_SINGLE, 1, 0, 16, out);
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpu_manual_distribution(const void* mat, sup_dtype t, int nov,
+                                                                             int gpu_num, int, int, double* out) {
+  return run_ref(mat, t, nov, SUP_KERNEL_DENSE, SUP_SCHED_MANUAL, gpu_num, 0, 16, out);
 }
-int sup_gpu_perman64_xshared_coalescing_mshared_multigpu_sparse(const void* mat, const int*, const int*,
-                                                                const void*, sup_dtype t, int nov, int gpu_num,
+int sup_gpu_perman64_xshared_coalescing_mshared_sparse(const void* mat, const int* cptrs, const int* rows,
+                                                       const void* cvals, sup_dtype t, int nov, int, int,
+                                                       double* out) {
+  int rc = check_compressed(mat, t, nov, cptrs, rows, cvals, nullptr, nullptr);
+  return rc ? rc : run_ref(mat, t, nov, SUP_KERNEL_SPARYSER, SUP_SCHED_SINGLE, 1, 0, 16, out);
+}
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpu_sparse(const void* mat, const int* cptrs, const int* rows,
+                                                                const void* cvals, sup_dtype t, int nov, int gpu_num,
                                                                 int, int, double* out) {
-  return run_ref(mat, t, nov, SUP_KERNEL_SPARYSER, SUP_SCHED_STATIC, gpu_num, 0, 16, out);
+  int rc = check_compressed(mat, t, nov, cptrs, rows, cvals, nullptr, nullptr);
+  return rc ? rc : run_ref(mat, t, nov, SUP_KERNEL_SPARYSER, SUP_SCHED_STATIC, gpu_num, 0, 16, out);
 }
-int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_sparse(const void* mat, const int*, const int*,
-                                                                          const void*, sup_dtype t, int nov,
-                                                                          int gpu_num, int cpu, int threads, int,
-                                                                          int, double* out) {
-  return run_ref(mat, t, nov, SUP_KERNEL_SPARYSER, SUP_SCHED_CHUNKS, gpu_num, cpu, threads, out);
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_sparse(const void* mat, const int* cptrs,
+                                                                          const int* rows, const void* cvals,
+                                                                          sup_dtype t, int nov, int gpu_num, int cpu,
+                                                                          int threads, int, int, double* out) {
+  int rc = check_compressed(mat, t, nov, cptrs, rows, cvals, nullptr, nullptr);
+  return rc ? rc : run_ref(mat, t, nov, SUP_KERNEL_SPARYSER, SUP_SCHED_CHUNKS, gpu_num, cpu, threads, out);
 }
-int sup_gpu_perman64_xshared_coalescing_mshared_skipper(const void* mat, const int*, const int*, const int*,
-                                                        const int*, const void*, sup_dtype t, int nov, int, int,
-                                                        double* out) {
-  return run_ref(mat, t, nov, SUP_KERNEL_SKIPPER, SUP_SCHED_SINGLE, 1, 0, 16, out);
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpu_sparse_manual_distribution(const void* mat, const int* cptrs,
+                                                                                    const int* rows, const void* cvals,
+                                                                                    sup_dtype t, int nov, int gpu_num,
+                                                                                    int, int, double* out) {
+  int rc = check_compressed(mat, t, nov, cptrs, rows, cvals, nullptr, nullptr);
+  return rc ? rc : run_ref(mat, t, nov, SUP_KERNEL_SPARYSER, SUP_SCHED_MANUAL, gpu_num, 0, 16, out);
 }
-int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper(const void* mat, const int*, const int*,
-                                                                           const int*, const int*, const void*,
-                                                                           sup_dtype t, int nov, int gpu_num,
-                                                                           int cpu, int threads, int, int,
-                                                                           double* out) {
-  return run_ref(mat, t, nov, SUP_KERNEL_SKIPPER, SUP_SCHED_CHUNKS, gpu_num, cpu, threads, out);
+int sup_gpu_perman64_xshared_coalescing_mshared_skipper(const void* mat, const int* rptrs, const int* cols,
+                                                        const int* cptrs, const int* rows, const void* cvals,
+                                                        sup_dtype t, int nov, int, int, double* out) {
+  int rc = check_compressed(mat, t, nov, cptrs, rows, cvals, rptrs, cols);
+  return rc ? rc : run_ref(mat, t, nov, SUP_KERNEL_SKIPPER, SUP_SCHED_SINGLE, 1, 0, 16, out);
+}
+int sup_gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks_skipper(const void* mat, const int* rptrs,
+                                                                           const int* cols, const int* cptrs,
+                                                                           const int* rows, const void* cvals,
+                                                                           sup_dtype t, int nov, int gpu_num, int cpu,
+                                                                           int threads, int, int, double* out) {
+  int rc = check_compressed(mat, t, nov, cptrs, rows, cvals, rptrs, cols);
+  return rc ? rc : run_ref(mat, t, nov, SUP_KERNEL_SKIPPER, SUP_SCHED_CHUNKS, gpu_num, cpu, threads, out);
 }
 
 

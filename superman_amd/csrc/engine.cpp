@@ -593,7 +593,7 @@ static int ensure(T*& p, size_t& cap, size_t need) {
   return SUP_OK;
 }
 
-int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visited, RangeResult& r) {
+int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visited, RangeResult& r, double* slot) {
   r = RangeResult();
   if (c1 <= c0) return SUP_OK;  // empty range: partial 0
   if (c1 > P.lay.chunks()) {
@@ -695,6 +695,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   }
   SUP_HIP(hipEventRecord(c->ev1, s));
   SUP_HIP(launch_pairwise_reduce(c->d_chunk, count, c->d_scratch, c->d_result, s));
+  if (slot) SUP_HIP(hipMemcpyAsync(slot, c->d_result, sizeof(double), hipMemcpyDeviceToDevice, s));
   double result = 0.0;
   SUP_HIP(hipMemcpyAsync(&result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
   std::vector<unsigned> vis;
@@ -838,60 +839,75 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
 
 // ------------------------------------------------------------------ RCCL --
 // Combine per-device partials over RCCL without giving up the fixed reduction
-// order: device g contributes a vector that is zero outside the slots it owns
-// (its own partial, or the chunk items it dequeued).  Every slot then has one
-// nonzero addend, so the all-reduce SUM is exact whatever ring order RCCL
-// uses, and the caller folds the merged vector with the same pairwise tree
-// as the host path: -R results are bit-identical to the host combine.
-int rccl_allreduce_partials(const std::vector<int>& devs, const std::vector<std::vector<double>>& contrib,
-                            std::vector<double>& merged) {
-  const int G = (int)devs.size();
-  const size_t len = merged.size();
-  std::vector<ncclComm_t> comms(G);
-  ncclResult_t nr = ncclCommInitAll(comms.data(), G, devs.data());
-  if (nr != ncclSuccess) {
-    set_error(std::string("ncclCommInitAll: ") + ncclGetErrorString(nr));
+// order: every device owns a `len`-slot buffer, zero outside the slots it
+// filled (its own partial, or the chunk items it dequeued) — each walk writes
+// its partial into its slot on the device, after the pairwise reduce.  Every
+// slot then has one nonzero addend, so the all-reduce SUM is exact whatever
+// ring order RCCL uses; one D2H of the merged buffer follows, and the caller
+// folds it with the same pairwise tree as the host path: -R results are
+// bit-identical to the host combine.  Communicators are created once per
+// device set and kept for the process (ncclCommInitAll is the slow part).
+struct RcclSlots {
+  std::vector<int> devs;
+  std::vector<double*> buf;
+  std::vector<hipStream_t> st;
+  size_t len = 0;
+  ~RcclSlots() {
+    for (size_t g = 0; g < devs.size(); ++g) {
+      (void)hipSetDevice(devs[g]);
+      if (buf[g]) (void)hipFree(buf[g]);
+      if (st[g]) (void)hipStreamDestroy(st[g]);
+    }
+  }
+};
+
+static int rccl_slots_init(const std::vector<int>& devs, size_t len, RcclSlots& r) {
+  r.devs = devs;
+  r.len = len;
+  r.buf.assign(devs.size(), nullptr);
+  r.st.assign(devs.size(), nullptr);
+  for (size_t g = 0; g < devs.size(); ++g) {
+    SUP_HIP(hipSetDevice(devs[g]));
+    SUP_HIP(hipMalloc(&r.buf[g], std::max<size_t>(len, 1) * sizeof(double)));
+    SUP_HIP(hipStreamCreateWithFlags(&r.st[g], hipStreamNonBlocking));
+    SUP_HIP(hipMemsetAsync(r.buf[g], 0, std::max<size_t>(len, 1) * sizeof(double), r.st[g]));
+    SUP_HIP(hipStreamSynchronize(r.st[g]));
+  }
+  return SUP_OK;
+}
+
+static std::mutex g_comm_mu;
+static std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;
+
+static int rccl_allreduce_slots(RcclSlots& r, std::vector<double>& merged) {
+  const int G = (int)r.devs.size();
+  std::lock_guard<std::mutex> lk(g_comm_mu);  // one collective per communicator at a time
+  auto it = g_comms.find(r.devs);
+  if (it == g_comms.end()) {
+    std::vector<ncclComm_t> comms(G);
+    const ncclResult_t nr = ncclCommInitAll(comms.data(), G, r.devs.data());
+    if (nr != ncclSuccess) {
+      set_error(std::string("ncclCommInitAll: ") + ncclGetErrorString(nr));
+      return SUP_ERCCL;
+    }
+    it = g_comms.emplace(r.devs, std::move(comms)).first;
+  }
+  ncclResult_t nr = ncclGroupStart();
+  for (int g = 0; g < G && nr == ncclSuccess; ++g)
+    nr = ncclAllReduce(r.buf[g], r.buf[g], r.len, ncclFloat64, ncclSum, it->second[g], r.st[g]);
+  const ncclResult_t ge = ncclGroupEnd();
+  if (nr != ncclSuccess || ge != ncclSuccess) {
+    set_error(std::string("ncclAllReduce: ") + ncclGetErrorString(nr != ncclSuccess ? nr : ge));
     return SUP_ERCCL;
   }
-  std::vector<double*> buf(G, nullptr);
-  std::vector<hipStream_t> st(G, nullptr);
-  int rc = SUP_OK;
-  for (int g = 0; g < G && rc == SUP_OK; ++g) {
-    if (contrib[g].size() != len || hipSetDevice(devs[g]) != hipSuccess ||
-        hipMalloc(&buf[g], len * sizeof(double)) != hipSuccess || hipStreamCreate(&st[g]) != hipSuccess ||
-        hipMemcpy(buf[g], contrib[g].data(), len * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
-      set_error("RCCL staging buffer setup failed");
-      rc = SUP_EHIP;
-    }
-  }
-  if (rc == SUP_OK) {
-    ncclGroupStart();
-    for (int g = 0; g < G; ++g) {
-      nr = ncclAllReduce(buf[g], buf[g], len, ncclFloat64, ncclSum, comms[g], st[g]);
-      if (nr != ncclSuccess) break;
-    }
-    ncclResult_t ge = ncclGroupEnd();
-    if (nr != ncclSuccess || ge != ncclSuccess) {
-      set_error(std::string("ncclAllReduce: ") + ncclGetErrorString(nr != ncclSuccess ? nr : ge));
-      rc = SUP_ERCCL;
-    }
-  }
-  if (rc == SUP_OK) {
-    for (int g = 0; g < G; ++g) {
-      if (hipSetDevice(devs[g]) != hipSuccess || hipStreamSynchronize(st[g]) != hipSuccess) rc = SUP_EHIP;
-    }
-    (void)hipSetDevice(devs[0]);
-    if (hipMemcpy(merged.data(), buf[0], len * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
-      rc = SUP_EHIP;
-    if (rc) set_error("RCCL all-reduce completion failed");
-  }
+  merged.assign(r.len, 0.0);
   for (int g = 0; g < G; ++g) {
-    (void)hipSetDevice(devs[g]);
-    if (buf[g]) (void)hipFree(buf[g]);
-    if (st[g]) (void)hipStreamDestroy(st[g]);
-    ncclCommDestroy(comms[g]);
+    SUP_HIP(hipSetDevice(r.devs[g]));
+    SUP_HIP(hipStreamSynchronize(r.st[g]));
   }
-  return rc;
+  SUP_HIP(hipSetDevice(r.devs[0]));
+  SUP_HIP(hipMemcpy(merged.data(), r.buf[0], r.len * sizeof(double), hipMemcpyDeviceToHost));
+  return SUP_OK;
 }
 
 // ------------------------------------------------------------ schedulers --
@@ -925,16 +941,33 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   const uint64_t total = c1 - c0;
   const bool want_visited = true;
 
+  const bool rccl = (G > 1 && o.use_rccl) || o.use_rccl == 2;  // 2: also on one device (exercises RCCL)
   if (sched != SUP_SCHED_CHUNKS) {
-    // single device, or a static contiguous split (-p5)
-    std::vector<RangeResult> rr(G);
+    // Single device, a static contiguous split (-p5: G equal pieces, piece g
+    // on device g), or the reference's manual distribution (-p66,
+    // gpu_exact_dense.cu:913-990 / gpu_exact_sparse.cu:1328-1400: 3/8, 3/8,
+    // 1/8, 1/8 of the space on 4 devices, for unequal GPUs) as eight equal
+    // pieces owned {0,0,0,1,1,1,2,3} (mod G).  Piece partials are folded by
+    // the pairwise tree in piece order; equal power-of-two pieces are subtrees
+    // of the one-device tree, so -p5 on 2/4/8 devices and -p66 on any give the
+    // one-device result bit for bit.
+    const bool manual = sched == SUP_SCHED_MANUAL;
+    const int npieces = manual ? 8 : G;
+    std::vector<int> owner(npieces);
+    for (int q = 0; q < npieces; ++q) owner[q] = manual ? (q < 3 ? 0 : q < 6 ? 1 : q == 6 ? 2 : 3) % G : q;
+    RcclSlots slots;
+    if (rccl && (rc = rccl_slots_init(devs, npieces, slots))) return rc;
+    std::vector<RangeResult> rr(npieces);
     std::vector<int> rcs(G, SUP_OK);
     std::vector<std::string> errs(G);  // g_err is thread_local: carry worker messages back
     auto work = [&](int g) {
-      const uint64_t a = c0 + total * (uint64_t)g / (uint64_t)G;
-      const uint64_t b = c0 + total * (uint64_t)(g + 1) / (uint64_t)G;
       auto t0 = std::chrono::steady_clock::now();
-      rcs[g] = run_range(devs[g], P, a, b, want_visited, rr[g]);
+      for (int q = 0; q < npieces && !rcs[g]; ++q) {
+        if (owner[q] != g) continue;
+        const uint64_t a = c0 + total * (uint64_t)q / (uint64_t)npieces;
+        const uint64_t b = c0 + total * (uint64_t)(q + 1) / (uint64_t)npieces;
+        rcs[g] = run_range(devs[g], P, a, b, want_visited, rr[q], rccl ? slots.buf[g] + q : nullptr);
+      }
       if (rcs[g]) errs[g] = last_error();
       if (o.verbose) {
         double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -953,24 +986,28 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
         set_error(errs[g]);
         return rcs[g];
       }
-    out.dev_partials.resize(G);
+    out.dev_partials.assign(G, 0.0);
+    std::vector<double> piece(npieces), dev_ms(G, 0.0), dev_jit(G, 0.0);
+    for (int q = 0; q < npieces; ++q) {
+      const int g = owner[q];
+      piece[q] = rr[q].partial;
+      out.dev_partials[g] += rr[q].partial;
+      dev_ms[g] += rr[q].kernel_ms;
+      dev_jit[g] += rr[q].compile_ms;
+      out.visited += rr[q].visited;
+      out.grid = std::max(out.grid, rr[q].grid);
+    }
     for (int g = 0; g < G; ++g) {
-      worker_jit_ms = std::max(worker_jit_ms, rr[g].compile_ms);
-      out.dev_partials[g] = rr[g].partial;
-      out.kernel_ms = std::max(out.kernel_ms, rr[g].kernel_ms);
-      out.visited += rr[g].visited;
-      out.grid = std::max(out.grid, rr[g].grid);
+      out.kernel_ms = std::max(out.kernel_ms, dev_ms[g]);
+      worker_jit_ms = std::max(worker_jit_ms, dev_jit[g]);
     }
     out.devices = G;
-    if ((G > 1 && o.use_rccl) || o.use_rccl == 2) {  // 2: also on one device (exercises RCCL)
-      std::vector<std::vector<double>> contrib(G, std::vector<double>(G, 0.0));
-      for (int g = 0; g < G; ++g) contrib[g][g] = out.dev_partials[g];
-      std::vector<double> merged(G, 0.0);
-      rc = rccl_allreduce_partials(devs, contrib, merged);
-      if (rc) return rc;
+    if (rccl) {
+      std::vector<double> merged;
+      if ((rc = rccl_allreduce_slots(slots, merged))) return rc;
       out.total = pairwise_host(merged);
     } else {
-      out.total = pairwise_host(out.dev_partials);
+      out.total = pairwise_host(piece);
     }
     return SUP_OK;
   }
@@ -987,8 +1024,12 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     while (item * 2 <= total && total / (item * 2) >= target_items) item <<= 1;
   }
   const uint64_t nitems = (total + item - 1) / item;
+  // -R: device g writes the partial of every item it takes into slot `item`
+  // of its own buffer (the CPU worker's items have no device: host combine)
+  const bool rccl_items = rccl && !o.cpu_worker;
+  RcclSlots slots;
+  if (rccl_items && (rc = rccl_slots_init(devs, nitems, slots))) return rc;
   std::vector<double> ipart(nitems, 0.0);
-  std::vector<int> owner(nitems, 0);
   std::vector<double> dev_ms(G + 1, 0.0), dev_jit(G, 0.0);
   std::vector<uint64_t> dev_vis(G + 1, 0);
   std::vector<int> dev_grid(G + 1, 0);
@@ -1007,7 +1048,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
       const uint64_t b = std::min(c1, a + item);
       RangeResult r;
       auto t0 = std::chrono::steady_clock::now();
-      int e = run_range(devs[g], P, a, b, want_visited, r);
+      int e = run_range(devs[g], P, a, b, want_visited, r, rccl_items ? slots.buf[g] + it : nullptr);
       if (e) {
         rcs[g] = e;
         errs[g] = last_error();
@@ -1019,7 +1060,6 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
         std::printf("ChunkID %llu is DONE by kernel%d in %f\n", (unsigned long long)it, devs[g], s);
       }
       ipart[it] = r.partial;
-      owner[it] = g;
       dev_sum[g] += r.partial;
       dev_ms[g] += r.kernel_ms;
       dev_jit[g] += r.compile_ms;
@@ -1062,13 +1102,9 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     out.grid = std::max(out.grid, dev_grid[g]);
   }
   out.dev_partials = dev_sum;
-  if (((G > 1 && o.use_rccl) || o.use_rccl == 2) && !o.cpu_worker) {
-    // device g owns the items it dequeued; the others contribute 0 there
-    std::vector<std::vector<double>> contrib(G, std::vector<double>(nitems, 0.0));
-    for (uint64_t it = 0; it < nitems; ++it) contrib[owner[it]][it] = ipart[it];
-    std::vector<double> merged(nitems, 0.0);
-    rc = rccl_allreduce_partials(devs, contrib, merged);
-    if (rc) return rc;
+  if (rccl_items) {
+    std::vector<double> merged;
+    if ((rc = rccl_allreduce_slots(slots, merged))) return rc;
     out.total = pairwise_host(merged);
   } else {
     out.total = pairwise_host(ipart);

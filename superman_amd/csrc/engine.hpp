@@ -191,7 +191,10 @@ struct RangeResult {
 };
 
 // Walk wave-chunks [c0, c1) of plan P on device `dev` (synchronous).
-int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visited, RangeResult& r);
+// slot (optional): a device pointer on `dev`; the range's partial is also
+// copied there on the device (the -R combine all-reduces those slots).
+int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visited, RangeResult& r,
+              double* slot = nullptr);
 
 // Combine partials with the same pairwise tree the device reduction uses.
 double pairwise_host(const std::vector<double>& v);

@@ -292,7 +292,7 @@ int main(int argc, char** argv) {
         sched = SUP_SCHED_CHUNKS;
       } else if (a == 66) {
         name = "gpu_perman64_xshared_coalescing_mshared_multigpu_manual_distribution";
-        sched = SUP_SCHED_STATIC;
+        sched = SUP_SCHED_MANUAL;
         o.gpu_num = 4;  // main.cu:75 hard-codes 4 devices
       } else {
         std::cout << "Unknown Algorithm ID" << std::endl;
@@ -321,7 +321,7 @@ int main(int argc, char** argv) {
         sched = SUP_SCHED_CHUNKS;
       } else if (a == 66) {
         name = "gpu_perman64_xshared_coalescing_mshared_multigpu_sparse_manual_distribution";
-        sched = SUP_SCHED_STATIC;
+        sched = SUP_SCHED_MANUAL;
         o.gpu_num = 4;
       } else {
         std::cout << "Unknown Algorithm ID" << std::endl;

@@ -86,3 +86,54 @@ def test_pairwise_fold_is_engine_tree():
     assert bench.pairwise(v) == ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]))
     assert bench.pairwise(v[:3]) == (v[0] + v[1]) + (v[2] + 0.0)
     assert bench.pairwise([2.5]) == 2.5
+
+
+def _plan_worker(rank, world, port, mat, perturb, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    import superman_amd as S
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a = mat.copy()
+    if perturb and rank == world - 1:
+        a[0, 0] += 1.0  # this rank would walk another matrix's plan
+    # what bench.timed does before its warmup: plan (+ compile), then the key
+    S.prepare(a, "dense", jit=1, gpu_num=world)
+    info = S.plan_info(a, "dense", jit=1, gpu_num=world)
+    key = S.plan_key(a, "dense", jit=1, gpu_num=world)
+    try:
+        keys = bench.check_plans_agree(key, rank, world, "cpu")
+        out = ("ok", keys, info["kind"])
+    except RuntimeError as e:
+        out = ("mismatch", str(e), info["kind"])
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("perturb", [False, True])
+def test_bench_plan_fingerprint_guard(perturb):
+    """bench.py all-gathers every rank's plan fingerprint (sup_plan_key) after
+    S.prepare and aborts when ranks planned different walks — a mismatch would
+    otherwise sum shards of two enumerations into a silently wrong permanent."""
+    n, world = 24, 2
+    rng = np.random.default_rng(17)
+    mat = np.where(rng.random((n, n)) < 0.5, rng.random((n, n)) * 5, 0.0)
+    mat[np.arange(n), rng.permutation(n)] = 1.0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, world, port, mat, perturb, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in range(world):
+        status, detail, kind = res[r]
+        assert kind == "seg"
+        if perturb:
+            assert status == "mismatch" and "planned different walks" in detail
+        else:
+            assert status == "ok" and len(set(detail)) == 1
