@@ -291,39 +291,23 @@ int sup_approx(const void* mat, sup_dtype t, int n, int method, uint64_t samples
     std::vector<DevWorker> dw(G);
     for (int g = 0; g < G && rc == SUP_OK; ++g) rc = dw[g].init(o.device_id + g, J, item);
     if (rc) return rc;
-    std::atomic<uint64_t> next{0};
-    std::atomic<int> failed{SUP_OK};
     std::atomic<int64_t> cpu_blocks{0};
-    auto gpu = [&](int g) {
-      for (;;) {
-        const uint64_t it = next.fetch_add(1);
-        if (it >= nitems || failed.load()) return;
-        const uint64_t b0 = it * item, b1 = std::min(nblocks, b0 + item);
-        double r[3];
-        const int e = dw[g].run(J, b0, b1 - b0, r);
-        if (e) {
-          failed.store(e);
-          return;
-        }
-        is[it] = r[0], iq[it] = r[1], iz[it] = r[2];
-      }
-    };
-    auto cpu = [&]() {  // hybrid worker (-c with -g), the reference's cpu_chunk
-      for (;;) {
-        const uint64_t it = next.fetch_add(1);
-        if (it >= nitems || failed.load()) return;
-        const uint64_t b0 = it * item, b1 = std::min(nblocks, b0 + item);
-        double r[3];
+    // takers 0..G-1: one host thread per device; taker G: the hybrid CPU
+    // worker (-c with -g), the reference's cpu_chunk
+    auto take = [&](int g, uint64_t it) -> int {
+      const uint64_t b0 = it * item, b1 = std::min(nblocks, b0 + item);
+      double r[3];
+      if (g == G) {
         cpu_item(J, b0, b1, std::max(1, o.threads), r);
-        is[it] = r[0], iq[it] = r[1], iz[it] = r[2];
         cpu_blocks += (int64_t)(b1 - b0);
+      } else {
+        const int e = dw[g].run(J, b0, b1 - b0, r);
+        if (e) return e;
       }
+      is[it] = r[0], iq[it] = r[1], iz[it] = r[2];
+      return SUP_OK;
     };
-    std::vector<std::thread> th;
-    for (int g = 0; g < G; ++g) th.emplace_back(gpu, g);
-    if (o.cpu_worker) th.emplace_back(cpu);
-    for (auto& x : th) x.join();
-    if (failed.load()) return failed.load();
+    if ((rc = run_item_queue(nitems, G + (o.cpu_worker ? 1 : 0), take))) return rc;
     for (int g = 0; g < G; ++g) res->kernel_ms = std::max(res->kernel_ms, dw[g].kernel_ms);
     res->devices = G;
     res->cpu_blocks = cpu_blocks.load();

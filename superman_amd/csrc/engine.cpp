@@ -911,6 +911,37 @@ static int rccl_allreduce_slots(RcclSlots& r, std::vector<double>& merged) {
 }
 
 // ------------------------------------------------------------ schedulers --
+int run_item_queue(uint64_t nitems, int takers, const std::function<int(int, uint64_t)>& take) {
+  std::atomic<uint64_t> next{0};
+  std::atomic<bool> failed{false};
+  std::vector<int> rcs(takers, SUP_OK);
+  std::vector<std::string> errs(takers);  // g_err is thread_local: carry worker messages back
+  auto worker = [&](int t) {
+    while (!failed.load()) {
+      const uint64_t it = next.fetch_add(1);
+      if (it >= nitems) return;
+      if ((rcs[t] = take(t, it)) != SUP_OK) {
+        errs[t] = last_error();
+        failed.store(true);
+        return;
+      }
+    }
+  };
+  if (takers == 1) {
+    worker(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < takers; ++t) th.emplace_back(worker, t);
+    for (auto& x : th) x.join();
+  }
+  for (int t = 0; t < takers; ++t)
+    if (rcs[t]) {
+      set_error(errs[t]);
+      return rcs[t];
+    }
+  return SUP_OK;
+}
+
 int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uint64_t c1,
              SchedResult& out) {
   out = SchedResult();
@@ -1033,32 +1064,21 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   std::vector<double> dev_ms(G + 1, 0.0), dev_jit(G, 0.0);
   std::vector<uint64_t> dev_vis(G + 1, 0);
   std::vector<int> dev_grid(G + 1, 0);
-  std::vector<int> rcs(G + 1, SUP_OK);
-  std::vector<std::string> errs(G + 1);  // worker-thread messages (g_err is thread_local)
   std::vector<double> dev_sum(G, 0.0);
-  std::atomic<uint64_t> next{0};
   std::atomic<int> cpu_items{0};
-  std::atomic<bool> failed{false};
-  auto gpu_worker = [&](int g) {
-    for (;;) {
-      if (failed.load()) return;
-      const uint64_t it = next.fetch_add(1);
-      if (it >= nitems) return;
-      const uint64_t a = c0 + it * item;
-      const uint64_t b = std::min(c1, a + item);
+  // takers 0..G-1: one host thread per device; taker G: the CPU worker
+  auto take = [&](int g, uint64_t it) -> int {
+    const uint64_t a = c0 + it * item;
+    const uint64_t b = std::min(c1, a + item);
+    auto t0 = std::chrono::steady_clock::now();
+    if (g == G) {
+      ipart[it] = cpu_walk_range(P, a, b, std::max(1, o.threads));
+      dev_vis[G] += (b - a) << (P.lay.L + P.lay.m);
+      cpu_items.fetch_add(1);
+    } else {
       RangeResult r;
-      auto t0 = std::chrono::steady_clock::now();
-      int e = run_range(devs[g], P, a, b, want_visited, r, rccl_items ? slots.buf[g] + it : nullptr);
-      if (e) {
-        rcs[g] = e;
-        errs[g] = last_error();
-        failed.store(true);
-        return;
-      }
-      if (o.verbose) {
-        double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        std::printf("ChunkID %llu is DONE by kernel%d in %f\n", (unsigned long long)it, devs[g], s);
-      }
+      const int e = run_range(devs[g], P, a, b, want_visited, r, rccl_items ? slots.buf[g] + it : nullptr);
+      if (e) return e;
       ipart[it] = r.partial;
       dev_sum[g] += r.partial;
       dev_ms[g] += r.kernel_ms;
@@ -1066,33 +1086,14 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
       dev_vis[g] += r.visited;
       dev_grid[g] = std::max(dev_grid[g], r.grid);
     }
-  };
-  auto cpu_worker = [&]() {
-    for (;;) {
-      if (failed.load()) return;
-      const uint64_t it = next.fetch_add(1);
-      if (it >= nitems) return;
-      const uint64_t a = c0 + it * item;
-      const uint64_t b = std::min(c1, a + item);
-      auto t0 = std::chrono::steady_clock::now();
-      ipart[it] = cpu_walk_range(P, a, b, std::max(1, o.threads));
-      dev_vis[G] += (b - a) << (P.lay.L + P.lay.m);
-      cpu_items.fetch_add(1);
-      if (o.verbose) {
-        double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        std::printf("ChunkID %llu is DONE by CPU in %f\n", (unsigned long long)it, s);
-      }
+    if (o.verbose) {
+      const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (g == G) std::printf("ChunkID %llu is DONE by CPU in %f\n", (unsigned long long)it, sec);
+      else std::printf("ChunkID %llu is DONE by kernel%d in %f\n", (unsigned long long)it, devs[g], sec);
     }
+    return SUP_OK;
   };
-  std::vector<std::thread> th;
-  for (int g = 0; g < G; ++g) th.emplace_back(gpu_worker, g);
-  if (o.cpu_worker) th.emplace_back(cpu_worker);
-  for (auto& t : th) t.join();
-  for (int g = 0; g <= G; ++g)
-    if (rcs[g]) {
-      set_error(errs[g]);
-      return rcs[g];
-    }
+  if ((rc = run_item_queue(nitems, G + (o.cpu_worker ? 1 : 0), take))) return rc;
   out.devices = G;
   out.cpu_items = cpu_items.load();
   for (int g = 0; g < G; ++g) worker_jit_ms = std::max(worker_jit_ms, dev_jit[g]);

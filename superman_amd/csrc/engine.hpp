@@ -191,6 +191,14 @@ struct RangeResult {
 };
 
 // Walk wave-chunks [c0, c1) of plan P on device `dev` (synchronous).
+// The dynamic item queue shared by -p6/-p8, the exact path and the
+// estimators: `takers` host threads (one per device, plus the hybrid CPU
+// worker) pull item indices 0..nitems-1 from one atomic counter until they run
+// out or a taker fails; take(taker, item) writes only its own outputs
+// (item-indexed slots, per-taker accumulators), so the combined result never
+// depends on who took which item.  Returns SUP_OK or the first failure (with
+// its message).
+int run_item_queue(uint64_t nitems, int takers, const std::function<int(int, uint64_t)>& take);
 // slot (optional): a device pointer on `dev`; the range's partial is also
 // copied there on the device (the -R combine all-reduces those slots).
 int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visited, RangeResult& r,

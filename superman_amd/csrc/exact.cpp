@@ -240,49 +240,31 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
     const uint64_t nitems = (C + item - 1) / item;
     std::vector<std::vector<uint64_t>> dres(takers, std::vector<uint64_t>(np, 0));
     std::vector<double> dms(takers, 0.0);
-    std::vector<int> drc(takers, SUP_OK), dtook(takers, 0);
-    std::vector<std::string> derr(takers);  // g_err is thread_local: carry worker messages back
-    std::atomic<uint64_t> next{0};
-    std::atomic<bool> failed{false};
+    std::vector<int> dtook(takers, 0);
     auto add = [&](int g, const std::vector<uint64_t>& r, int q0) {
       for (size_t i = 0; i < r.size(); ++i) dres[g][q0 + i] = (dres[g][q0 + i] + r[i]) % (uint64_t)primes[q0 + i];
     };
-    auto worker = [&](int g) {
-      for (;;) {
-        if (failed.load()) return;
-        const uint64_t it = next.fetch_add(1);
-        if (it >= nitems) return;
-        const uint64_t a = it * item, b = std::min(C, a + item);
-        if (g == G) {  // the CPU worker: every prime in one pass
+    auto take = [&](int g, uint64_t it) -> int {
+      const uint64_t a = it * item, b = std::min(C, a + item);
+      if (g == G) {  // the CPU worker: every prime in one pass
+        std::vector<uint64_t> r;
+        cpu_exact_range(P, a, b, primes, std::max(o.threads, 1), r);
+        add(g, r, 0);
+      } else {
+        for (int q0 = 0; q0 < np; q0 += kMaxPrimes) {
+          const std::vector<double> pr(primes.begin() + q0, primes.begin() + std::min(np, q0 + kMaxPrimes));
           std::vector<uint64_t> r;
-          cpu_exact_range(P, a, b, primes, std::max(o.threads, 1), r);
-          add(g, r, 0);
-        } else {
-          for (int q0 = 0; q0 < np; q0 += kMaxPrimes) {
-            const std::vector<double> pr(primes.begin() + q0, primes.begin() + std::min(np, q0 + kMaxPrimes));
-            std::vector<uint64_t> r;
-            double ms = 0.0;
-            if ((drc[g] = run_range_exact(o.device_id + g, P, group, a, b, pr, r, &ms))) {
-              derr[g] = last_error();
-              failed.store(true);
-              return;
-            }
-            add(g, r, q0);
-            dms[g] += ms;
-          }
+          double ms = 0.0;
+          const int e = run_range_exact(o.device_id + g, P, group, a, b, pr, r, &ms);
+          if (e) return e;
+          add(g, r, q0);
+          dms[g] += ms;
         }
-        ++dtook[g];
       }
+      ++dtook[g];
+      return SUP_OK;
     };
-    std::vector<std::thread> th;
-    for (int g = 1; g < takers; ++g) th.emplace_back(worker, g);
-    worker(0);
-    for (auto& t : th) t.join();
-    for (int g = 0; g < takers; ++g)
-      if (drc[g]) {
-        set_error(derr[g]);
-        return drc[g];
-      }
+    if ((rc = run_item_queue(nitems, takers, take))) return rc;
     for (int q = 0; q < np; ++q)
       for (int g = 0; g < takers; ++g) res[q] = (res[q] + dres[g][q]) % (uint64_t)primes[q];
     kms = *std::max_element(dms.begin(), dms.begin() + G);

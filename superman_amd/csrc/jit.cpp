@@ -1337,9 +1337,13 @@ struct Gen {
     if (const char* e = std::getenv("SUP_JIT_PHASE"))
       if (std::atoi(e) > 0)
         o << "  if (blockIdx.x & 1u) __builtin_amdgcn_s_sleep(" << std::min(127, std::atoi(e)) << ");\n";
+    // A group's chunk partials (and walked-step counts) wait in LDS, not in
+    // registers held across the walk loop: two fewer VGPR values live in the
+    // loop (LDS is otherwise unused; 3 KB per block).
+    o << "  __shared__ double s_keep[" << kBlock / 64 << "][64];\n";
+    o << "  __shared__ uint32_t s_vkeep[" << kBlock / 64 << "][64];\n";
+    o << "  const uint32_t wv = threadIdx.x >> 6;\n";
     o << "  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {\n";
-    o << "    double keep = 0.0;\n";
-    o << "    uint32_t vkeep = 0;\n";  // per chunk: Gray steps walked per lane (0 when skipped)
     o << "    for (uint32_t j = 0; j < (uint32_t)p.group; ++j) {\n";
     o << "      const uint64_t a = (uint64_t)g * p.group + j;\n";
     o << "      if (a >= p.chunk_count) break;\n";
@@ -1442,14 +1446,17 @@ struct Gen {
     o << "      if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;\n";
     o << "      }\n";
     o << "      const double part = wave_sum(lane_valid ? acc : 0.0);\n";
-    o << "      keep = (lane == j) ? part : keep;\n";
-    o << "      vkeep = (lane == j) ? vis : vkeep;\n";
+    o << "      if (lane == j) s_keep[wv][j] = part, s_vkeep[wv][j] = vis;\n";
     o << "    }\n";
+    o << "    __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n";
+    o << "    __builtin_amdgcn_wave_barrier();\n";
+    o << "    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n";
     o << "    const uint64_t a = (uint64_t)g * p.group + lane;\n";
     o << "    if (lane < (uint32_t)p.group && a < p.chunk_count) {\n";
-    o << "      p.chunk_out[a] = keep;\n";
-    o << "      if (p.visited) p.visited[a] = vkeep;\n";
+    o << "      p.chunk_out[a] = s_keep[wv][lane];\n";
+    o << "      if (p.visited) p.visited[a] = s_vkeep[wv][lane];\n";
     o << "    }\n";
+    o << "    __builtin_amdgcn_wave_barrier();\n";
     o << "  }\n";
     o << "}\n";
     o << "}  // namespace sup\n";

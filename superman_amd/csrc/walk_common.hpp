@@ -39,16 +39,20 @@ typedef const __attribute__((address_space(4))) int cint;
 
 // Hide a uniform address from LLVM's loop-invariant code motion: otherwise the
 // k = 0 columns (constant addresses) are hoisted out of the walk and pinned in
-// SGPRs, which spills.  "+s" keeps the value wave-uniform and in SGPRs.
+// SGPRs, which spills.  "+s" keeps the value wave-uniform and in SGPRs.  The
+// base goes through the asm and the offset is added after it, so neither the
+// load nor its address can leave the loop (an address formed before the asm
+// was hoisted: one SGPR pair per constant, live for the whole kernel), and a
+// constant offset folds into the s_load immediate.
 __device__ __forceinline__ cdbl* opaque_c(const double* base, uint32_t byte_off) {
-  uint64_t a = (uint64_t)base + byte_off;
+  uint64_t a = (uint64_t)base;
   asm volatile("" : "+s"(a));
-  return (cdbl*)a;
+  return (cdbl*)(a + byte_off);
 }
 __device__ __forceinline__ cint* opaque_i(const int* base, uint32_t byte_off) {
-  uint64_t a = (uint64_t)base + byte_off;
+  uint64_t a = (uint64_t)base;
   asm volatile("" : "+s"(a));
-  return (cint*)a;
+  return (cint*)(a + byte_off);
 }
 
 // x[LO..HI) += col[LO..HI)   (col wave-uniform -> SGPR operands)

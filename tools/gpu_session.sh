@@ -42,6 +42,7 @@ for step in "$@"; do
              run "pmc44_sq_$k" 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT --kernel-trace -d "$OUT/pmc44_sq_$k" -o run --output-format csv -- python3 tools/run_one.py synth44_0.15_int 2 $k
              run "pmc44_wait_$k" 300 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_WAIT_ANY --kernel-trace -d "$OUT/pmc44_wait_$k" -o run --output-format csv -- python3 tools/run_one.py synth44_0.15_int 2 $k
            done;;
+    *=*) run "${step%%=*}" 900 bash -c "${step#*=}";;   # name=command
     *) run "$step" 900 bash -c "$step";;
   esac
 done
