@@ -24,12 +24,15 @@ BASELINE configs 2, 3 and 5 are timed the same way under "configs"
 (--configs 0 skips them).
 
 Prints ONE JSON line on rank 0 (driver contract), including the roofline of
-the walk kernel (hipEvents on its own stream, measured inside the library)
-and a CPU baseline (oracle/ port of the reference's parallel_perman64 chunk
-loop, timed on a bounded sample of the same workload on this host's cores).
-The roofline object also carries the committed rocprofv3 PMC evidence for the
-walk kernel (achieved occupancy, LDS bank conflicts, VALU instructions per
-step, HBM bytes per launch; profiles/, tools/pmc_summary.py).
+the walk kernel and a CPU baseline (oracle/ port of the reference's
+parallel_perman64 chunk loop, timed on a bounded sample of the same workload
+on this host's cores; beside it the reference's own compiled CPU code on
+config 1).  Roofline: `achieved` = the walk's fp64 flops per Gray step
+measured by rocprofv3 --pmc (SQ_INSTS_VALU_{ADD,MUL,FMA}_F64, FMA = 2 flops;
+a child run of this script under rocprofv3, --pmc 1, N = 1) x the Gray steps
+of a launch / the launch's mean duration (hipEvents on the walk's stream,
+inside the library); `traffic` = HBM bytes per launch from the committed
+FETCH_SIZE / WRITE_SIZE passes of the same plan (profiles/r3, tools/pmc_r3.py).
 """
 from __future__ import annotations
 
@@ -62,9 +65,14 @@ def parse():
                     help="all ranks on device 0 over gloo: rehearse the N-rank path on a one-GPU box")
     ap.add_argument("--prep", type=int, default=0, choices=[0, 1, 2], help="-r: 1 SortOrder, 2 SkipOrder")
     ap.add_argument("--configs", type=int, default=1, help="also time BASELINE configs 2, 3 and 5 (0 = skip)")
-    ap.add_argument("--also", default=os.path.join(ROOT, "tests", "fixtures", "double__40_0.20_0"),
+    ap.add_argument("--also", default=",".join(os.path.join(ROOT, "tests", "fixtures", f)
+                                                for f in ("double__40_0.20_0", "double__40_0.90_0")),
                     help="comma-separated companion matrices timed the same way (north star: densities "
-                         "0.2 and 0.5 at every N); '' = none")
+                         "0.2 and 0.5 at every N; 0.9: a near-dense point); '' = none")
+    ap.add_argument("--pmc", type=int, default=1,
+                    help="1: measure the walk kernel's fp64 flops with rocprofv3 --pmc in a child run "
+                         "(N = 1, rank 0; falls back to the committed profile); 0: committed profile only")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -124,18 +132,102 @@ def check_plans_agree(key: int, rank: int, world: int, device) -> list:
     return keys
 
 
-def pmc_record(n: int, kernel: str):
-    """The committed rocprofv3 PMC summary of this walk kernel at this n
-    (tools/pmc_summary.py: HBM bytes per launch, achieved occupancy, LDS bank
-    conflicts), newest round first; None if there is none."""
+# fp64 instruction counters (gfx950, rocprofv3 counter_defs.yaml: per-wave
+# instructions, summed over SEs); flops = 64 lanes x (ADD + MUL + 2 FMA), the
+# same expression as rocprofv3's derived FP64 FLOPS counter.  One pass: 6 SQ
+# + 2 GRBM counters (the hardware allows 8 SQ, 2 GRBM per pass).
+PMC_COUNTERS = ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU",
+                "SQ_WAVES", "SQ_INSTS_SALU", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
+
+
+def pmc_child(args) -> None:
+    """--pmc-child: one launch of the walk the parent times (same plan: same
+    matrix, kernel request, jit, one shard), run under rocprofv3 by the parent."""
+    import superman_amd as S
+    a = S.read_matrix(args.matrix)[0]
+    if args.prep == 1:
+        a = S.sort_order(a)[0]
+    elif args.prep == 2:
+        a = S.skip_order(a)[0]
+    S.prepare(a, args.kernel, jit=args.jit, gpu_num=1)
+    _, st = S.perman_shard(a, 0, 1, kernel=args.kernel, jit=args.jit, return_stats=True)
+    print(json.dumps({"gray_steps": st["gray_steps"], "visited_steps": st["visited_steps"],
+                      "walk_kind": st["walk_kind"]}), flush=True)
+
+
+def pmc_live(matrix: str, kernel: str, jit: int, prep: int, walk: str):
+    """Measured fp64 work of one launch of `walk`: runs this script's
+    --pmc-child under `rocprofv3 --pmc` (a child process, --kernel-trace only)
+    and reads the counters of the walk kernel's dispatch.  None if rocprofv3
+    is absent or the pass fails (the caller falls back to the committed
+    profile)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None
+    out = tempfile.mkdtemp(prefix="sup_pmc_")
+    cmd = [prof, "--pmc", *PMC_COUNTERS, "--kernel-trace", "-d", out, "-o", "run", "--output-format", "csv", "--",
+           sys.executable, os.path.abspath(__file__), "--pmc-child", "--matrix", matrix, "--kernel", kernel,
+           "--jit", str(jit), "--prep", str(prep)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+        child = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
+        vals, ns = {}, []
+        for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                if walk in row["Kernel_Name"]:
+                    vals[row["Counter_Name"]] = vals.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+                    ns.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+        if r.returncode != 0 or not child or "SQ_INSTS_VALU_FMA_F64" not in vals:
+            return None
+    except (subprocess.SubprocessError, OSError, ValueError):
+        return None
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+    steps = child[-1]["gray_steps"]
+    flops = 64.0 * (vals["SQ_INSTS_VALU_ADD_F64"] + vals["SQ_INSTS_VALU_MUL_F64"] + 2.0 * vals["SQ_INSTS_VALU_FMA_F64"])
+    fp64_insts = vals["SQ_INSTS_VALU_ADD_F64"] + vals["SQ_INSTS_VALU_MUL_F64"] + vals["SQ_INSTS_VALU_FMA_F64"]
+    wave_steps = steps / 64.0
+    return {"flops_per_gray_step": flops / steps,
+            "fp64_insts_per_lane_step": fp64_insts / wave_steps,
+            "fma_share": vals["SQ_INSTS_VALU_FMA_F64"] / fp64_insts,
+            "valu_insts_per_lane_step": vals.get("SQ_INSTS_VALU", 0.0) / wave_steps,
+            "kernel_ns_under_pmc": max(ns) if ns else None,
+            "counters": {k: vals[k] for k in PMC_COUNTERS if k in vals},
+            "source": "rocprofv3 --pmc " + " ".join(PMC_COUNTERS) + " --kernel-trace, one launch of this walk "
+                      "(bench.py --pmc-child, same plan), measured in this run"}
+
+
+def pmc_committed(n: int, walk: str, key: str):
+    """The committed F64-counter profile of this walk (profiles/*/pmc_f64_*.json,
+    tools/pmc_summary.py f64) when it was taken on the same plan (plan key)."""
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "pmc_f64_*.json"), recursive=True), reverse=True):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if d.get("n") == n and walk in d.get("kernel", "") and d.get("plan_key") == key:
+            d["source"] = f"committed profile {os.path.relpath(p, ROOT)} (same plan key)"
+            return d
+    return None
+
+
+def pmc_record(n: int, kernel: str, key: str):
+    """The committed rocprofv3 HBM profile (FETCH_SIZE + WRITE_SIZE per launch,
+    tools/pmc_r3.py hbm) of this walk kernel taken on the same plan (plan
+    key); None if there is none."""
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc*.json"), recursive=True), reverse=True):
         try:
             d = json.load(open(p))
-            if d.get("n") == n and "hbm_bytes_per_launch" in d and kernel in d.get("kernel", ""):
-                d["_path"] = os.path.relpath(p, ROOT)
-                return d
-        except Exception:
-            pass
+        except (OSError, ValueError):
+            continue
+        if (d.get("n") == n and "hbm_bytes_per_launch" in d and kernel in d.get("kernel", "")
+                and d.get("plan_key") == key):
+            d["_path"] = os.path.relpath(p, ROOT)
+            return d
     return None
 
 
@@ -198,6 +290,8 @@ def cpu_reference_config1(S, threads: int):
 def main():
     global args
     args = parse()
+    if args.pmc_child:
+        return pmc_child(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -263,40 +357,77 @@ def main():
             elapsed = float(t.item())
         return elapsed, perm, sum(kms) / len(kms), st, prep["compile_ms"]
 
-    a = load(args.matrix)
-    n = a.shape[0]
-    L, m, _ = S.layout(n)
-    c0, c1 = shard_chunks(n, rank, world)
-    my_steps = (c1 - c0) << (L + m)
-    elapsed, perm, k_ms, st, compile_ms = timed(a)
     walk_names = {0: "dense", 1: "prefix-blocked", 2: "skipper", 3: "segmented (pattern-specialised)",
                   4: "dense, X in LDS"}
 
-    # companion densities (north star: 0.2 and 0.5), same shards / all-reduce / clock
+    def walk_kernel(st, n):
+        return {0: f"sup::walk_dense<{n}>", 1: f"sup::walk_sparse<{n}>", 2: f"sup::walk_skip<{n}>",
+                3: "sup_walk_seg", 4: f"sup::walk_lds<{n}>"}[st["walk_kind"]]
+
+    def roofline(path, b, prep, kernel, jit, kms, st):
+        """Roofline of the walk kernel for this rank's shard.  achieved = the
+        walk's fp64 flops per Gray step MEASURED with rocprofv3 --pmc (FMA = 2
+        flops; pmc_live, or the committed profile of the same plan) x this
+        rank's Gray steps / its mean walk-kernel time (hipEvents on the walk's
+        stream, inside the library).  Without a measurement the cost model
+        stands in and `achieved_source` says so.  SURVEY 8(d)'s nominal 2n
+        flops per Gray step (the plain walk's n adds + n muls) is kept as
+        gray_step_equiv_*: the rate the plain algorithm would need."""
+        nb = b.shape[0]
+        steps = st["gray_steps"]  # this rank's shard
+        walk = walk_kernel(st, nb)
+        key = hex(S.plan_key(b, kernel, jit=jit, gpu_num=world, device_id=dev))
+        meas = pmc_live(path, kernel, jit, prep, walk) if (args.pmc and world == 1 and rank == 0) else None
+        meas = meas or pmc_committed(nb, walk, key)
+        fps = meas["flops_per_gray_step"] if meas else st["est_ops_per_step"]
+        achieved = fps * steps / (kms * 1e-3) / 1e12
+        nominal = 2.0 * nb * steps / (kms * 1e-3) / 1e12
+        r = {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+             "frac": achieved / FP64_PEAK_TFLOPS, "kernel": walk, "kernel_ms_avg": kms,
+             "flops_per_gray_step": fps,
+             "achieved_source": meas["source"] if meas else "cost model (no rocprofv3 measurement available)",
+             "algorithmic_flops_per_launch": fps * steps,
+             "flops_definition": "fp64 flops per Gray step executed by the walk kernel: 64 x (SQ_INSTS_VALU_ADD_F64 "
+                                 "+ SQ_INSTS_VALU_MUL_F64 + 2 SQ_INSTS_VALU_FMA_F64) per launch / its Gray steps",
+             "model_ops_per_gray_step": st["est_ops_per_step"],
+             "gray_step_equiv_tflops": nominal, "gray_step_equiv_frac": nominal / FP64_PEAK_TFLOPS,
+             "gray_step_equiv_definition": f"2n = {2 * nb} fp64 flops per Gray step (SURVEY 8(d), the plain walk's "
+                                           "n adds + n muls); above 1 where the walk skips the operations "
+                                           "structural zeros make redundant", "plan_key": key}
+        if meas:
+            r["fp64_insts_per_lane_step"] = meas.get("fp64_insts_per_lane_step")
+            r["fma_share"] = meas.get("fma_share")
+            r["valu_insts_per_lane_step"] = meas.get("valu_insts_per_lane_step")
+            # fp64 VALU issue: one wave-instruction per 4 cycles per SIMD; an
+            # fma is 2 flops in one issue, so the issue-bound peak is
+            # peak x (1 + fma share) / 2
+            share = meas.get("fma_share") or 0.0
+            r["issue_frac"] = achieved / (FP64_PEAK_TFLOPS * (1.0 + share) / 2.0)
+        return r
+
+    a = load(args.matrix)
+    n = a.shape[0]
+    elapsed, perm, k_ms, st, compile_ms = timed(a)
+
+    # companion densities (north star: 0.2 and 0.5; 0.9 near-dense), same shards / all-reduce / clock
     also = []
     for path in [p for p in args.also.split(",") if p and os.path.abspath(p) != os.path.abspath(args.matrix)]:
         b = load(path)
         nb = b.shape[0]
         e2, perm2, kms2, st2, _ = timed(b)
-        Lb, mb, _ = S.layout(nb)
-        b0, b1 = shard_chunks(nb, rank, world)
-        ach = st2["est_ops_per_step"] * ((b1 - b0) << (Lb + mb)) / (kms2 * 1e-3) / 1e12  # as the headline
         also.append({"matrix": os.path.basename(path).replace("__", "/"), "n": nb,
                      "density": round(float((b != 0).sum()) / (nb * nb), 4),
                      "value": args.steps * (1 << (nb - 1)) / e2, "unit": "gray-steps/s",
                      "ms_per_step": e2 / args.steps * 1e3, "kernel_ms_avg": kms2,
                      "walk": walk_names[st2["walk_kind"]],
-                     "roofline": {"achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                  "frac": ach / FP64_PEAK_TFLOPS, "issue_frac": ach / (FP64_PEAK_TFLOPS / 2),
-                                  "gray_step_equiv_frac": 2.0 * nb * ((b1 - b0) << (Lb + mb)) /
-                                  (kms2 * 1e-3) / 1e12 / FP64_PEAK_TFLOPS},
-                     "est_fp64_ops_per_step": st2["est_ops_per_step"], "permanent": perm2})
+                     "roofline": roofline(path, b, args.prep, args.kernel, args.jit, kms2, st2),
+                     "permanent": perm2})
 
     # the other BASELINE configs (2, 3, 5), same shards / all-reduce / clock.
     # Configs 2 and 3 with --jit 1 (the compile is outside the timed steps, as
     # for the headline; the CLI's auto mode keeps the AOT walk there because a
-    # single run would not repay the 0.2 s compile); config 5 both as the
-    # SkipPer kernel itself and as the engine's choice for the -p8 request
+    # single run would not repay the compile); config 5 both as the SkipPer
+    # kernel itself and as the engine's choice for the -p8 request
     configs = []
     if args.configs:
         fx = os.path.join(ROOT, "tests", "fixtures")
@@ -332,23 +463,10 @@ def main():
 
     total_steps = args.steps * (1 << (n - 1))
     value = total_steps / elapsed
-    # Roofline of the walk kernel.  Algorithmic work per Gray step = the fp64
-    # operations of the walk that runs (its cost model: est_ops_per_step, 18.0
-    # for the bench matrix's segmented walk), so `frac` is a true
-    # fraction of the fp64 peak.  Every one of those ops is an add, a mul or an
-    # fma issued as one VALU instruction; counting each as one flop (an fma as
-    # one too) makes `achieved` a lower bound.  Without FMA the issue ceiling
-    # is peak / 2, hence `issue_frac` = achieved / (peak / 2).  SURVEY §8(d)'s
-    # nominal 2n flops per Gray step (the plain walk's n adds + n muls) is kept
-    # as gray_step_equiv_*: the rate the plain algorithm would need.
-    ops_step = st["est_ops_per_step"]
-    flops = ops_step * my_steps
-    achieved = flops / (k_ms * 1e-3) / 1e12
-    nominal = 2.0 * n * my_steps / (k_ms * 1e-3) / 1e12
-    walk = {0: f"sup::walk_dense<{n}>", 1: f"sup::walk_sparse<{n}>", 2: f"sup::walk_skip<{n}>",
-            3: "sup_walk_seg", 4: f"sup::walk_lds<{n}>"}[st["walk_kind"]]
-    pmc = pmc_record(n, walk)
-    traffic = pmc["hbm_bytes_per_launch"] if pmc else None
+    roof = roofline(args.matrix, a, args.prep, args.kernel, args.jit, k_ms, st)
+    walk = roof["kernel"]
+    pmc = pmc_record(n, walk, roof["plan_key"])
+    roof["traffic"] = pmc["hbm_bytes_per_launch"] if pmc else None
     fname = os.path.basename(args.matrix).replace("__", "/")
     density = float((a != 0).sum()) / (n * n)
     rec = {
@@ -371,33 +489,17 @@ def main():
                    "walk": walk_names[st["walk_kind"]],
                    "jit_compile_ms": compile_ms,
                    "parallelism": f"dp{world}: contiguous wave-chunk shards + one RCCL all-reduce"},
-        "roofline": {"bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": walk, "kernel_ms_avg": k_ms,
-                     "algorithmic_flops_per_launch": flops,
-                     "flops_definition": f"{ops_step:.2f} fp64 ops per Gray step: the {walk} walk's cost model "
-                                         "(adds, muls, fmas it issues per step, each counted as 1 flop); "
-                                         "fp64 issue ceiling without FMA = 0.5 of peak",
-                     "issue_frac": achieved / (FP64_PEAK_TFLOPS / 2),
-                     "gray_step_equiv_tflops": nominal,
-                     "gray_step_equiv_frac": nominal / FP64_PEAK_TFLOPS,
-                     "gray_step_equiv_definition": f"2n = {2 * n} fp64 flops per Gray step (SURVEY 8(d), the "
-                                                   "plain walk's n adds + n muls); above 1 because the walk "
-                                                   "skips the operations structural zeros make redundant"},
+        "roofline": roof,
         "permanent": perm,
         "kernel_ms_per_rank": rank_kms,
         "densities": also,
         "configs": configs,
     }
-    if pmc:  # rocprofv3 evidence for the dominant kernel (committed profile of this kernel at this n)
-        sq = pmc.get("sq", {})
+    if pmc:  # rocprofv3 HBM evidence for the dominant kernel (committed profile of the same plan)
         rec["roofline"].update({
-            "pmc_source": pmc["_path"],
-            "achieved_waves_per_simd": sq.get("achieved_waves_per_simd"),
-            "achieved_occupancy_frac": sq.get("achieved_occupancy_frac"),
-            "lds_bank_conflicts": sq.get("SQ_LDS_BANK_CONFLICT"),
-            "valu_insts_per_step": sq.get("valu_insts_per_lane_step"),
-            "valu_busy_frac": sq.get("valu_busy_frac_est")})
+            "traffic_source": pmc["_path"],
+            "algorithmic_bytes_per_launch": pmc.get("algorithmic_bytes_per_launch"),
+            "traffic_over_algorithmic": pmc.get("hbm_over_algorithmic")})
     # true error: the corpus files hold 6-digit decimals, whose exact permanent the
     # exact integer path computed once (tests/golden/exact_corpus.json)
     try:
@@ -405,10 +507,14 @@ def main():
         key = os.path.basename(args.matrix)
         if key in ex and args.prep == 0:
             rec["rel_err_vs_exact"] = abs(perm - ex[key]) / abs(ex[key])
-            for d in also:
-                k2 = d["matrix"].replace("/", "__")
-                if k2 in ex:
-                    d["rel_err_vs_exact"] = abs(d["permanent"] - ex[k2]) / abs(ex[k2])
+        for d in also:
+            k2 = d["matrix"].replace("/", "__")
+            if k2 in ex:
+                d["rel_err_vs_exact"] = abs(d["permanent"] - ex[k2]) / abs(ex[k2])
+        for d in configs:
+            k2 = d["matrix"].replace("/", "__")
+            if k2 in ex:
+                d["rel_err_vs_exact"] = abs(d["permanent"] - ex[k2]) / abs(ex[k2])
     except (OSError, ValueError):
         pass
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

@@ -147,3 +147,23 @@ def test_reduced_exact_vs_direct(sup, orc, tmp_path):
     assert int(line.split()[1]) == r
     with pytest.raises(sup.SupError):
         sup.perman_reduced_exact(a.astype(np.float64) + 0.5, cpu=True)
+
+
+def test_exact_corpus_integers_consistent():
+    """tests/golden/exact_corpus.json: every committed exact integer (the GPU
+    residue walk's output, profiles/r3/probe_exact_truth.log) divided by its
+    decimal scale rounds to the committed fp64 value the -m gpu tests pin the
+    benchmarked walks against (tests/test_gpu_pinned.py)."""
+    import json
+    import os
+    from fractions import Fraction
+
+    from conftest import ROOT, fixture_path
+    ex = json.load(open(os.path.join(ROOT, "tests", "golden", "exact_corpus.json")))
+    assert set(ex["_integers"]) >= {"double__32_0.50_0", "double__36_0.20_0", "double__40_0.90_0",
+                                    "synth44_0.15_int"}
+    for name, rec in ex["_integers"].items():
+        with open(fixture_path(name)) as f:
+            n = int(f.readline().split()[0])
+        scale = 1 if rec["scale"] == "1" else 10 ** (6 * n)
+        assert float(Fraction(int(rec["integer"]), scale)) == ex[name]
