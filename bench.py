@@ -73,6 +73,7 @@ def parse():
                     help="1: measure the walk kernel's fp64 flops with rocprofv3 --pmc in a child run "
                          "(N = 1, rank 0; falls back to the committed profile); 0: committed profile only")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cold", type=int, default=1, help="time the CLI end to end with an empty / warm cache (N = 1)")
     return ap.parse_args()
 
 
@@ -254,6 +255,39 @@ def cpu_baseline(a, n: int, budget_s: float, gpu_sup, kernel: str):
     return {"value": size / dt, "unit": "gray-steps/s", "cores": threads, "kind": "port",
             "sample": f"reference Gray indices [2^{n-2}, 2^{n-2}+2^{k}) of {os.path.basename(args.matrix)} "
                       f"({dt:.1f} s, oracle/oracle.c orc_ref_dense_partial = cpu_perman64 restated)"}, err
+
+
+def cold_start(matrix: str) -> dict:
+    """End-to-end wall time of the drop-in CLI (`perman -f <matrix> -g -p4`,
+    a fresh process: HIP init, read, plan, compile, walk, print) with an
+    empty code/plan cache and again with the cache the first runs filled:
+      cold_default  jit = 0 (auto; cold it keeps the ahead-of-time walk: the
+                    segmented plan's search + compile would cost more than it
+                    saves on one run),
+      cold_jit1     --jit 1 (search + compile + segmented walk),
+      warm_default  jit = 0 again: the plan choices and kernel are on disk, so
+                    auto mode takes the segmented walk."""
+    import shutil
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "superman_amd", "bin", "perman")
+    cache = tempfile.mkdtemp(prefix="sup_cold_")
+    env = dict(os.environ, SUP_JIT_CACHE_DIR=cache)
+    out = {"command": f"superman_amd/bin/perman -f {os.path.relpath(matrix, ROOT)} -g -p4 [--jit 1]",
+           "cache": "empty SUP_JIT_CACHE_DIR for the cold runs; the same directory for the warm run"}
+    try:
+        for label, extra in (("cold_default", []), ("cold_jit1", ["--jit", "1"]), ("warm_default", [])):
+            t = time.perf_counter()
+            r = subprocess.run([exe, "-f", matrix, "-g", "-p4", *extra], capture_output=True, text=True, env=env,
+                               timeout=300)
+            wall = time.perf_counter() - t
+            perm = [ln.split()[1] for ln in r.stdout.splitlines() if ln.startswith("Permanent:")]
+            out[label] = {"wall_s": wall, "rc": r.returncode, "permanent": float(perm[0]) if perm else None}
+    except (subprocess.SubprocessError, OSError, ValueError) as e:
+        out["error"] = repr(e)
+    finally:
+        shutil.rmtree(cache, ignore_errors=True)
+    return out
 
 
 def cpu_reference_config1(S, threads: int):
@@ -525,6 +559,8 @@ def main():
         rec["cpu_baseline_reference_config1"] = cpu_reference_config1(S, cb_rec["cores"])
     else:
         rec["cpu_baseline"] = None
+    if rank == 0 and world == 1 and args.cold:
+        rec["cold_start"] = cold_start(args.matrix)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -162,7 +162,8 @@ static double walk_cost_eff(const Plan& P) {
   return P.kind == kWalkSeg ? walk_cost(P) * (1.0 - P.seg_skip) : walk_cost(P);
 }
 
-int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const Layout& lay, Plan& P) {
+int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const Layout& lay, Plan& P,
+              const SegChoice* choice) {
   if (n < 1 || n > SUP_MAX_N) {
     set_error("n must be in [1, 64]");
     return SUP_EINVAL;
@@ -183,9 +184,15 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
     // walk: seg_walk_order), lane bits the next L columns of that order, high
     // bits the rest in matrix order.
     int segb = 0;
-    std::vector<int> order =
-        kind == kWalkSeg ? seg_walk_order(A, n, m, m + L, &segb) : greedy_walk_order(A, n, m + L);
+    std::vector<int> order;
+    if (kind == kWalkSeg && choice && (int)choice->order.size() == m + L) {
+      order = choice->order;
+      segb = choice->b;
+    } else {
+      order = kind == kWalkSeg ? seg_walk_order(A, n, m, m + L, &segb) : greedy_walk_order(A, n, m + L);
+    }
     P.seg_b = segb;
+    if (kind == kWalkSeg) P.seg_order.assign(order.begin(), order.begin() + (m + L));
     std::vector<char> used(n, 0);
     for (int k = 0; k < m; ++k) P.colmap[L + k] = order[k], used[order[k]] = 1;
     for (int e = 0; e < L; ++e) P.colmap[e] = order[m + e], used[order[m + e]] = 1;
@@ -277,7 +284,7 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
       if (A[(size_t)i * n + P.colmap[L + k]] != 0.0) rm |= 1ull << k;
     P.rowmask[j] = rm;
   }
-  if (kind == kWalkSeg) return build_seg(P);
+  if (kind == kWalkSeg) return build_seg(P, choice ? choice->budget : 0);
   return SUP_OK;
 }
 
@@ -289,6 +296,13 @@ static constexpr double kLaneOpsPerSec = 3.7e13;
 // are paid once per matrix; auto mode specialises when the predicted walk time
 // saved is clearly larger than both.
 static constexpr double kJitMinSavingSec = 3.0;
+// When an earlier process recorded this matrix's segmented-walk choices (disk
+// cache, make_seg_plan), the plan is rebuilt in ~5-50 ms and its code object
+// loads from disk: auto mode specialises whenever the walk saves more than this.
+static constexpr double kJitWarmSavingSec = 0.1;
+// Below this order no walk lasts kJitWarmSavingSec (2^29 steps at ~3e12/s):
+// auto mode does not look at the disk cache.
+static constexpr int kJitWarmMinN = 30;
 
 static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit,
                              int ndev, int dev);
@@ -305,22 +319,62 @@ static constexpr double kSegStartOps = 2048.0;
 // start and chunk skip included, wins.  At least 2^15 chunks remain (16 per
 // resident wave of one GPU).  The layout depends only on the matrix, so every
 // GPU count sums the same chunks (bit-identical results).
-static int make_seg_plan(const double* A, int n, const Layout& lay, Plan& P) {
-  int rc = make_plan(A, n, kWalkSeg, false, lay, P);
-  if (rc || lay.fixed) return rc;
-  const int mmax = std::min(lay.m + lay.h - 15, 31);
-  int m2 = lay.m;
-  while (m2 < mmax && std::ldexp(walk_cost(P), m2) < 32.0 * kSegStartOps) ++m2;
-  if (m2 == lay.m) return SUP_OK;
-  Layout l2 = lay;
-  l2.m = m2;
-  l2.h = lay.m + lay.h - m2;
-  Plan s2;
-  if (make_plan(A, n, kWalkSeg, false, l2, s2) != SUP_OK) return SUP_OK;
-  auto eff = [](const Plan& q) {
-    return (1.0 - q.seg_skip) * (walk_cost(q) + std::ldexp(kSegStartOps, -q.lay.m));
+static uint64_t knob_hash_env();
+
+// Disk key of a segmented-walk plan: matrix, layout request, experiment knobs
+// and the toolchain the choices were priced with.
+static uint64_t seg_disk_key(const double* A, int n, const Layout& lay) {
+  uint64_t h = 0x5eed5e9a11ull ^ jit_toolchain_hash();
+  auto mix = [&h](const void* p, size_t bytes) {
+    const unsigned char* c = (const unsigned char*)p;
+    for (size_t i = 0; i < bytes; ++i) h = (h ^ c[i]) * 1099511628211ull;
   };
-  if (eff(s2) < eff(P)) P = std::move(s2);
+  const int32_t head[] = {2 /* format */, n, lay.L, lay.m, (int32_t)lay.fixed};
+  mix(head, sizeof head);
+  mix(A, (size_t)n * n * sizeof(double));
+  const uint64_t k = knob_hash_env();
+  mix(&k, sizeof k);
+  return h;
+}
+
+static int make_seg_plan(const double* A, int n, const Layout& lay, Plan& P) {
+  // a later process rebuilds the plan from its recorded choices (no search,
+  // no compiler check: ~0.1 s instead of seconds)
+  const uint64_t dkey = seg_disk_key(A, n, lay);
+  {
+    int m2 = 0;
+    SegChoice c;
+    if (seg_choice_load(dkey, &m2, &c) && m2 >= 3 && m2 <= lay.m + lay.h && (!lay.fixed || m2 == lay.m)) {
+      Layout l2 = lay;
+      l2.m = m2;
+      l2.h = lay.m + lay.h - m2;
+      if (make_plan(A, n, kWalkSeg, false, l2, P, &c) == SUP_OK) return SUP_OK;
+    }
+  }
+  int rc = make_plan(A, n, kWalkSeg, false, lay, P);
+  if (rc) return rc;
+  if (!lay.fixed) {
+    const int mmax = std::min(lay.m + lay.h - 15, 31);
+    int m2 = lay.m;
+    while (m2 < mmax && std::ldexp(walk_cost(P), m2) < 32.0 * kSegStartOps) ++m2;
+    if (m2 != lay.m) {
+      Layout l2 = lay;
+      l2.m = m2;
+      l2.h = lay.m + lay.h - m2;
+      Plan s2;
+      if (make_plan(A, n, kWalkSeg, false, l2, s2) == SUP_OK) {
+        auto eff = [](const Plan& q) {
+          return (1.0 - q.seg_skip) * (walk_cost(q) + std::ldexp(kSegStartOps, -q.lay.m));
+        };
+        if (eff(s2) < eff(P)) P = std::move(s2);
+      }
+    }
+  }
+  SegChoice c;
+  c.order = P.seg_order;
+  c.b = P.seg_b;
+  c.budget = P.seg_budget;
+  seg_choice_store(dkey, P.lay.m, c);
   return SUP_OK;
 }
 
@@ -334,9 +388,10 @@ struct PlanKey {
   int n, kernel, L, m, jit, ndev;
   bool fixed;      // walk length asked for (sup_opts::walk_log2): make_seg_plan keeps it
   uint64_t knobs;  // SUP_JIT_* experiment settings the planner and code generator read
+  bool warm;       // auto mode: this matrix's segmented-walk choices are in the disk cache
   bool operator<(const PlanKey& o) const {
-    return std::tie(hash, n, kernel, L, m, jit, ndev, fixed, knobs) <
-           std::tie(o.hash, o.n, o.kernel, o.L, o.m, o.jit, o.ndev, o.fixed, o.knobs);
+    return std::tie(hash, n, kernel, L, m, jit, ndev, fixed, knobs, warm) <
+           std::tie(o.hash, o.n, o.kernel, o.L, o.m, o.jit, o.ndev, o.fixed, o.knobs, o.warm);
   }
 };
 std::mutex g_plan_mu;
@@ -360,6 +415,8 @@ uint64_t knob_hash() {
 }
 }  // namespace
 
+static uint64_t knob_hash_env() { return knob_hash(); }
+
 int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit, int ndev, int dev) {
   const size_t nn = (size_t)n * n;
   uint64_t h = 1469598103934665603ull;
@@ -369,7 +426,10 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
     h = (h ^ b) * 1099511628211ull;
   }
   // ndev only feeds auto mode's compile-or-not decision
-  const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0, lay.fixed, knob_hash()};
+  // auto mode at sizes where specialising can pay: whether an earlier process
+  // recorded this matrix's choices decides the bar (plan_for_uncached)
+  const bool warm = jit == 0 && n >= kJitWarmMinN && seg_choice_exists(seg_disk_key(A, n, lay));
+  const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0, lay.fixed, knob_hash(), warm};
   {
     std::lock_guard<std::mutex> g(g_plan_mu);
     auto it = g_plans.find(key);
@@ -420,6 +480,11 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
   // candidates in preference order; the cheapest by walk_cost wins
   std::vector<WalkKind> kinds;
   auto make_seg = [&](Plan& s) { return make_seg_plan(A, n, lay, s); };
+  // auto mode's bar for specialising: the predicted walk time saved must
+  // exceed the planning + compile it costs — seconds cold, ~0 when an earlier
+  // process left this matrix's plan choices and kernel in the disk cache
+  double min_saving = kJitMinSavingSec;
+  if (jit == 0 && n >= kJitWarmMinN && seg_choice_exists(seg_disk_key(A, n, lay))) min_saving = kJitWarmSavingSec;
   switch (kernel) {
     case SUP_KERNEL_SKIPPER: {
       // SkipPer only gains where some x_j(S) is exactly zero.  With a
@@ -436,18 +501,18 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
       double skip_cost = walk_cost(P) / (integral ? kSkipEfficiency : 1.0);  // f <= 1
       // auto mode: no segmented plan (its search takes ~0.1-1 s) where even a
       // free walk could not save the compile
-      if (jit < 1 && steps * skip_cost / kLaneOpsPerSec < kJitMinSavingSec) return SUP_OK;
+      if (jit < 1 && steps * skip_cost / kLaneOpsPerSec < min_saving) return SUP_OK;
       Plan s;
       if (make_seg(s) != SUP_OK) return SUP_OK;
       if (walk_cost_eff(s) >= skip_cost) return SUP_OK;
-      if (jit < 1 && steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec < kJitMinSavingSec) return SUP_OK;
+      if (jit < 1 && steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec < min_saving) return SUP_OK;
       if (integral) {
         const double f = skip_visited_fraction(P, dev);
         if (f < 0.0) return SUP_OK;
         skip_cost *= f;
       }
       const double saved = steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec;
-      if (walk_cost_eff(s) < skip_cost && (jit >= 1 || saved >= kJitMinSavingSec)) P = std::move(s);
+      if (walk_cost_eff(s) < skip_cost && (jit >= 1 || saved >= min_saving)) P = std::move(s);
       return SUP_OK;
     }
     case SUP_KERNEL_DENSE_PLAIN: return make_plan(A, n, kWalkDense, false, lay, P);
@@ -474,13 +539,13 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
     if (make_plan(A, n, kinds[i], false, lay, c) == SUP_OK && walk_cost(c) < walk_cost(best)) best = std::move(c);
   }
   const bool may_save = std::ldexp(1.0, n - 1) / std::max(ndev, 1) * walk_cost(best) / kLaneOpsPerSec >=
-                        kJitMinSavingSec;  // auto mode: skip the segmented plan's search where it cannot pay
+                        min_saving;  // auto mode: skip the segmented plan's search where it cannot pay
   if (jit >= 0 && n >= 8 && lay.m >= 3 && (jit >= 1 || may_save)) {
     Plan s;
     if (make_seg(s) == SUP_OK && walk_cost_eff(s) < walk_cost(best)) {
       const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
       const double saved = steps * (walk_cost(best) - walk_cost_eff(s)) / kLaneOpsPerSec;
-      if (jit >= 1 || saved >= kJitMinSavingSec) best = std::move(s);
+      if (jit >= 1 || saved >= min_saving) best = std::move(s);
     }
   }
   P = std::move(best);

@@ -105,12 +105,26 @@ struct Plan {
   uint64_t jit_key = 0;            // hash of jit_src + compile options
   uint64_t uid = 0;                // plan-cache identity (0: uncached); a device that holds
                                    // this plan's tables skips their upload (run_range)
+  std::vector<int> seg_order;      // segmented walk: the m walk + L lane columns its search chose
+};
+
+// The choices a segmented-walk plan is rebuilt from without searching: walk +
+// lane column order, specialised pair bits, live-value budget (persisted on
+// disk by make_seg_plan, so a later process skips the walk-order search and
+// the compiler check).
+struct SegChoice {
+  std::vector<int> order;
+  int b = 0;
+  int budget = 0;
 };
 
 // Build a plan.  identity_map keeps engine bit e = column e (needed when a
 // chunk range must match reference Gray indices: sup_partial); otherwise the
 // SpaRyser walk takes its walk columns in greedy_walk_order.
-int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const Layout& lay, Plan& P);
+// `choice` (segmented walk only): rebuild from recorded choices instead of
+// searching (SegChoice).
+int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const Layout& lay, Plan& P,
+              const SegChoice* choice = nullptr);
 
 // Walk-column order minimising the prefix-block cost (first `count` columns).
 std::vector<int> greedy_walk_order(const double* A, int n, int count);
@@ -132,7 +146,16 @@ double seg_skip_fraction_plan(const Plan& P, int samples);
 std::vector<int> seg_row_order(const double* A, int n, const std::vector<int>& walk);
 // Fill the segment structure, packed table and generated source of a plan
 // whose rows are already in first-touch order (make_plan, kind kWalkSeg).
-int build_seg(Plan& P);
+// fixed_budget > 0: fit the storage plan to that live-value budget, no
+// compiler check (a recorded choice).
+int build_seg(Plan& P, int fixed_budget = 0);
+// Disk cache of segmented-walk choices (next to the code objects): key ->
+// (walk bits m, SegChoice).  jit_toolchain_hash() covers what the choices
+// were priced with (generated-code headers, compile options, hiprtc).
+bool seg_choice_load(uint64_t key, int* m, SegChoice* c);
+bool seg_choice_exists(uint64_t key);
+void seg_choice_store(uint64_t key, int m, const SegChoice& c);
+uint64_t jit_toolchain_hash();
 // Default specialised pair bits, min(m - 1, 5) (the walk loop is unrolled by
 // 2^b pair steps; walk bits > b share one straight-line step).  Plans choose
 // b in 5..8 by the op count (seg_walk_order / build_seg).

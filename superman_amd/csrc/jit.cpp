@@ -1489,6 +1489,14 @@ std::string hiprtc_version() {
   return "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + " hip " + std::to_string(HIP_VERSION);
 }
 
+uint64_t toolchain_hash_impl() {
+  std::string key;
+  for (const std::string& opt : jit_opts()) key += "\n//" + opt;
+  key += std::string("\n//") + kWalkCommonSrc + kWalkParamsSrc;
+  key += "\n//" + hiprtc_version();
+  return fnv1a(key);
+}
+
 // Code-object key of a generated source: the source, the compile options, the
 // embedded headers and the compiler's version.
 uint64_t jit_source_key(const std::string& src) {
@@ -1501,7 +1509,7 @@ uint64_t jit_source_key(const std::string& src) {
 
 }  // namespace
 
-int build_seg(Plan& P) {
+int build_seg(Plan& P, int fixed_budget) {
   const int n = P.n, L = P.lay.L, m = P.lay.m;
   if (m < 3) {
     set_error("segmented walk needs >= 3 walk bits");
@@ -1622,9 +1630,11 @@ int build_seg(Plan& P) {
     Q.jit_key = jit_source_key(Q.jit_src);
     (void)n;
   };
-  // SUP_JIT_BUDGET (experiments): this budget, no compiler check
-  const char* fixed_budget = std::getenv("SUP_JIT_BUDGET");
-  finish(P, fixed_budget ? std::max(1, std::atoi(fixed_budget)) : kRegsMax);
+  // SUP_JIT_BUDGET (experiments) or a recorded choice: this budget, no
+  // compiler check
+  const char* env_budget = std::getenv("SUP_JIT_BUDGET");
+  if (env_budget) fixed_budget = std::max(1, std::atoi(env_budget));
+  finish(P, fixed_budget > 0 ? fixed_budget : kRegsMax);
   // The live-value budget against the compiler (walks of 10 ms or more).  The
   // estimate is rough: on the n = 40 bench matrix budgets up to 192 compile
   // without a spill, 194-216 spill 5-13 VGPRs, 218+ 17-27; denser or larger
@@ -1639,7 +1649,7 @@ int build_seg(Plan& P) {
   // inside the walk loop, or hiprtc's register allocator gives up (some dense
   // n >= 46 patterns), there is no segmented plan and the engine runs the
   // ahead-of-time walk.
-  const bool fixed = fixed_budget || std::getenv("SUP_JIT_REGMAX") || std::getenv("SUP_JIT_STORAGE") ||
+  const bool fixed = fixed_budget > 0 || std::getenv("SUP_JIT_REGMAX") || std::getenv("SUP_JIT_STORAGE") ||
                      std::getenv("SUP_JIT_CC") || std::getenv("SUP_JIT_NOVERIFY");
   const double walk_s = std::ldexp(1.0, n - 1) * P.seg_ops / 3.7e13;
   if (!fixed && walk_s >= 0.01 && P.seg_regs > kRegs3) {
@@ -1950,5 +1960,46 @@ int jit_launch(int dev, const Plan& P, const WalkParams& p, int grid, hipStream_
 }
 
 double jit_compile_ms_thread() { return t_compile_ms; }
+
+uint64_t jit_toolchain_hash() {
+  static const uint64_t h = toolchain_hash_impl();
+  return h;
+}
+
+// Recorded segmented-walk choices: a small text file next to the code objects,
+// "supseg 2 <m> <b> <budget> <count> <order...>".
+bool seg_choice_load(uint64_t key, int* m, SegChoice* c) {
+  const std::string dir = cache_dir();
+  if (dir.empty()) return false;
+  std::vector<char> buf;
+  if (!read_file(dir + "/plan_" + key_hex(key) + ".txt", buf)) return false;
+  buf.push_back('\0');
+  std::istringstream in(buf.data());
+  std::string tag;
+  int ver = 0, cnt = 0;
+  if (!(in >> tag >> ver >> *m >> c->b >> c->budget >> cnt) || tag != "supseg" || ver != 2 || cnt < 1 || cnt > 64)
+    return false;
+  c->order.resize(cnt);
+  for (int& v : c->order)
+    if (!(in >> v) || v < 0 || v > 63) return false;
+  return true;
+}
+
+bool seg_choice_exists(uint64_t key) {
+  const std::string dir = cache_dir();
+  struct stat sb;
+  return !dir.empty() && ::stat((dir + "/plan_" + key_hex(key) + ".txt").c_str(), &sb) == 0;
+}
+
+void seg_choice_store(uint64_t key, int m, const SegChoice& c) {
+  const std::string dir = cache_dir();
+  if (dir.empty() || c.order.empty()) return;
+  std::ostringstream o;
+  o << "supseg 2 " << m << ' ' << c.b << ' ' << c.budget << ' ' << c.order.size();
+  for (int v : c.order) o << ' ' << v;
+  o << '\n';
+  const std::string str = o.str();
+  write_file_atomic(dir, "plan_" + key_hex(key) + ".txt", std::vector<char>(str.begin(), str.end()));
+}
 
 }  // namespace sup

@@ -154,18 +154,26 @@ static void test_io_and_reductions(const std::string& root) {
   int n = 0, nnz = 0;
   CHECK(sup_read_mtx((root + "/tests/fixtures/mtx/chesapeake.mtx").c_str(), 0, &mat, &t, &n, &nnz) == SUP_OK);
   if (mat) {
-    sup_reduce_opts r;
-    sup_reduce_opts_init(&r);
-    r.compress = 1;
-    sup_opts o;
-    sup_opts_init(&o);
-    o.threads = 4;
-    char e[600];
-    CHECK(sup_perman_reduced_exact(mat, t, n, &o, 1, &r, e, sizeof e, nullptr) == SUP_OK);
-    CHECK(std::strcmp(e, "13173481190272") == 0);
     int cnt = 0;
     CHECK(sup_count_nnz(mat, t, n, &cnt) == SUP_OK);
     sup_free(mat);
+  }
+  {
+    // -o reductions down to small leaves (min_n 12), exact leaves on host
+    // threads, against the direct exact walk of the same matrix
+    const int m = 24;
+    std::vector<double> R = random_matrix(m, 0.15, 11, true);
+    sup_reduce_opts r;
+    sup_reduce_opts_init(&r);
+    r.compress = 1;
+    r.min_n = 12;
+    sup_opts o;
+    sup_opts_init(&o);
+    o.threads = 4;
+    char red[600], dir[600];
+    CHECK(sup_perman_reduced_exact(R.data(), SUP_FLOAT64, m, &o, 1, &r, red, sizeof red, nullptr) == SUP_OK);
+    CHECK(sup_perman_exact(R.data(), SUP_FLOAT64, m, &o, 1, dir, sizeof dir, nullptr) == SUP_OK);
+    CHECK(std::strcmp(red, dir) == 0);
   }
   std::vector<double> A = random_matrix(24, 0.3, 5, false);
   int cnt = 0;

@@ -48,14 +48,21 @@ def test_cpu_seg_corpus_vs_sparse(sup, orc):
     assert rel(got, sup.perman_cpu(b, "sparse", threads=8)) < 1e-12
 
 
-def test_planner_choice(sup):
+def test_planner_choice(sup, tmp_path, monkeypatch):
+    monkeypatch.setenv("SUP_JIT_CACHE_DIR", str(tmp_path))  # cold: nothing recorded yet
     a, _, _ = sup.read_matrix(fixture_path("double__40_0.50_0"))
     assert sup.plan_info(a, "dense", jit=-1)["kind"] == "sparse"
-    assert sup.plan_info(a, "dense", jit=1)["kind"] == "seg"
-    # auto: the n = 40 walk saves ~0.5 s on one GPU, below the 3 s plan + compile
-    # threshold (a one-shot call is faster on the prefix walk); n = 44 saves seconds
+    # auto, cold: the n = 40 walk saves ~0.5 s on one GPU, below the 3 s plan +
+    # compile threshold (a one-shot call is faster on the prefix walk); n = 44
+    # saves seconds
     assert sup.plan_info(a, "dense", jit=0)["kind"] == "sparse"
     assert sup.plan_info(a, "dense", jit=0, gpu_num=8)["kind"] == "sparse"
+    assert sup.plan_info(a, "dense", jit=1)["kind"] == "seg"
+    # warm: the jit = 1 plan left its choices (and kernel) in the disk cache,
+    # rebuilding costs ~ms, so auto mode now takes the segmented walk
+    assert any(p.name.startswith("plan_") for p in tmp_path.iterdir())
+    assert sup.plan_info(a, "dense", jit=0)["kind"] == "seg"
+    assert sup.plan_key(a, "dense", jit=0) == sup.plan_key(a, "dense", jit=1)
     c, _, _ = sup.read_matrix(fixture_path("double__32_0.50_0"))
     assert sup.plan_info(c, "dense", jit=0)["kind"] == "sparse"  # 2^31 steps: ms saved
     b, _, _ = sup.read_matrix(fixture_path("synth44_0.15_int"))
