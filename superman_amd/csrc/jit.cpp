@@ -408,6 +408,13 @@ SegFit seg_fit(const SegRows& R, int cc, int budget, int budget_hi = -1, SegFit*
 // Best number of cached classes (0 .. min(kMaxCachedBits, b-1)) within the
 // register budget.
 std::atomic<long> g_fit_calls{0};  // planning effort (SUP_JIT_VERBOSE)
+// Live-value budget the walk-order search prices orders at (SUP_JIT_SEARCH_BUDGET
+// for experiments; the compiler check then refits the chosen order).
+int search_budget() {
+  static const int b = std::getenv("SUP_JIT_SEARCH_BUDGET") ? std::atoi(std::getenv("SUP_JIT_SEARCH_BUDGET")) : kRegsMax;
+  return b;
+}
+
 SegFit seg_best(const SegRows& R, int cc_max = kMaxCachedBits, int regs_max = kRegsMax) {
   ++g_fit_calls;
   SegFit best;
@@ -555,7 +562,8 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
   auto cost = [&](const std::vector<int>& o, int b) {
     if (nnz[o[0]] == 0) return 1e300;
     if (m < 3) return 0.0;
-    const SegFit f = seg_best(seg_rows_of(A, n, std::vector<int>(o.begin(), o.begin() + m), b));
+    const SegFit f = seg_best(seg_rows_of(A, n, std::vector<int>(o.begin(), o.begin() + m), b), kMaxCachedBits,
+                              search_budget());
     return seg_block_bytes(f, b) > kMaxBlockBytes ? 1e300 : seg_score(f);
   };
   if (m == 0) {
