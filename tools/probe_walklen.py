@@ -13,8 +13,10 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import superman_amd as S  # noqa: E402
 
-CASES = [("double__40_0.50_0", 0, "dense"), ("double__40_0.20_0", 0, "dense"), ("double__32_0.50_0", 0, "dense"),
-         ("double__36_0.20_0", 1, "sparse"), ("synth44_0.15_int", 2, "sparse")]
+CASES = [("double__40_0.50_0", 0, "dense"), ("double__40_0.20_0", 0, "dense"), ("double__40_0.90_0", 0, "dense"),
+         ("double__32_0.50_0", 0, "dense"), ("double__36_0.20_0", 1, "sparse"), ("synth44_0.15_int", 2, "sparse")]
+if os.environ.get("PROBE_CASES"):
+    CASES = [c for c in CASES if c[0] in os.environ["PROBE_CASES"].split(",")]
 ms = [int(v) for v in sys.argv[1:]] or [0, 11, 12, 13, 14, 15, 16]
 for name, prep, kernel in CASES:
     a, _, _ = S.read_matrix(os.path.join("tests", "fixtures", name))
