@@ -69,6 +69,36 @@ def test_walk_option_bounds(sup):
     with pytest.raises(sup.SupError) as e:
         sup.partial(a, 0, 1 << 20, walk_log2=32)
     assert e.value.code == -1
+    # sup_perman_shard and sup_plan_key validate them too (n = 60 with
+    # walk_log2 = 40 would give T = 1u << 40 in the kernels)
+    b = np.ones((60, 60))
+    for call in (lambda: sup.perman_shard(b, 0, 1, walk_log2=40), lambda: sup.plan_key(b, walk_log2=40),
+                 lambda: sup.plan_info(b, walk_log2=40), lambda: sup.prepare(b, walk_log2=40)):
+        with pytest.raises(sup.SupError) as e:
+            call()
+        assert e.value.code == -1 and "walk_log2" in str(e.value)
+
+
+def test_fixed_walk_length_is_its_own_plan(sup, tmp_path):
+    """A walk_log2 request equal to the default m is a fixed layout (the
+    segmented planner keeps it) and must not share a plan-cache slot with the
+    auto layout (which may lengthen m): after plan_info(mat), a fixed request
+    gets the plan a fresh process gets."""
+    a = sup.read_matrix(fixture_path("double__36_0.20_0"))[0]
+    a = sup.sort_order(a)[0]
+    L, m, h = sup.layout(36)
+    auto = sup.plan_info(a, "seg")
+    here = sup.plan_key(a, "seg", walk_log2=m)
+    code = ("import sys; sys.path.insert(0, {root!r}); import numpy as np, superman_amd as S; "
+            "a = np.load({p!r}); print(S.plan_key(a, 'seg', walk_log2={m}))").format(root=ROOT, p=str(tmp_path / "a.npy"),
+                                                                                      m=m)
+    np.save(tmp_path / "a.npy", a)
+    fresh = int(subprocess.run(["python3", "-c", code], capture_output=True, text=True, check=True,
+                               env=dict(os.environ, SUP_JIT_CACHE_DIR="")).stdout.split()[-1])
+    assert here == fresh
+    info = sup.plan_info(a, "seg", walk_log2=m)
+    assert info["m"] == m
+    assert auto["m"] >= m  # the auto layout lengthens cheap walks (config 3: m 14)
 
 
 def test_partial_range_validation(sup):
