@@ -722,6 +722,8 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   // stores, 2.5x the partials' bytes in WRITE_SIZE)
   unsigned group = 64;
   while (group > 1 && count / ((uint64_t)group * res_waves) < 32) group >>= 1;
+  if (const char* e = std::getenv("SUP_WALK_GROUP"))  // experiments: force the chunk group (power of two <= 64)
+    group = std::max(1u, std::min(64u, 1u << (31 - __builtin_clz((unsigned)std::max(1, std::atoi(e))))));
   const uint64_t waves_needed = (count + group - 1) / group;  // one chunk group per wave at a time
   uint64_t grid = (waves_needed + wpb - 1) / wpb;
   if (grid > resident) grid = resident;

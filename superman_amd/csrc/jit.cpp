@@ -1481,6 +1481,8 @@ std::vector<std::string> jit_opts() {
   std::vector<std::string> v(kJitOpts, kJitOpts + kJitNopts);
   if (const char* e = std::getenv("SUP_JIT_SCHED"))
     if (*e) v.push_back("-mllvm"), v.push_back(std::string("-amdgpu-sched-strategy=") + e);
+  if (const char* e = std::getenv("SUP_JIT_OPAQUE_R2"))
+    if (std::atoi(e)) v.push_back("-DSUP_OPAQUE_BEFORE_OFFSET=1");
   return v;
 }
 

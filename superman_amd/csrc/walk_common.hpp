@@ -45,9 +45,15 @@ typedef const __attribute__((address_space(4))) int cint;
 // was hoisted: one SGPR pair per constant, live for the whole kernel), and a
 // constant offset folds into the s_load immediate.
 __device__ __forceinline__ cdbl* opaque_c(const double* base, uint32_t byte_off) {
+#ifdef SUP_OPAQUE_BEFORE_OFFSET  // the round-2 form (experiments: SUP_JIT_OPAQUE_R2=1)
+  uint64_t a = (uint64_t)base + byte_off;
+  asm volatile("" : "+s"(a));
+  return (cdbl*)a;
+#else
   uint64_t a = (uint64_t)base;
   asm volatile("" : "+s"(a));
   return (cdbl*)(a + byte_off);
+#endif
 }
 __device__ __forceinline__ cint* opaque_i(const int* base, uint32_t byte_off) {
   uint64_t a = (uint64_t)base;
