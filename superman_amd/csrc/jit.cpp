@@ -1351,9 +1351,16 @@ struct Gen {
     o << "  __shared__ double s_keep[" << kBlock / 64 << "][64];\n";
     o << "  __shared__ uint32_t s_vkeep[" << kBlock / 64 << "][64];\n";
     o << "  const uint32_t wv = threadIdx.x >> 6;\n";
-    o << "  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {\n";
-    o << "    for (uint32_t j = 0; j < (uint32_t)p.group; ++j) {\n";
-    o << "      const uint64_t a = (uint64_t)g * p.group + j;\n";
+    // ticket t -> chunks [base, base + len): groups of p.group, then (from
+    // p.tail_begin) groups of p.tail_group
+    o << "  const uint32_t main_tickets = p.tail_group ? (uint32_t)(p.tail_begin / p.group) : 0xffffffffu;\n";
+    o << "  for (uint32_t t = next_chunk(p.counter);; t = next_chunk(p.counter)) {\n";
+    o << "    const uint64_t base = t < main_tickets ? (uint64_t)t * p.group\n";
+    o << "                                           : p.tail_begin + (uint64_t)(t - main_tickets) * p.tail_group;\n";
+    o << "    const uint32_t len = t < main_tickets ? p.group : p.tail_group;\n";
+    o << "    if (base >= p.chunk_count) break;\n";
+    o << "    for (uint32_t j = 0; j < len; ++j) {\n";
+    o << "      const uint64_t a = base + j;\n";
     o << "      if (a >= p.chunk_count) break;\n";
     o << "      const uint64_t ga = p.chunk_begin + a;\n";
     o << "      double x[N], y[" << len0 << "];\n";
@@ -1459,8 +1466,8 @@ struct Gen {
     o << "    __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n";
     o << "    __builtin_amdgcn_wave_barrier();\n";
     o << "    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n";
-    o << "    const uint64_t a = (uint64_t)g * p.group + lane;\n";
-    o << "    if (lane < (uint32_t)p.group && a < p.chunk_count) {\n";
+    o << "    const uint64_t a = base + lane;\n";
+    o << "    if (lane < len && a < p.chunk_count) {\n";
     o << "      p.chunk_out[a] = s_keep[wv][lane];\n";
     o << "      if (p.visited) p.visited[a] = s_vkeep[wv][lane];\n";
     o << "    }\n";

@@ -40,7 +40,12 @@ struct WalkParams {
   // The host picks the largest group that still leaves >= 32 groups per
   // resident wave (tail balance beats write coalescing).
   unsigned int group;
-  unsigned int pad2_;
+  // segmented walk: the queue's tail phase.  Tickets below tail_begin / group
+  // hand out `group` chunks each; the chunks from tail_begin on go out in
+  // groups of tail_group (< group), so the waves finish within a smaller group
+  // of each other (tail_group 0: no tail phase).
+  unsigned int tail_group;
+  unsigned long long tail_begin;
   // segmented walk (jit.cpp): per walk bit, the values of the rows its column
   // touches, packed (+ block, then - block, each padded to 8 doubles)
   const double* jtab;
