@@ -321,17 +321,33 @@ static constexpr double kSegStartOps = 2048.0;
 // GPU count sums the same chunks (bit-identical results).
 static uint64_t knob_hash_env();
 
-// Disk key of a segmented-walk plan: matrix, layout request, experiment knobs
-// and the toolchain the choices were priced with.
+// Disk key of a segmented-walk plan: what its choices depend on, the layout
+// request, experiment knobs and the toolchain the choices were priced with.
+// For a non-integer matrix the choices (walk-order search, trees, budget, the
+// generated source) depend on the zero pattern only, so the key is the
+// pattern: matrices that differ only in their nonzero values (a rescaled row,
+// another draw of the same pattern) share one record and one kernel.  Integer
+// matrices add their values (the chunk-skip estimate and the column order of
+// the chunk bits look at exact zeros of row sums).
 static uint64_t seg_disk_key(const double* A, int n, const Layout& lay) {
   uint64_t h = 0x5eed5e9a11ull ^ jit_toolchain_hash();
   auto mix = [&h](const void* p, size_t bytes) {
     const unsigned char* c = (const unsigned char*)p;
     for (size_t i = 0; i < bytes; ++i) h = (h ^ c[i]) * 1099511628211ull;
   };
-  const int32_t head[] = {2 /* format */, n, lay.L, lay.m, (int32_t)lay.fixed};
+  const size_t nn = (size_t)n * n;
+  bool integral = true;
+  for (size_t i = 0; i < nn && integral; ++i) integral = A[i] == std::floor(A[i]);
+  const int32_t head[] = {3 /* format */, n, lay.L, lay.m, (int32_t)lay.fixed, (int32_t)integral};
   mix(head, sizeof head);
-  mix(A, (size_t)n * n * sizeof(double));
+  if (integral) {
+    mix(A, nn * sizeof(double));
+  } else {
+    std::vector<unsigned char> pat((nn + 7) / 8, 0);
+    for (size_t i = 0; i < nn; ++i)
+      if (A[i] != 0.0) pat[i / 8] |= (unsigned char)(1u << (i % 8));
+    mix(pat.data(), pat.size());
+  }
   const uint64_t k = knob_hash_env();
   mix(&k, sizeof k);
   return h;
