@@ -776,6 +776,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   p.group = group;
   p.tail_group = tail_group;
   p.tail_begin = tail_begin;
+  p.tail_ticket = tail_group ? (unsigned)(tail_begin / group) : 0xffffffffu;
   p.jtab = seg ? c->d_jtab : nullptr;
   p.nb_lo = p.nb_hi = 0;
   for (int k = 0; k < P.lay.m && k < 32; ++k) {

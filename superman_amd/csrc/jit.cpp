@@ -1353,11 +1353,13 @@ struct Gen {
     o << "  const uint32_t wv = threadIdx.x >> 6;\n";
     // ticket t -> chunks [base, base + len): groups of p.group, then (from
     // p.tail_begin) groups of p.tail_group
-    o << "  const uint32_t main_tickets = p.tail_group ? (uint32_t)(p.tail_begin / p.group) : 0xffffffffu;\n";
+    // (p.tail_ticket = p.tail_begin / p.group from the host: all of it
+    // wave-uniform scalar arithmetic)
     o << "  for (uint32_t t = next_chunk(p.counter);; t = next_chunk(p.counter)) {\n";
-    o << "    const uint64_t base = t < main_tickets ? (uint64_t)t * p.group\n";
-    o << "                                           : p.tail_begin + (uint64_t)(t - main_tickets) * p.tail_group;\n";
-    o << "    const uint32_t len = t < main_tickets ? p.group : p.tail_group;\n";
+    o << "    const bool head = t < p.tail_ticket;\n";
+    o << "    const uint64_t base = head ? (uint64_t)t * p.group\n";
+    o << "                               : p.tail_begin + (uint64_t)(t - p.tail_ticket) * p.tail_group;\n";
+    o << "    const uint32_t len = head ? p.group : p.tail_group;\n";
     o << "    if (base >= p.chunk_count) break;\n";
     o << "    for (uint32_t j = 0; j < len; ++j) {\n";
     o << "      const uint64_t a = base + j;\n";

@@ -45,6 +45,8 @@ struct WalkParams {
   // groups of tail_group (< group), so the waves finish within a smaller group
   // of each other (tail_group 0: no tail phase).
   unsigned int tail_group;
+  unsigned int tail_ticket;        // = tail_begin / group (0xffffffff: no tail phase)
+  unsigned int pad3_;
   unsigned long long tail_begin;
   // segmented walk (jit.cpp): per walk bit, the values of the rows its column
   // touches, packed (+ block, then - block, each padded to 8 doubles)
