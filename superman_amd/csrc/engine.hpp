@@ -91,6 +91,7 @@ struct Plan {
   ProdTree outer_tree;             // rows outside segment 0 (over x)
   ProdTree inner_tree;             // segment 0's rows (once over x, once over y)
   bool lds = false;                // kWalkDense run by the LDS-staged kernel (walk_lds.hip; same bits)
+  bool integral = false;           // every entry an integer (the segmented walk may then skip chunks)
   int seg_cc = 0;                  // cached step classes: walk bits 1..seg_cc held in every state
   double seg_ops = 0.0;            // fp64 VALU ops per Gray step of the generated kernel
   double seg_skip = 0.0;           // sampled fraction of wave-chunks the kernel skips (integer matrices)

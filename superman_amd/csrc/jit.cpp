@@ -1337,9 +1337,10 @@ struct Gen {
     o << "extern \"C\" __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(" << waves
       << "))) void sup_walk_seg(WalkParams p) {\n";
     o << "  constexpr int N = " << n << ";\n";
-    o << "  const uint32_t lane = threadIdx.x & 63u;\n";
-    o << "  const bool lane_valid = lane < " << (1u << L) << "u;\n";
-    o << "  const uint32_t lane_par = __builtin_popcount(lane) & 1u;\n";
+    // The lane id is re-read (v_mbcnt, asm volatile: not hoisted) where a
+    // chunk starts and where it ends, instead of one value live across the
+    // walk loop; the wave's slot in the block is an SGPR.
+    o << "#define SUP_LANE() ({ uint32_t l_; asm volatile(\"v_mbcnt_lo_u32_b32 %0, -1, 0\\n\\tv_mbcnt_hi_u32_b32 %0, -1, %0\" : \"=v\"(l_)); l_; })\n";
     // experiment (SUP_JIT_PHASE=k): odd workgroups start 64 k cycles late, so
     // the two waves sharing a SIMD (one per workgroup) are out of phase
     if (const char* e = std::getenv("SUP_JIT_PHASE"))
@@ -1350,12 +1351,16 @@ struct Gen {
     // loop (LDS is otherwise unused; 3 KB per block).
     o << "  __shared__ double s_keep[" << kBlock / 64 << "][64];\n";
     o << "  __shared__ uint32_t s_vkeep[" << kBlock / 64 << "][64];\n";
-    o << "  const uint32_t wv = threadIdx.x >> 6;\n";
+    o << "  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n";
     // ticket t -> chunks [base, base + len): groups of p.group, then (from
     // p.tail_begin) groups of p.tail_group
     // (p.tail_ticket = p.tail_begin / p.group from the host: all of it
     // wave-uniform scalar arithmetic)
-    o << "  for (uint32_t t = next_chunk(p.counter);; t = next_chunk(p.counter)) {\n";
+    // tickets below p.static_tickets are dealt out statically (wave w of W:
+    // w, w + W, ...), the rest come from the atomic counter
+    o << "  const uint32_t nw = gridDim.x * " << kBlock / 64 << "u, gw = blockIdx.x * " << kBlock / 64 << "u + wv;\n";
+    o << "  for (uint32_t t = gw < p.static_tickets ? gw : p.static_tickets + next_chunk(p.counter);;\n";
+    o << "       t = t + nw < p.static_tickets ? t + nw : p.static_tickets + next_chunk(p.counter)) {\n";
     o << "    const bool head = t < p.tail_ticket;\n";
     o << "    const uint64_t base = head ? (uint64_t)t * p.group\n";
     o << "                               : p.tail_begin + (uint64_t)(t - p.tail_ticket) * p.tail_group;\n";
@@ -1366,7 +1371,7 @@ struct Gen {
     o << "      if (a >= p.chunk_count) break;\n";
     o << "      const uint64_t ga = p.chunk_begin + a;\n";
     o << "      double x[N], y[" << len0 << "];\n";
-    o << "      chunk_start<N>(x, p, ga, lane);\n";
+    o << "      chunk_start<N>(x, p, ga, SUP_LANE());\n";
     o << "      {\n";  // y = x + a_0 on segment 0 (the + block of walk bit 0) = y^0
     o << "        cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off_const(0, 0) << ");\n";
     for (int r = 0; r < len0; ++r) o << "        y[" << r << "] = x[" << r << "] + cv[" << r / 8 << "][" << r % 8 << "];\n";
@@ -1398,7 +1403,7 @@ struct Gen {
     o << "      double acc = 0.0;\n";
     o << "      uint32_t vis = 0;\n";
     if (P.outer_tree.tail_hi > P.outer_tree.tail_lo)
-      o << "      if (__builtin_amdgcn_ballot_w64(lane_valid && Ro != 0.0) != 0) {\n";
+      o << "      if (__builtin_amdgcn_ballot_w64(SUP_LANE() < " << (1u << L) << "u && Ro != 0.0) != 0) {\n";
     else
       o << "      {\n";
     o << "      vis = " << (1u << m) << "u;\n";
@@ -1460,14 +1465,16 @@ struct Gen {
     }
     o << "      }\n";
     o << "      acc = tot + acc;\n";
-    o << "      if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;\n";
+    o << "      if (((uint32_t)ga ^ (uint32_t)__builtin_popcount(SUP_LANE())) & 1u) acc = -acc;\n";
     o << "      }\n";
-    o << "      const double part = wave_sum(lane_valid ? acc : 0.0);\n";
+    o << "      const uint32_t lane = SUP_LANE();\n";
+    o << "      const double part = wave_sum(lane < " << (1u << L) << "u ? acc : 0.0);\n";
     o << "      if (lane == j) s_keep[wv][j] = part, s_vkeep[wv][j] = vis;\n";
     o << "    }\n";
     o << "    __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n";
     o << "    __builtin_amdgcn_wave_barrier();\n";
     o << "    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n";
+    o << "    const uint32_t lane = SUP_LANE();\n";
     o << "    const uint64_t a = base + lane;\n";
     o << "    if (lane < len && a < p.chunk_count) {\n";
     o << "      p.chunk_out[a] = s_keep[wv][lane];\n";
