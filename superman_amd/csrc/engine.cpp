@@ -749,8 +749,8 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   // tail phase holds ~2 groups per resident wave, rounded to whole groups.
   unsigned tail_group = 0;
   uint64_t tail_begin = count;
-  if (seg && group >= 4) {
-    tail_group = group / 4;
+  if (seg && group >= 2) {
+    tail_group = std::max(1u, group / 4);
     if (const char* e = std::getenv("SUP_WALK_TAIL"))  // experiments: tail group (0 = no tail phase)
       tail_group = std::min(group, (unsigned)std::max(0, std::atoi(e)));
     const uint64_t tail = 2 * res_waves * group;
