@@ -7,4 +7,5 @@ bash tools/gpu_session.sh r3i \
  "pmc_fetch_d050=$P --pmc FETCH_SIZE -d gpurun_out/r3i/pmc_fetch_d050 -- $B1" \
  "pmc_write_d050=$P --pmc WRITE_SIZE -d gpurun_out/r3i/pmc_write_d050 -- $B1" \
  "pmc_tcc_d050=$P --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_ATOMIC_sum TCC_ATOMIC_sum -d gpurun_out/r3i/pmc_tcc_d050 -- $B1" \
+ "shards=python3 -u tools/probe_shards.py" \
  "bench=python3 bench.py"
