@@ -779,19 +779,6 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   p.tail_group = tail_group;
   p.tail_begin = tail_begin;
   p.tail_ticket = tail_group ? (unsigned)(tail_begin / group) : 0xffffffffu;
-  // Segmented walk with uniform work per chunk (no chunk can be skipped: a
-  // non-integer matrix, or no walk-untouched rows): the head of the queue is
-  // dealt out statically, wave w taking tickets w, w + W, ... (every launched
-  // wave is resident: grid <= resident blocks), and only the last round of
-  // full groups and the tail phase go through the atomic counter — one queue
-  // atomic per wave and round instead of per group (each is a 32-byte
-  // memory-side request on a multi-XCD part).
-  p.static_tickets = 0;
-  if (seg && (!P.integral || P.outer_tree.tail_hi <= P.outer_tree.tail_lo) && !std::getenv("SUP_WALK_NOSTATIC")) {
-    const uint64_t W = grid * wpb;
-    const uint64_t head = tail_group ? tail_begin / group : (count + group - 1) / group;
-    if (head >= 2 * W) p.static_tickets = (unsigned)((head / W - 1) * W);
-  }
   p.jtab = seg ? c->d_jtab : nullptr;
   p.nb_lo = p.nb_hi = 0;
   for (int k = 0; k < P.lay.m && k < 32; ++k) {

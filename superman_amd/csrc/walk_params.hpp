@@ -46,8 +46,7 @@ struct WalkParams {
   // of each other (tail_group 0: no tail phase).
   unsigned int tail_group;
   unsigned int tail_ticket;        // = tail_begin / group (0xffffffff: no tail phase)
-  unsigned int static_tickets;     // segmented walk: tickets [0, static_tickets) dealt out
-                                   // statically (wave w: w, w + W, ...), the rest from counter
+  unsigned int pad3_;
   unsigned long long tail_begin;
   // segmented walk (jit.cpp): per walk bit, the values of the rows its column
   // touches, packed (+ block, then - block, each padded to 8 doubles)
