@@ -35,6 +35,7 @@ namespace {
 struct Cli {
   bool generic = true, dense = true, approximation = false, gpu = false, cpu = false, grid_graph = false;
   bool rccl = false, verbose = false, compression = false, exact = false, quad = false;
+  bool half_calc = false, half_store = false;
   int gpu_num = 2, threads = 16, perman_algo = 1, preprocessing = 0, device = 0, reps = 1;
   double scaling = -1.0;
   long number_of_times = 100000;  // main.cu:338-344 defaults
@@ -125,7 +126,7 @@ int run_approx(const Cli& c) {
 
 int main(int argc, char** argv) {
   Cli c;
-  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rvou:S:J:Eq";
+  const char* const short_options = "bsr:t:f:gd:cap:x:y:z:im:n:l:k:Rvou:S:J:Eqhwe:";
   const struct option long_options[] = {{"binary", 0, NULL, 'b'},       {"sparse", 0, NULL, 's'},
                                         {"preprocessing", 1, NULL, 'r'}, {"threads", 1, NULL, 't'},
                                         {"file", 1, NULL, 'f'},          {"gpu", 0, NULL, 'g'},
@@ -139,7 +140,8 @@ int main(int argc, char** argv) {
                                         {"compression", 0, NULL, 'o'},   {"scaling", 1, NULL, 'u'},
                                         {"seed", 1, NULL, 'S'},          {"jit", 1, NULL, 'J'},
                                         {"exact", 0, NULL, 'E'},         {"quad", 0, NULL, 'q'},
-                                        {NULL, 0, NULL, 0}};
+                                        {"halfCalc", 0, NULL, 'h'},      {"halfStore", 0, NULL, 'w'},
+                                        {"gridMultip", 1, NULL, 'e'},    {NULL, 0, NULL, 0}};
   int opt;
   auto need_arg = [&](char o) -> bool {
     if (optarg[0] == '-') {
@@ -174,6 +176,17 @@ int main(int argc, char** argv) {
       case 'E': c.exact = true; break;
       case 'q': c.quad = true; break;
       case 'v': c.verbose = true; break;
+      // v2 flags (revised_perman/main.cpp:1431-1460): -w stores the matrix in
+      // single precision (the permanent of the float-rounded entries); -h asks
+      // for single-precision calculation, which this engine does not provide
+      // (float X loses every digit at n >= 30): computed in fp64,
+      // with a note; -e <multiplier> scales the reference's launch grid, which
+      // the engine sizes from the occupancy itself: accepted, no effect.  (v2's
+      // -v, quad storage, is this CLI's verbose flag: fp64 storage rounds an
+      // entry by at most 2^-53 relative, below the walk's own rounding.)
+      case 'h': c.half_calc = true; break;
+      case 'w': c.half_store = true; break;
+      case 'e': if (!need_arg('e')) return 1; break;
       case 'o': c.compression = true; break;  // revised_perman/main.cpp:1462
       case 'u':                                // main.cpp:1465 (atoi)
         if (!need_arg('u')) return 1;
@@ -196,6 +209,17 @@ int main(int argc, char** argv) {
   int n = 0, nnz = 0;
   if (sup_read_matrix(c.filename.c_str(), c.generic ? 0 : 1, &mat, &t, &n, &nnz) != SUP_OK)
     return fail("reading matrix");
+  if (c.half_store && t == SUP_FLOAT64) {  // v2 -w: single-precision storage
+    double* d = (double*)mat;
+    float* f = (float*)std::malloc(sizeof(float) * (size_t)n * n);
+    if (!f) return fail("allocating the single-precision matrix");
+    for (size_t i = 0; i < (size_t)n * n; ++i) f[i] = (float)d[i];
+    sup_free(mat);
+    mat = f;
+    t = SUP_FLOAT32;
+  }
+  if (c.half_calc)
+    std::fprintf(stderr, "perman: -h (single-precision calculation) is computed in fp64 by this engine\n");
   // main.cu:512-518 / 544-550 / 577-583: preprocessing rewrites mat (with
   // -o / -u it is applied to every leaf of the reductions instead).
   const bool reduce = c.compression || c.scaling > 0.0;

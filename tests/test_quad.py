@@ -114,3 +114,38 @@ def test_cli_quad_cpu(sup, tmp_path):
         hi, lo = [float(v) for v in [l for l in out.splitlines() if l.startswith("Permanent (double-double)")][0]
                   .split(":")[1].split()]
         assert Fraction(hi) + Fraction(lo) == e
+
+
+def test_cli_v2_precision_flags(sup, tmp_path):
+    """v2's -w (single-precision storage: the permanent of the float-rounded
+    entries), -h (single-precision calculation: computed in fp64 with a note)
+    and -e <grid multiplier> (accepted, no effect): revised_perman/main.cpp
+    :1431-1460."""
+    import os
+    import subprocess
+    rng = np.random.default_rng(11)
+    n = 14
+    a = np.where(rng.random((n, n)) < 0.5, rng.random((n, n)) + 0.1, 0.0)
+    a[np.arange(n), rng.permutation(n)] = 0.3
+    path = tmp_path / "m14"
+    nz = np.argwhere(a != 0)
+    with open(path, "w") as f:
+        f.write(f"{n} {len(nz)} double\n")
+        for i, j in nz:
+            f.write(f"{i} {j} {float(a[i, j])!r}\n")
+    exe = os.path.join(os.path.dirname(sup.__file__), "bin", "perman")
+
+    def hi_of(extra):
+        r = subprocess.run([exe, "-f", str(path), "-c", "-q", "-t", "2"] + extra, capture_output=True, text=True,
+                           check=True)
+        line = [l for l in r.stdout.splitlines() if l.startswith("Permanent (double-double)")][0]
+        return float(line.split(":")[1].split()[0]), r.stderr
+
+    full, _ = hi_of([])
+    single, _ = hi_of(["-w"])
+    hi_f, _ = sup.perman_quad(a.astype(np.float32).astype(np.float64), cpu=True, threads=2)
+    hi_d, _ = sup.perman_quad(a, cpu=True, threads=2)
+    assert full == hi_d
+    assert single == hi_f and single != full
+    same, err = hi_of(["-h", "-e", "4"])
+    assert same == full and "-h" in err
