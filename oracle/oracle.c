@@ -739,10 +739,10 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
       if (P->kind == 3) {
         /* cached walk bits 1..cc: one full state per assignment S of them,
          * its rows derived from x0 (e_derive) */
-        static __thread etv vo[8], vx[8], vy[8];
+        static __thread etv vo[16], vx[16], vy[16]; /* cc <= 4 */
         static __thread etree outer, inner;
-        static __thread double xs[8][ORC_MAXN], ys[8][ORC_MAXN];
-        double D[8];
+        static __thread double xs[16][ORC_MAXN], ys[16][ORC_MAXN];
+        double D[16];
         int NS = 1 << P->cc;
         e_seg_trees(P, &outer, &inner);
         for (int r = 0; r < n; ++r) e_derive(P, x, xs, ys, r);

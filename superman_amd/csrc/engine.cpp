@@ -191,7 +191,7 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
       order = choice->order;
       segb = choice->b;
     } else {
-      order = kind == kWalkSeg ? seg_walk_order(A, n, m, m + L, &segb) : greedy_walk_order(A, n, m + L);
+      order = kind == kWalkSeg ? seg_walk_order(A, n, m, m + L, &segb, lay.cc_cap) : greedy_walk_order(A, n, m + L);
     }
     P.seg_b = segb;
     if (kind == kWalkSeg) P.seg_order.assign(order.begin(), order.begin() + (m + L));
@@ -340,7 +340,7 @@ static uint64_t seg_disk_key(const double* A, int n, const Layout& lay) {
   const size_t nn = (size_t)n * n;
   bool integral = true;
   for (size_t i = 0; i < nn && integral; ++i) integral = A[i] == std::floor(A[i]);
-  const int32_t head[] = {3 /* format */, n, lay.L, lay.m, (int32_t)lay.fixed, (int32_t)integral};
+  const int32_t head[] = {5 /* format: bump when the planner changes */, n, lay.L, lay.m, (int32_t)lay.fixed, (int32_t)integral};
   mix(head, sizeof head);
   if (integral) {
     mix(A, nn * sizeof(double));
@@ -366,10 +366,22 @@ static int make_seg_plan(const double* A, int n, const Layout& lay, Plan& P) {
       Layout l2 = lay;
       l2.m = m2;
       l2.h = lay.m + lay.h - m2;
+      l2.cc_cap = c.cc_cap;
       if (make_plan(A, n, kWalkSeg, false, l2, P, &c) == SUP_OK) return SUP_OK;
     }
   }
-  int rc = make_plan(A, n, kWalkSeg, false, lay, P);
+  // a short walk whose 4-cached-bit kernel touches scratch in its loop
+  // (build_seg's check) is planned again with 3 cached bits
+  auto plan = [A, n](const Layout& l, Plan& Q) {
+    int r = make_plan(A, n, kWalkSeg, false, l, Q);
+    if (r == SUP_OK && Q.seg_loop_scratch && l.cc_cap > 3) {
+      Layout l3 = l;
+      l3.cc_cap = 3;
+      r = make_plan(A, n, kWalkSeg, false, l3, Q);
+    }
+    return r;
+  };
+  int rc = plan(lay, P);
   if (rc) return rc;
   if (!lay.fixed) {
     const int mmax = std::min(lay.m + lay.h - 15, 31);
@@ -380,7 +392,7 @@ static int make_seg_plan(const double* A, int n, const Layout& lay, Plan& P) {
       l2.m = m2;
       l2.h = lay.m + lay.h - m2;
       Plan s2;
-      if (make_plan(A, n, kWalkSeg, false, l2, s2) == SUP_OK) {
+      if (plan(l2, s2) == SUP_OK) {
         auto eff = [](const Plan& q) {
           return (1.0 - q.seg_skip) * (walk_cost(q) + std::ldexp(kSegStartOps, -q.lay.m));
         };
@@ -392,6 +404,7 @@ static int make_seg_plan(const double* A, int n, const Layout& lay, Plan& P) {
   c.order = P.seg_order;
   c.b = P.seg_b;
   c.budget = P.seg_budget;
+  c.cc_cap = P.lay.cc_cap;
   seg_choice_store(dkey, P.lay.m, c);
   return SUP_OK;
 }

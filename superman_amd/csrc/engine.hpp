@@ -26,6 +26,10 @@ int to_double(const void* mat, sup_dtype t, int n, std::vector<double>& out);
 // x0[j] = a[j][n-1] - rs/2, p0 = prod_j x0[j] (ascending j, starting 1.0).
 void nw_start(const double* A, int n, double* x0, double* p0);
 
+// Cached walk bits (Plan::seg_cc) at most (the host twin and the oracle size
+// their per-state arrays for 2^4 states).
+constexpr int kMaxCachedBits = 4;
+
 // Walk layout for an n x n problem (depends on n only, so results are
 // bit-reproducible across grids and device counts).
 struct Layout {
@@ -33,6 +37,7 @@ struct Layout {
   int m;          // walk bits
   int h;          // high (wave-chunk) bits = n-1-L-m
   bool fixed = false;  // m asked for by the caller (sup_opts::walk_log2): plans keep it
+  int cc_cap = kMaxCachedBits;  // segmented walk: cached walk bits at most (make_seg_plan)
   uint64_t chunks() const { return 1ull << h; }
 };
 Layout default_layout(int n);
@@ -61,9 +66,6 @@ struct ProdTree {
   int root() const { return K() ? items() + K() - 1 : (items() ? 0 : -1); }
   uint32_t root_sig() const { return K() ? sig.back() : (items() ? item_sig[0] : 0u); }
 };
-
-// Cached walk bits (Plan::seg_cc) at most.
-constexpr int kMaxCachedBits = 3;
 
 struct Plan {
   int n = 0;
@@ -107,6 +109,7 @@ struct Plan {
   uint64_t uid = 0;                // plan-cache identity (0: uncached); a device that holds
                                    // this plan's tables skips their upload (run_range)
   std::vector<int> seg_order;      // segmented walk: the m walk + L lane columns its search chose
+  bool seg_loop_scratch = false;   // build_seg's check of a short walk's kernel found scratch in its loop
 };
 
 // The choices a segmented-walk plan is rebuilt from without searching: walk +
@@ -117,6 +120,7 @@ struct SegChoice {
   std::vector<int> order;
   int b = 0;
   int budget = 0;
+  int cc_cap = kMaxCachedBits;
 };
 
 // Build a plan.  identity_map keeps engine bit e = column e (needed when a
@@ -134,7 +138,7 @@ std::vector<int> greedy_walk_order(const double* A, int n, int count);
 // Walk-column order for the segmented walk: greedy starts from every column,
 // then pairwise-swap descent on seg_cost (first `count` columns returned).
 // *b_out = the specialised pair bits the order was chosen for (seg_b).
-std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b_out);
+std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b_out, int cc_cap = kMaxCachedBits);
 // Sampled fraction of wave-chunks the segmented kernel skips (walk-untouched
 // rows exactly zero in every lane) for an extended walk order (m walk
 // columns, then the lane columns); integer matrices.

@@ -415,7 +415,15 @@ int search_budget() {
   return b;
 }
 
-SegFit seg_best(const SegRows& R, int cc_max = kMaxCachedBits, int regs_max = kRegsMax) {
+// Cap on the cached walk bits the planner tries: kMaxCachedBits, or lower with
+// SUP_JIT_MAXCC (experiments: A/B against fewer cached bits with the budget
+// check still on).
+int max_cached() {
+  const char* e = std::getenv("SUP_JIT_MAXCC");
+  return e ? std::max(0, std::min(kMaxCachedBits, std::atoi(e))) : kMaxCachedBits;
+}
+
+SegFit seg_best(const SegRows& R, int cc_max, int regs_max = kRegsMax) {
   ++g_fit_calls;
   SegFit best;
   double bscore = 1e300;
@@ -528,7 +536,8 @@ int seg_search_starts(int n) {
   return std::ldexp(1.0, n - 1) * (2.0 * n + 1.0) / 3.7e13 >= 1.0 ? 32 : 3;
 }
 
-std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b_out) {
+std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b_out, int cc_cap) {
+  cc_cap = std::min(cc_cap, max_cached());
   const int nb = n - 1;
   m = std::min(m, nb);
   count = std::min(std::max(count, m), nb);
@@ -562,7 +571,7 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
   auto cost = [&](const std::vector<int>& o, int b) {
     if (nnz[o[0]] == 0) return 1e300;
     if (m < 3) return 0.0;
-    const SegFit f = seg_best(seg_rows_of(A, n, std::vector<int>(o.begin(), o.begin() + m), b), kMaxCachedBits,
+    const SegFit f = seg_best(seg_rows_of(A, n, std::vector<int>(o.begin(), o.begin() + m), b), cc_cap,
                               search_budget());
     return seg_block_bytes(f, b) > kMaxBlockBytes ? 1e300 : seg_score(f);
   };
@@ -659,7 +668,29 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
   // the descent's best at 512 (0.176 ops per nominal step) measured 0.216.
   constexpr int kPolishSamples = 8192;
   constexpr int kPolishEvals = 48;
+  // Shard balance: make_plan puts the high columns that touch no
+  // walk-untouched row (they never change a skip) on the top chunk bits, so
+  // contiguous shards of 2, 4, 8 GPUs see the same skips only when there are
+  // at least 3 of them (min(3, high bits)).  Orders with fewer are not taken
+  // (config 5 with 16 polish starts: the best order had fewer, and 4 of 8
+  // shards walked nothing).
+  const int need_free = std::min(3, std::max(0, nb - count));
+  auto balanced = [&](const std::vector<int>& full) {
+    std::vector<char> wrow(n, 0), used(n, 0);
+    for (int k = 0; k < m; ++k)
+      for (int i = 0; i < n; ++i) wrow[i] |= A[(size_t)i * n + full[k]] != 0.0;
+    for (int c : full) used[c] = 1;
+    int free_cols = 0;
+    for (int c = 0; c < nb; ++c) {
+      if (used[c]) continue;
+      bool f = true;
+      for (int i = 0; i < n && f; ++i) f = wrow[i] || A[(size_t)i * n + c] == 0.0;
+      free_cols += f;
+    }
+    return free_cols >= need_free;
+  };
   auto polish = [&](std::vector<int>& bo, int bb, double beff) {
+    if (!balanced(extend(bo, count))) beff = 1e300;  // any balanced order improves on it
     const int npos = std::min(count, m + std::min(6, nb - m));
     std::vector<int> cur(bo.begin(), bo.begin() + npos);
     double cur_ops = cost(std::vector<int>(cur.begin(), cur.begin() + m), bb);
@@ -688,6 +719,7 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
       for (size_t t = 0; t < trials.size() && (int)t < kPolishEvals; ++t) {
         if (cur_ops * 0.85 * std::get<0>(trials[t]) >= best) break;
         const std::vector<int>& o = std::get<2>(trials[t]);
+        if (!balanced(extend(o, count))) continue;
         const double keep = 1.0 - seg_skip_estimate(A, n, extend(o, count), m, kPolishSamples);
         const double ops = std::get<1>(trials[t]) ? cur_ops : cost(std::vector<int>(o.begin(), o.begin() + m), bb);
         if (ops < 1e300 && ops * keep < best - 1e-12) best = ops * keep, bi = (int)t, bops = ops;
@@ -707,7 +739,7 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
       for (const auto& fc : finals[ci]) {
         if (fc.first >= 1e300) continue;
         const std::vector<int> full = extend(fc.second, count);
-        const double eff = fc.first * (1.0 - seg_skip_estimate(A, n, full, m, kPolishSamples));
+        const double eff = balanced(full) ? fc.first * (1.0 - seg_skip_estimate(A, n, full, m, kPolishSamples)) : 1e300;
         if (std::getenv("SUP_JIT_VERBOSE"))
           std::fprintf(stderr, "  candidate b=%d ops=%.4f skip=%.3f eff=%.4f\n", cands[ci], fc.first,
                        1.0 - eff / fc.first, eff);
@@ -716,18 +748,19 @@ std::vector<int> seg_walk_order(const double* A, int n, int m, int count, int* b
       }
     if (!bo.empty()) {
       // polish: swap descent on ops x (1 - skip) (SUP_JIT_POLISH=0 skips
-      // it) of the kPolish best distinct
-      // candidates, one host thread each; the best result wins.  The descent
-      // is local and its end varies a lot with the start: on config 5 (n = 44
-      // d = 0.15 int) the best candidates end at 0.19-0.49 ops per nominal
-      // step (best: ~87 % of the chunks skipped at ~1.5 ops per step).
+      // it) of the kPolish best distinct candidates (16; SUP_JIT_NPOLISH), one
+      // host thread each; the best result wins.  The descent is local and its
+      // end varies a lot with the start: on config 5 (n = 44 d = 0.15 int,
+      // up to 4 cached bits) the 16 starts end at 0.15-0.42 ops per nominal
+      // step, the 4 best-ranked ones all at 0.36-0.37 (planning 5.8 s with 4
+      // starts, 7.5 s with 16 on 8 host threads).
       // Every walk position and the lane columns (positions m .. m+L-1) are
       // polished: the lanes cost no ops, and with the walk columns they
       // decide which rows stay untouched (config 5: 0.205 -> 0.201 against
       // the first 12 walk positions only).
       const char* pe = std::getenv("SUP_JIT_POLISH");
       if (!pe || std::atoi(pe) != 0) {
-        constexpr int kPolish = 4;
+        const int kPolish = std::getenv("SUP_JIT_NPOLISH") ? std::max(1, std::atoi(std::getenv("SUP_JIT_NPOLISH"))) : 16;
         std::stable_sort(ranked.begin(), ranked.end(),
                          [](const auto& x, const auto& y) { return std::get<0>(x) < std::get<0>(y); });
         std::vector<std::tuple<double, int, std::vector<int>>> starts;
@@ -1595,7 +1628,7 @@ int build_seg(Plan& P, int fixed_budget) {
         R.n = n, R.m = m, R.touched = P.touched;
         R.len0 = P.seg_start[1], R.s_end = P.sub_start.back(), R.r_end = P.seg_start.back();
         seg_rows_finish(R, cb);
-        const SegFit f = seg_best(R);
+        const SegFit f = seg_best(R, std::min(max_cached(), P.lay.cc_cap));
         const double sc = seg_block_bytes(f, cb) > kMaxBlockBytes ? 1e300 : seg_score(f);
         if (sc < best - 1e-12) best = sc, P.seg_b = cb;
       }
@@ -1617,14 +1650,15 @@ int build_seg(Plan& P, int fixed_budget) {
   seg_rows_finish(SR, P.seg_b);
   // trees, cached classes and storage plan for live-value budget `budget`,
   // then the tables and the generated source (Q starts as a copy of P)
-  auto finish = [&SR, n, L, m](Plan& Q, int budget) {
+  const int cc_cap = std::min(max_cached(), P.lay.cc_cap);
+  auto finish = [&SR, &cc_cap, n, L, m](Plan& Q, int budget) {
     SegFit f;
     // experiments / tests: SUP_JIT_CC forces cc; SUP_JIT_STORAGE forces the
     // storage budget of the chosen plan (same walk order and trees, other
     // live/on-demand choices: the same values, so bit-identical results)
     if (const char* e = std::getenv("SUP_JIT_CC"))
       f = seg_fit(SR, std::max(0, std::min({std::atoi(e), SR.b - 1, kMaxCachedBits})), budget);
-    else f = seg_best(SR, kMaxCachedBits, budget);
+    else f = seg_best(SR, cc_cap, budget);
     if (const char* e = std::getenv("SUP_JIT_STORAGE")) f = seg_fit(SR, f.cc, std::max(0, std::atoi(e)));
     Q.outer_tree = std::move(f.outer);
     Q.inner_tree = std::move(f.inner);
@@ -1678,6 +1712,22 @@ int build_seg(Plan& P, int fixed_budget) {
   const bool fixed = fixed_budget > 0 || std::getenv("SUP_JIT_REGMAX") || std::getenv("SUP_JIT_STORAGE") ||
                      std::getenv("SUP_JIT_CC") || std::getenv("SUP_JIT_NOVERIFY");
   const double walk_s = std::ldexp(1.0, n - 1) * P.seg_ops / 3.7e13;
+  if (fixed && std::getenv("SUP_JIT_VERBOSE")) {  // experiments: what the compiler made of the fixed plan
+    CodeScan s;
+    const int rc = jit_code_scan(P, &s);
+    std::fprintf(stderr, "  fixed budget %d: ops %.4f rc %d vgprs %d spills %d scratch %dB (loop %d of %d insts)\n",
+                 P.seg_budget, P.seg_ops, rc, s.vgprs, s.vgpr_spills, s.scratch_bytes, s.loop_scratch, s.loop_insts);
+  }
+  // Short walks skip the ladder (its compiles would cost more than they save),
+  // but 16 cached states need many registers: the kernel that would run is
+  // compiled (it is needed anyway; cached by its key) and checked, and if its
+  // walk loop touches scratch make_seg_plan plans again with 3 cached bits (on
+  // the 0.6 ms n = 32 config 2 walk, 4 cached bits spill 21 VGPRs inside the
+  // loop: 0.665 ms against 0.588 ms with 3).
+  if (!fixed && walk_s < 0.01 && P.seg_cc > 3) {
+    CodeScan s;
+    P.seg_loop_scratch = jit_code_scan(P, &s) != SUP_OK || s.loop_scratch != 0;
+  }
   if (!fixed && walk_s >= 0.01 && P.seg_regs > kRegs3) {
     // the ladder of budgets, one candidate plan per budget (host threads)
     std::vector<int> budgets;
@@ -2003,7 +2053,8 @@ bool seg_choice_load(uint64_t key, int* m, SegChoice* c) {
   std::istringstream in(buf.data());
   std::string tag;
   int ver = 0, cnt = 0;
-  if (!(in >> tag >> ver >> *m >> c->b >> c->budget >> cnt) || tag != "supseg" || ver != 2 || cnt < 1 || cnt > 64)
+  if (!(in >> tag >> ver >> *m >> c->b >> c->budget >> c->cc_cap >> cnt) || tag != "supseg" || ver != 3 || cnt < 1 ||
+      cnt > 64 || c->cc_cap < 0 || c->cc_cap > kMaxCachedBits)
     return false;
   c->order.resize(cnt);
   for (int& v : c->order)
@@ -2021,7 +2072,7 @@ void seg_choice_store(uint64_t key, int m, const SegChoice& c) {
   const std::string dir = cache_dir();
   if (dir.empty() || c.order.empty()) return;
   std::ostringstream o;
-  o << "supseg 2 " << m << ' ' << c.b << ' ' << c.budget << ' ' << c.order.size();
+  o << "supseg 3 " << m << ' ' << c.b << ' ' << c.budget << ' ' << c.cc_cap << ' ' << c.order.size();
   for (int v : c.order) o << ' ' << v;
   o << '\n';
   const std::string str = o.str();

@@ -1,9 +1,10 @@
 """A/B of one SUP_JIT_* code-generation knob on the walk kernels the bench
 times: each (matrix, setting) is planned and compiled, then timed (median of
-5 launches through sup_perman_shard).  Settings are env assignments;
-'-' is the default.
+5 launches through sup_perman_shard).  A setting is one or more env
+assignments joined by commas; '-' is the default.  PROBE_CASES (comma-separated
+fixture names) restricts the matrices.
 
-    python3 tools/probe_ab.py KNOB=val [KNOB=val ...]
+    python3 tools/probe_ab.py KNOB=val[,KNOB2=val] [...]
 """
 import os
 import statistics
@@ -15,6 +16,8 @@ import superman_amd as S  # noqa: E402
 CASES = [("double__40_0.50_0", 0, "dense"), ("double__36_0.20_0", 1, "sparse"), ("double__32_0.50_0", 0, "dense"),
          ("double__40_0.20_0", 0, "dense"), ("synth44_0.15_int", 2, "skip")]
 settings = ["-"] + sys.argv[1:]
+if os.environ.get("PROBE_CASES"):
+    CASES = [c for c in CASES if c[0] in os.environ["PROBE_CASES"].split(",")]
 for name, prep, kernel in CASES:
     a = S.read_matrix(os.path.join("tests", "fixtures", name))[0]
     if prep == 1:
@@ -24,8 +27,9 @@ for name, prep, kernel in CASES:
     for st in settings:
         env = {}
         if st != "-":
-            k, v = st.split("=", 1)
-            env[k] = v
+            for kv in st.split(","):
+                k, v = kv.split("=", 1)
+                env[k] = v
         for k, v in env.items():
             os.environ[k] = v
         info = S.plan_info(a, kernel, jit=1)
