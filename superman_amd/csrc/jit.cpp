@@ -1350,6 +1350,16 @@ struct Gen {
         off = (off + cls_consts[c].size() + 7) & ~(size_t)7;
       }
     }
+    if (std::getenv("SUP_JIT_VERBOSE")) {
+      std::fprintf(stderr, "  constant streams (doubles): directory %zu", ctab.size());
+      for (int c = 0; c <= b; ++c) {
+        int same = -1;
+        for (int c2 = 0; c2 < c && same < 0; ++c2)
+          if (!cls_consts[c].empty() && cls_consts[c2] == cls_consts[c]) same = c2;
+        std::fprintf(stderr, ", class %d: %zu%s", c, cls_consts[c].size(), same >= 0 ? " (= earlier)" : "");
+      }
+      std::fprintf(stderr, "\n");
+    }
     int nlive = 0;
     for (int r = 0; r < n; ++r)
       for (int v = 0; v < 2; ++v) nlive += live(r, v);
@@ -1807,8 +1817,10 @@ int build_seg(Plan& P, int fixed_budget) {
   }
   P.seg_skip = seg_skip_fraction_plan(P, 2048);
   if (std::getenv("SUP_JIT_VERBOSE"))
-    std::fprintf(stderr, "seg plan n=%d m=%d b=%d ops/step=%.4f regs=%d cc=%d key=%016llx (storage plans evaluated: %ld)\n",
-                 n, m, P.seg_b, P.seg_ops, P.seg_regs, P.seg_cc, (unsigned long long)P.jit_key, g_fit_calls.load());
+    std::fprintf(stderr, "seg plan n=%d m=%d b=%d ops/step=%.4f regs=%d cc=%d table=%zu B (columns %zu B) key=%016llx "
+                 "(storage plans evaluated: %ld)\n", n, m, P.seg_b, P.seg_ops, P.seg_regs, P.seg_cc,
+                 P.jtab.size() * sizeof(double), P.seg_cbase * sizeof(double), (unsigned long long)P.jit_key,
+                 g_fit_calls.load());
   return SUP_OK;
 }
 

@@ -119,7 +119,7 @@ def test_seg_n40_bench_matrix(sup):
     assert -2 * full == r_seg
 
 
-@pytest.mark.parametrize("cc", [0, 1, 2, 3])
+@pytest.mark.parametrize("cc", [0, 1, 2, 3, 4])
 def test_seg_cached_bits_bitexact(sup, orc, monkeypatch, cc):
     """Each cached-walk-bit count (SUP_JIT_CC forces it) on the GPU: bit-exact
     against the oracle's per-state mirror and the host twin."""
