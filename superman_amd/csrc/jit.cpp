@@ -67,6 +67,7 @@
 // live-value budget (no compiler check), search starts, skip polish, register
 // budget, SGPR pieces per region, prefetch, cross-step regions, occupancy,
 // dynamic LDS.
+#include <dlfcn.h>
 #include <hip/hiprtc.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -1550,12 +1551,28 @@ uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
   return h;
 }
 
-// hiprtc's own version: part of the code-object key, so a disk cache written
-// by another ROCm release is not reused
+// The compiler: hiprtc's version and the library file it runs from (path,
+// size, mtime) — part of the code-object key and the plan-choice key, so a
+// disk cache written by another ROCm release is not reused.  The file matters
+// within one release number: a process that imports torch first resolves
+// hiprtc (and comgr) to torch's bundled copies, which report the same version
+// as /opt/rocm's but generate different code (the n = 40 bench matrix: the
+// budget check picks 214 live values with one, 206 with the other).
 std::string hiprtc_version() {
-  int major = 0, minor = 0;
-  if (hiprtcVersion(&major, &minor) != HIPRTC_SUCCESS) return "hiprtc ?";
-  return "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + " hip " + std::to_string(HIP_VERSION);
+  static const std::string v = [] {
+    int major = 0, minor = 0;
+    if (hiprtcVersion(&major, &minor) != HIPRTC_SUCCESS) return std::string("hiprtc ?");
+    std::string r = "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + " hip " + std::to_string(HIP_VERSION);
+    Dl_info di;
+    if (dladdr(reinterpret_cast<void*>(&hiprtcCreateProgram), &di) && di.dli_fname) {
+      r += std::string(" ") + di.dli_fname;
+      struct stat sb;
+      if (::stat(di.dli_fname, &sb) == 0)
+        r += " " + std::to_string((long long)sb.st_size) + " " + std::to_string((long long)sb.st_mtime);
+    }
+    return r;
+  }();
+  return v;
 }
 
 uint64_t toolchain_hash_impl() {

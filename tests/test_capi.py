@@ -5,6 +5,7 @@ import ctypes as C
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -89,7 +90,9 @@ def test_fixed_walk_length_is_its_own_plan(sup, tmp_path):
     L, m, h = sup.layout(36)
     auto = sup.plan_info(a, "seg")
     here = sup.plan_key(a, "seg", walk_log2=m)
-    code = ("import sys; sys.path.insert(0, {root!r}); import numpy as np, superman_amd as S; "
+    # the same compiler as this process (torch first resolves hiprtc to its own copy)
+    code = ("import torch; " if "torch" in sys.modules else "") + (
+            "import sys; sys.path.insert(0, {root!r}); import numpy as np, superman_amd as S; "
             "a = np.load({p!r}); print(S.plan_key(a, 'seg', walk_log2={m}))").format(root=ROOT, p=str(tmp_path / "a.npy"),
                                                                                       m=m)
     np.save(tmp_path / "a.npy", a)

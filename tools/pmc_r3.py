@@ -21,6 +21,8 @@ import json
 import os
 import sys
 
+import torch  # noqa: F401,E402  (first, as in bench.py: the kernels and the plan key come from torch's hiprtc)
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import superman_amd as S  # noqa: E402

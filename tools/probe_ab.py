@@ -2,13 +2,17 @@
 times: each (matrix, setting) is planned and compiled, then timed (median of
 5 launches through sup_perman_shard).  A setting is one or more env
 assignments joined by commas; '-' is the default.  PROBE_CASES (comma-separated
-fixture names) restricts the matrices.
+fixture names) restricts the matrices; PROBE_TORCH=1 imports torch first (its
+bundled HIP runtime, hiprtc and comgr then compile the kernels, as in bench.py).
 
     python3 tools/probe_ab.py KNOB=val[,KNOB2=val] [...]
 """
 import os
 import statistics
 import sys
+
+if os.environ.get("PROBE_TORCH") == "1":
+    import torch  # noqa: F401
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import superman_amd as S  # noqa: E402
