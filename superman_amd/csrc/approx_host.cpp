@@ -159,9 +159,9 @@ struct DevWorker {
 
   int init(int device, const Job& J, uint64_t item) {
     dev = device;
-    AHIP(hipSetDevice(dev));
+    AHIP(hipSetDevice(phys_device(dev)));
     hipDeviceProp_t prop;
-    AHIP(hipGetDeviceProperties(&prop, dev));
+    AHIP(hipGetDeviceProperties(&prop, phys_device(dev)));
     cus = prop.multiProcessorCount;
     // The cooperative form for large n (tools/probe_approx_coop.py,
     // profiles/r2/probe_approx_coop.log): the scaling estimator from n > 96
@@ -191,7 +191,7 @@ struct DevWorker {
     return SUP_OK;
   }
   int run(const Job& J, uint64_t b0, uint64_t nb, double out[3]) {
-    AHIP(hipSetDevice(dev));
+    AHIP(hipSetDevice(phys_device(dev)));
     ApproxParams p{};
     p.rowpat = d_row;
     p.colpat = d_col;
@@ -221,7 +221,7 @@ struct DevWorker {
   }
   ~DevWorker() {
     if (!st) return;
-    (void)hipSetDevice(dev);
+    (void)hipSetDevice(phys_device(dev));
     (void)hipFree(d_row);
     (void)hipFree(d_col);
     (void)hipFree(d_part);

@@ -598,7 +598,8 @@ double pairwise_host(const std::vector<double>& v) {
 
 // -------------------------------------------------------- device contexts --
 struct DeviceCtx {
-  int dev = 0;
+  int dev = 0;   // logical id (the API's)
+  int phys = 0;  // the HIP device it runs on (phys_device)
   int cus = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -629,6 +630,33 @@ struct DeviceCtx {
 static std::mutex g_ctx_mu;
 static std::vector<std::unique_ptr<DeviceCtx>> g_ctx;
 
+// Logical devices.  Every device id of the API (sup_opts::device_id, the
+// devices of a multi-device schedule) is a logical id; SUP_DEVICE_MAP (a
+// comma list of physical ids, e.g. "0,0,0,0") puts several logical devices on
+// one physical GPU, each with its own context (stream, buffers, queue), so the
+// multi-device schedulers' per-device threads, combines and item queues run —
+// concurrently — on a one-GPU machine.  Unset: logical = physical.  RCCL needs
+// distinct physical devices (rccl_allreduce_slots refuses a duplicated map).
+static std::vector<int> device_map() {
+  std::vector<int> m;
+  const char* e = std::getenv("SUP_DEVICE_MAP");
+  if (!e || !*e) return m;
+  for (const char* p = e; *p;) {
+    char* end = nullptr;
+    const long v = std::strtol(p, &end, 10);
+    if (end == p || v < 0 || v > 1023) return {-1};  // malformed: device_count reports it
+    m.push_back((int)v);
+    p = *end == ',' ? end + 1 : end;
+    if (*end && *end != ',') return {-1};
+  }
+  return m;
+}
+
+int phys_device(int dev) {
+  const std::vector<int> m = device_map();
+  return (m.empty() || dev < 0 || dev >= (int)m.size()) ? dev : m[dev];
+}
+
 int device_count(int* n) {
   int c = 0;
   hipError_t e = hipGetDeviceCount(&c);
@@ -637,13 +665,26 @@ int device_count(int* n) {
     set_error(std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
     return SUP_ENODEV;
   }
+  const std::vector<int> m = device_map();
+  if (!m.empty() && c > 0) {
+    for (int p : m)
+      if (p < 0 || p >= c) {
+        *n = 0;
+        set_error("SUP_DEVICE_MAP names a device that does not exist (" + std::to_string(c) +
+                  " physical devices; expected a comma list of their ids)");
+        return SUP_ENODEV;
+      }
+    c = (int)m.size();
+  }
   *n = c;
   return SUP_OK;
 }
 
 static int get_ctx(int dev, DeviceCtx** out) {
   int cnt = 0;
-  if (device_count(&cnt) != SUP_OK || cnt == 0) {
+  int rc = device_count(&cnt);
+  if (rc) return rc;
+  if (cnt == 0) {
     set_error("no HIP device available (the engine has no CPU fallback for GPU algorithms)");
     return SUP_ENODEV;
   }
@@ -651,14 +692,21 @@ static int get_ctx(int dev, DeviceCtx** out) {
     set_error("device id " + std::to_string(dev) + " out of range (" + std::to_string(cnt) + " devices)");
     return SUP_ENODEV;
   }
+  const int pd = phys_device(dev);
   std::lock_guard<std::mutex> g(g_ctx_mu);
   if (g_ctx.size() < (size_t)cnt) g_ctx.resize(cnt);
+  if (g_ctx[dev] && g_ctx[dev]->phys != pd) {
+    set_error("logical device " + std::to_string(dev) + " moved to another physical device (SUP_DEVICE_MAP "
+              "changed after first use)");
+    return SUP_EINVAL;
+  }
   if (!g_ctx[dev]) {
     auto c = std::make_unique<DeviceCtx>();
     c->dev = dev;
-    SUP_HIP(hipSetDevice(dev));
+    c->phys = pd;
+    SUP_HIP(hipSetDevice(pd));
     hipDeviceProp_t prop;
-    SUP_HIP(hipGetDeviceProperties(&prop, dev));
+    SUP_HIP(hipGetDeviceProperties(&prop, pd));
     c->cus = prop.multiProcessorCount;
     SUP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     SUP_HIP(hipEventCreate(&c->ev0));
@@ -700,7 +748,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   int rc = get_ctx(dev, &c);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(c->mu);
-  SUP_HIP(hipSetDevice(dev));
+  SUP_HIP(hipSetDevice(c->phys));
   const uint64_t count = c1 - c0;
   const double* cols_before = c->d_cols;
   const double* jtab_before = c->d_jtab;
@@ -733,7 +781,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
 
   int occ_seg = 0, occ_lds = 0;
-  if (seg && (rc = jit_occupancy(dev, P, &occ_seg, &r.compile_ms))) return rc;
+  if (seg && (rc = jit_occupancy(c->phys, P, &occ_seg, &r.compile_ms))) return rc;
   if (P.lds) {  // LDS-staged dense walk: one wave per block, LDS-limited residency
     SUP_HIP(lds_occupancy(P.n, P.lay.m, &occ_lds));
     if (occ_lds < 1) occ_lds = 1;
@@ -802,7 +850,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
 
   SUP_HIP(hipEventRecord(c->ev0, s));
   if (seg) {
-    if ((rc = jit_launch(dev, P, p, (int)grid, s))) return rc;
+    if ((rc = jit_launch(c->phys, P, p, (int)grid, s))) return rc;
   } else if (P.lds) {
     SUP_HIP(launch_lds(P.n, p, (int)grid, s));
   } else {
@@ -852,7 +900,7 @@ int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1,
   int rc = get_ctx(dev, &c);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(c->mu);
-  SUP_HIP(hipSetDevice(dev));
+  SUP_HIP(hipSetDevice(c->phys));
   int occ = 0;
   SUP_HIP(exact_occupancy(P.n, group, &occ));
   if (occ < 1) occ = 1;
@@ -913,7 +961,7 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
   int rc = get_ctx(dev, &c);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(c->mu);
-  SUP_HIP(hipSetDevice(dev));
+  SUP_HIP(hipSetDevice(c->phys));
   int occ = 0;
   SUP_HIP(dd_occupancy(P.n, &occ));
   if (occ < 1) occ = 1;
@@ -977,7 +1025,16 @@ struct RcclSlots {
 };
 
 static int rccl_slots_init(const std::vector<int>& devs, size_t len, RcclSlots& r) {
-  r.devs = devs;
+  r.devs.clear();
+  for (int d : devs) r.devs.push_back(phys_device(d));  // RCCL ranks are physical devices
+  std::vector<int> uniq = r.devs;
+  std::sort(uniq.begin(), uniq.end());
+  if (std::adjacent_find(uniq.begin(), uniq.end()) != uniq.end()) {
+    r.devs.clear();
+    set_error("RCCL combine (-R) needs distinct physical devices; SUP_DEVICE_MAP puts several logical devices on "
+              "one (use the host combine)");
+    return SUP_ERCCL;
+  }
   r.len = len;
   r.buf.assign(devs.size(), nullptr);
   r.st.assign(devs.size(), nullptr);

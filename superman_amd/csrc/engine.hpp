@@ -236,6 +236,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
 double pairwise_host(const std::vector<double>& v);
 
 int device_count(int* n);
+int phys_device(int dev);  // logical -> physical (SUP_DEVICE_MAP; identity when unset)
 
 // Schedulers (one host thread per device).
 struct SchedResult {

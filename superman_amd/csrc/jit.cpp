@@ -73,6 +73,9 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstring>
+#include <fstream>
+#include <iterator>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -1551,8 +1554,8 @@ uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
   return h;
 }
 
-// The compiler: hiprtc's version and the library file it runs from (path,
-// size, mtime) — part of the code-object key and the plan-choice key, so a
+// The compiler: hiprtc's version and the library file it runs from (name,
+// size, content hash) — part of the code-object key and the plan-choice key, so a
 // disk cache written by another ROCm release is not reused.  The file matters
 // within one release number: a process that imports torch first resolves
 // hiprtc (and comgr) to torch's bundled copies, which report the same version
@@ -1565,10 +1568,18 @@ std::string hiprtc_version() {
     std::string r = "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + " hip " + std::to_string(HIP_VERSION);
     Dl_info di;
     if (dladdr(reinterpret_cast<void*>(&hiprtcCreateProgram), &di) && di.dli_fname) {
-      r += std::string(" ") + di.dli_fname;
-      struct stat sb;
-      if (::stat(di.dli_fname, &sb) == 0)
-        r += " " + std::to_string((long long)sb.st_size) + " " + std::to_string((long long)sb.st_mtime);
+      // the file's name and a hash of its bytes (~1 MB, ~1 ms): the same
+      // library on another machine of the same image gives the same key (its
+      // path may differ by symlinks, its mtime by how the image was unpacked)
+      const char* slash = std::strrchr(di.dli_fname, '/');
+      r += std::string(" ") + (slash ? slash + 1 : di.dli_fname);
+      std::ifstream f(di.dli_fname, std::ios::binary);
+      if (f) {
+        std::string bytes((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        char hx[40];
+        std::snprintf(hx, sizeof hx, " %zu %016llx", bytes.size(), (unsigned long long)fnv1a(bytes));
+        r += hx;
+      }
     }
     return r;
   }();
