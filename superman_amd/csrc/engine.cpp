@@ -298,6 +298,11 @@ static constexpr double kLaneOpsPerSec = 3.7e13;
 // are paid once per matrix; auto mode specialises when the predicted walk time
 // saved is clearly larger than both.
 static constexpr double kJitMinSavingSec = 3.0;
+// Once this host has made a cold segmented plan (make_seg_plan records its
+// cost next to the code objects: ~0.4 s at n = 40 on a GPU box's 16 threads,
+// 2.4-3.4 s on an 8-CPU container), auto mode's cold bar is twice that cost,
+// within [kJitColdBarMin, kJitMinSavingSec].
+static constexpr double kJitColdBarMin = 0.25;
 // When an earlier process recorded this matrix's segmented-walk choices (disk
 // cache, make_seg_plan), the plan is rebuilt in ~5-50 ms and its code object
 // loads from disk: auto mode specialises whenever the walk saves more than this.
@@ -307,7 +312,8 @@ static constexpr double kJitWarmSavingSec = 0.1;
 static constexpr int kJitWarmMinN = 30;
 
 static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit,
-                             int ndev, int dev);
+                             int ndev, int dev, double min_saving);
+static double auto_min_saving(const double* A, int n, const Layout& lay, int jit);
 
 // Chunk start of the segmented walk (start index's column sums, row copies,
 // trees of every cached state), in VALU ops per lane: ~750 fitted from config
@@ -370,6 +376,7 @@ static int make_seg_plan(const double* A, int n, const Layout& lay, Plan& P) {
       if (make_plan(A, n, kWalkSeg, false, l2, P, &c) == SUP_OK) return SUP_OK;
     }
   }
+  const auto t_cold = std::chrono::steady_clock::now();
   // a short walk whose 4-cached-bit kernel touches scratch in its loop
   // (build_seg's check) is planned again with 3 cached bits
   auto plan = [A, n](const Layout& l, Plan& Q) {
@@ -406,6 +413,9 @@ static int make_seg_plan(const double* A, int n, const Layout& lay, Plan& P) {
   c.budget = P.seg_budget;
   c.cc_cap = P.lay.cc_cap;
   seg_choice_store(dkey, P.lay.m, c);
+  // what this cold plan cost (search + the compiler check's compiles): auto
+  // mode's cold bar on this host (plan_for)
+  seg_cost_store(std::chrono::duration<double>(std::chrono::steady_clock::now() - t_cold).count());
   return SUP_OK;
 }
 
@@ -419,10 +429,10 @@ struct PlanKey {
   int n, kernel, L, m, jit, ndev;
   bool fixed;      // walk length asked for (sup_opts::walk_log2): make_seg_plan keeps it
   uint64_t knobs;  // SUP_JIT_* experiment settings the planner and code generator read
-  bool warm;       // auto mode: this matrix's segmented-walk choices are in the disk cache
+  int bar_ms;      // auto mode's bar (auto_min_saving): warm choices on disk, this host's cold plan cost
   bool operator<(const PlanKey& o) const {
-    return std::tie(hash, n, kernel, L, m, jit, ndev, fixed, knobs, warm) <
-           std::tie(o.hash, o.n, o.kernel, o.L, o.m, o.jit, o.ndev, o.fixed, o.knobs, o.warm);
+    return std::tie(hash, n, kernel, L, m, jit, ndev, fixed, knobs, bar_ms) <
+           std::tie(o.hash, o.n, o.kernel, o.L, o.m, o.jit, o.ndev, o.fixed, o.knobs, o.bar_ms);
   }
 };
 std::mutex g_plan_mu;
@@ -456,11 +466,12 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
     std::memcpy(&b, A + i, 8);
     h = (h ^ b) * 1099511628211ull;
   }
-  // ndev only feeds auto mode's compile-or-not decision
-  // auto mode at sizes where specialising can pay: whether an earlier process
-  // recorded this matrix's choices decides the bar (plan_for_uncached)
-  const bool warm = jit == 0 && n >= kJitWarmMinN && seg_choice_exists(seg_disk_key(A, n, lay));
-  const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0, lay.fixed, knob_hash(), warm};
+  // ndev only feeds auto mode's compile-or-not decision, and so does its bar
+  // (whether an earlier process recorded this matrix's choices, what this
+  // host's last cold plan cost)
+  const double min_saving = auto_min_saving(A, n, lay, jit);
+  const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0, lay.fixed, knob_hash(),
+                    (int)std::lround(min_saving * 1000.0)};
   {
     std::lock_guard<std::mutex> g(g_plan_mu);
     auto it = g_plans.find(key);
@@ -469,7 +480,7 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
       return SUP_OK;
     }
   }
-  const int rc = plan_for_uncached(A, n, kernel, lay, P, jit, ndev, dev);
+  const int rc = plan_for_uncached(A, n, kernel, lay, P, jit, ndev, dev, min_saving);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(g_plan_mu);
   if (g_plans.size() >= kPlanCacheMax) g_plans.clear();
@@ -506,16 +517,22 @@ static double skip_visited_fraction(const Plan& P, int dev) {
   return tot ? (double)vis / (double)tot : 1.0;
 }
 
+// Auto mode's bar for specialising: the predicted walk time saved must exceed
+// the planning + compile it costs — seconds cold (or twice what this host's
+// last cold plan measured), ~0 when an earlier process left this matrix's plan
+// choices and kernel in the disk cache.
+static double auto_min_saving(const double* A, int n, const Layout& lay, int jit) {
+  if (jit != 0 || n < kJitWarmMinN) return kJitMinSavingSec;  // below: no walk lasts even the lowest bar
+  if (seg_choice_exists(seg_disk_key(A, n, lay))) return kJitWarmSavingSec;
+  const double c = seg_cost_load();
+  return c > 0.0 ? std::min(kJitMinSavingSec, std::max(kJitColdBarMin, 2.0 * c)) : kJitMinSavingSec;
+}
+
 static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit,
-                             int ndev, int dev) {
+                             int ndev, int dev, double min_saving) {
   // candidates in preference order; the cheapest by walk_cost wins
   std::vector<WalkKind> kinds;
   auto make_seg = [&](Plan& s) { return make_seg_plan(A, n, lay, s); };
-  // auto mode's bar for specialising: the predicted walk time saved must
-  // exceed the planning + compile it costs — seconds cold, ~0 when an earlier
-  // process left this matrix's plan choices and kernel in the disk cache
-  double min_saving = kJitMinSavingSec;
-  if (jit == 0 && n >= kJitWarmMinN && seg_choice_exists(seg_disk_key(A, n, lay))) min_saving = kJitWarmSavingSec;
   switch (kernel) {
     case SUP_KERNEL_SKIPPER: {
       // SkipPer only gains where some x_j(S) is exactly zero.  With a

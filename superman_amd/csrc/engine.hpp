@@ -159,6 +159,8 @@ int build_seg(Plan& P, int fixed_budget = 0);
 // were priced with (generated-code headers, compile options, hiprtc).
 bool seg_choice_load(uint64_t key, int* m, SegChoice* c);
 bool seg_choice_exists(uint64_t key);
+double seg_cost_load();             // seconds of the last cold segmented plan on this host, -1 if none
+void seg_cost_store(double seconds);
 void seg_choice_store(uint64_t key, int m, const SegChoice& c);
 uint64_t jit_toolchain_hash();
 // Default specialised pair bits, min(m - 1, 5) (the walk loop is unrolled by

@@ -2119,4 +2119,33 @@ void seg_choice_store(uint64_t key, int m, const SegChoice& c) {
   write_file_atomic(dir, "plan_" + key_hex(key) + ".txt", std::vector<char>(str.begin(), str.end()));
 }
 
+// What a cold segmented plan (walk-order search + the compiler check's
+// compiles) cost on this host with this compiler, as make_seg_plan last
+// measured it: "supcost 1 <seconds>", one file per toolchain next to the code
+// objects.  Auto mode's cold bar follows it (plan_for).  -1 when none.
+static std::string seg_cost_name() { return "cost_" + key_hex(jit_toolchain_hash()) + ".txt"; }
+
+double seg_cost_load() {
+  const std::string dir = cache_dir();
+  if (dir.empty()) return -1.0;
+  std::vector<char> buf;
+  if (!read_file(dir + "/" + seg_cost_name(), buf)) return -1.0;
+  buf.push_back('\0');
+  std::istringstream in(buf.data());
+  std::string tag;
+  int ver = 0;
+  double sec = -1.0;
+  if (!(in >> tag >> ver >> sec) || tag != "supcost" || ver != 1 || !(sec > 0.0) || sec > 3600.0) return -1.0;
+  return sec;
+}
+
+void seg_cost_store(double seconds) {
+  const std::string dir = cache_dir();
+  if (dir.empty() || !(seconds > 0.0)) return;
+  char b[64];
+  std::snprintf(b, sizeof b, "supcost 1 %.4f\n", seconds);
+  const std::string str = b;
+  write_file_atomic(dir, seg_cost_name(), std::vector<char>(str.begin(), str.end()));
+}
+
 }  // namespace sup

@@ -77,6 +77,28 @@ def test_planner_choice(sup, tmp_path, monkeypatch):
     assert sup.plan_info(np.ones((12, 12)), "seg")["cached"] >= 1
 
 
+def test_auto_cold_bar_follows_recorded_plan_cost(sup, tmp_path, monkeypatch):
+    # make_seg_plan records what a cold plan cost on this host (cost_<toolchain>.txt);
+    # auto mode's cold bar is then twice that, within [0.25 s, 3 s]
+    monkeypatch.setenv("SUP_JIT_CACHE_DIR", str(tmp_path))
+    a, _, _ = sup.read_matrix(fixture_path("double__40_0.50_0"))
+    b = np.ascontiguousarray(a.T)  # another zero pattern: its choices are not on disk
+    assert sup.plan_info(b, "dense", jit=0)["kind"] == "sparse"  # no record: 3 s bar, ~0.5 s saved
+    # a cold plan records its cost (values scaled: not in this process's plan cache either)
+    assert sup.plan_info(0.5 * a, "dense", jit=1)["kind"] == "seg"
+    cost = list(tmp_path.glob("cost_*.txt"))
+    assert len(cost) == 1
+    tag, ver, sec = cost[0].read_text().split()
+    assert (tag, ver) == ("supcost", "1") and 0 < float(sec) < 600
+    cost[0].write_text("supcost 1 5.0\n")  # a slow host: the bar stays at its 3 s cap
+    assert sup.plan_info(b, "dense", jit=0)["kind"] == "sparse"
+    cost[0].write_text("supcost 1 0.01\n")  # a fast host: bar 0.25 s < the ~0.5 s the walk saves
+    assert sup.plan_info(b, "dense", jit=0)["kind"] == "seg"
+    cost[0].write_text("garbage\n")  # unreadable record: the 3 s default
+    c = np.ascontiguousarray(a[::-1])  # a third pattern
+    assert sup.plan_info(c, "dense", jit=0)["kind"] == "sparse"
+
+
 def test_seg_cost_model_reported(sup):
     a, _, _ = sup.read_matrix(fixture_path("synth/22_0.20_int"))
     _, st_seg = sup.perman_cpu(a, "seg", threads=4, return_stats=True)
