@@ -141,6 +141,24 @@ PMC_COUNTERS = ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU
                 "SQ_WAVES", "SQ_INSTS_SALU", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
 
 
+def auto_decision(S, a, kernel: str, rank: int, world: int, dev: int, device) -> int:
+    """Auto mode (jit = 0) decides from the disk cache's state: whether this
+    matrix's plan choices are recorded, what this host's last cold plan cost.
+    Ranks sharing a cache see it at different moments (one rank's plan writes
+    what the next one reads), so they could decide differently.  Rank 0
+    decides; every rank then walks that choice explicitly (jit = 1: the
+    segmented walk, -1: the ahead-of-time kernel), the same plan auto mode
+    chose."""
+    import torch
+    import torch.distributed as dist
+    v = 0
+    if rank == 0:
+        v = 1 if S.plan_info(a, kernel, jit=0, gpu_num=world, device_id=dev)["kind"] == "seg" else -1
+    t = torch.tensor([v], dtype=torch.int64, device=device)
+    dist.broadcast(t, 0)
+    return int(t.item())
+
+
 def pmc_child(args) -> None:
     """--pmc-child: one launch of the walk the parent times (same plan: same
     matrix, kernel request, jit, one shard), run under rocprofv3 by the parent."""
@@ -363,6 +381,8 @@ def main():
         n = a.shape[0]
         kernel = args.kernel if kernel is None else kernel
         jit = args.jit if jit is None else jit
+        if jit == 0 and world > 1:
+            jit = auto_decision(S, a, kernel, rank, world, dev, tdev)
         # plan + (segmented walk) hiprtc compile, once, before the timed region;
         # gpu_num = world so that --jit 0 decides as the N-rank plan would
         prep = S.prepare(a, kernel, jit=jit, gpu_num=world, device_id=dev)

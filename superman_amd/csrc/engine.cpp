@@ -429,10 +429,15 @@ struct PlanKey {
   int n, kernel, L, m, jit, ndev;
   bool fixed;      // walk length asked for (sup_opts::walk_log2): make_seg_plan keeps it
   uint64_t knobs;  // SUP_JIT_* experiment settings the planner and code generator read
-  int bar_ms;      // auto mode's bar (auto_min_saving): warm choices on disk, this host's cold plan cost
+  // Not in the key: auto mode's bar (auto_min_saving), which moves with the
+  // disk cache (this matrix's choices recorded, this host's cold plan cost) —
+  // possibly written meanwhile by another rank or thread.  The first auto-mode
+  // decision for a matrix and request is kept for the process, so a call after
+  // sup_prepare / sup_plan_key (the bench's plan-agreement check) walks the
+  // plan that was checked.
   bool operator<(const PlanKey& o) const {
-    return std::tie(hash, n, kernel, L, m, jit, ndev, fixed, knobs, bar_ms) <
-           std::tie(o.hash, o.n, o.kernel, o.L, o.m, o.jit, o.ndev, o.fixed, o.knobs, o.bar_ms);
+    return std::tie(hash, n, kernel, L, m, jit, ndev, fixed, knobs) <
+           std::tie(o.hash, o.n, o.kernel, o.L, o.m, o.jit, o.ndev, o.fixed, o.knobs);
   }
 };
 std::mutex g_plan_mu;
@@ -466,12 +471,8 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
     std::memcpy(&b, A + i, 8);
     h = (h ^ b) * 1099511628211ull;
   }
-  // ndev only feeds auto mode's compile-or-not decision, and so does its bar
-  // (whether an earlier process recorded this matrix's choices, what this
-  // host's last cold plan cost)
-  const double min_saving = auto_min_saving(A, n, lay, jit);
-  const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0, lay.fixed, knob_hash(),
-                    (int)std::lround(min_saving * 1000.0)};
+  // ndev only feeds auto mode's compile-or-not decision
+  const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0, lay.fixed, knob_hash()};
   {
     std::lock_guard<std::mutex> g(g_plan_mu);
     auto it = g_plans.find(key);
@@ -480,9 +481,16 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
       return SUP_OK;
     }
   }
-  const int rc = plan_for_uncached(A, n, kernel, lay, P, jit, ndev, dev, min_saving);
+  const int rc = plan_for_uncached(A, n, kernel, lay, P, jit, ndev, dev, auto_min_saving(A, n, lay, jit));
   if (rc) return rc;
   std::lock_guard<std::mutex> g(g_plan_mu);
+  {
+    auto it = g_plans.find(key);  // another thread planned the same request meanwhile: its plan stands
+    if (it != g_plans.end() && std::equal(A, A + nn, it->second.first.begin())) {
+      P = it->second.second;
+      return SUP_OK;
+    }
+  }
   if (g_plans.size() >= kPlanCacheMax) g_plans.clear();
   static uint64_t next_uid = 0;
   P.uid = ++next_uid;

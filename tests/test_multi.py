@@ -137,3 +137,57 @@ def test_bench_plan_fingerprint_guard(perturb):
             assert status == "mismatch" and "planned different walks" in detail
         else:
             assert status == "ok" and len(set(detail)) == 1
+
+
+def _auto_worker(rank, world, port, mat, dirs, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["SUP_JIT_CACHE_DIR"] = dirs[rank]
+    import bench
+    import superman_amd as S
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    naive = S.plan_info(mat, "dense", jit=0, gpu_num=world)["kind"]  # this rank's own auto decision
+    jit = bench.auto_decision(S, mat, "dense", rank, world, 0, "cpu")
+    key = S.plan_key(mat, "dense", jit=jit, gpu_num=world)
+    try:
+        bench.check_plans_agree(key, rank, world, "cpu")
+        status = "ok"
+    except RuntimeError as e:
+        status = str(e)
+    q.put((rank, (naive, jit, status)))
+    dist.destroy_process_group()
+
+
+def test_bench_auto_mode_decided_by_rank0(tmp_path):
+    """Auto mode (jit = 0) decides from the disk cache's state, which ranks see
+    at different moments: here rank 1's cache already holds the bench matrix's
+    segmented-walk choices (warm: specialise when it saves > 0.1 s) and rank
+    0's is empty (cold: > 3 s), so on their own they would plan different
+    walks.  bench.auto_decision makes rank 0's choice everyone's."""
+    import superman_amd as S
+    from conftest import fixture_path
+    a, _, _ = S.read_matrix(fixture_path("double__40_0.50_0"))
+    warm, cold = tmp_path / "warm", tmp_path / "cold"
+    warm.mkdir()
+    cold.mkdir()
+    os.environ["SUP_JIT_CACHE_DIR"] = str(warm)
+    try:  # record the pattern's choices (a scaled copy: same pattern, not in this process's plan cache)
+        assert S.plan_info(0.125 * a, "dense", jit=1)["kind"] == "seg"
+    finally:
+        del os.environ["SUP_JIT_CACHE_DIR"]
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    dirs = [str(cold), str(warm)]
+    procs = [ctx.Process(target=_auto_worker, args=(r, world, port, a, dirs, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert res[0][0] == "sparse" and res[1][0] == "seg"  # left alone, the ranks disagree
+    for r in range(world):
+        assert res[r][1] == -1 and res[r][2] == "ok"  # rank 0's choice (the ahead-of-time walk) for all

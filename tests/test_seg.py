@@ -60,9 +60,13 @@ def test_planner_choice(sup, tmp_path, monkeypatch):
     assert sup.plan_info(a, "dense", jit=1)["kind"] == "seg"
     # warm: the jit = 1 plan left its choices (and kernel) in the disk cache,
     # rebuilding costs ~ms, so auto mode now takes the segmented walk
+    # (another matrix of the same zero pattern: the choices are keyed by the pattern; `a` itself keeps its
+    # first auto-mode decision for the life of the process)
     assert any(p.name.startswith("plan_") for p in tmp_path.iterdir())
-    assert sup.plan_info(a, "dense", jit=0)["kind"] == "seg"
-    assert sup.plan_key(a, "dense", jit=0) == sup.plan_key(a, "dense", jit=1)
+    assert sup.plan_info(a, "dense", jit=0)["kind"] == "sparse"
+    a2 = 0.5 * a
+    assert sup.plan_info(a2, "dense", jit=0)["kind"] == "seg"
+    assert sup.plan_key(a2, "dense", jit=0) == sup.plan_key(a2, "dense", jit=1)
     c, _, _ = sup.read_matrix(fixture_path("double__32_0.50_0"))
     assert sup.plan_info(c, "dense", jit=0)["kind"] == "sparse"  # 2^31 steps: ms saved
     b, _, _ = sup.read_matrix(fixture_path("synth44_0.15_int"))
@@ -85,15 +89,17 @@ def test_auto_cold_bar_follows_recorded_plan_cost(sup, tmp_path, monkeypatch):
     b = np.ascontiguousarray(a.T)  # another zero pattern: its choices are not on disk
     assert sup.plan_info(b, "dense", jit=0)["kind"] == "sparse"  # no record: 3 s bar, ~0.5 s saved
     # a cold plan records its cost (values scaled: not in this process's plan cache either)
-    assert sup.plan_info(0.5 * a, "dense", jit=1)["kind"] == "seg"
+    assert sup.plan_info(0.375 * a, "dense", jit=1)["kind"] == "seg"
     cost = list(tmp_path.glob("cost_*.txt"))
     assert len(cost) == 1
     tag, ver, sec = cost[0].read_text().split()
     assert (tag, ver) == ("supcost", "1") and 0 < float(sec) < 600
+    # (each check on a new matrix of b's pattern: a matrix keeps its first auto-mode decision in a process)
     cost[0].write_text("supcost 1 5.0\n")  # a slow host: the bar stays at its 3 s cap
-    assert sup.plan_info(b, "dense", jit=0)["kind"] == "sparse"
+    assert sup.plan_info(0.5 * b, "dense", jit=0)["kind"] == "sparse"
     cost[0].write_text("supcost 1 0.01\n")  # a fast host: bar 0.25 s < the ~0.5 s the walk saves
-    assert sup.plan_info(b, "dense", jit=0)["kind"] == "seg"
+    assert sup.plan_info(0.25 * b, "dense", jit=0)["kind"] == "seg"
+    assert sup.plan_info(b, "dense", jit=0)["kind"] == "sparse"  # b's own first decision stands
     cost[0].write_text("garbage\n")  # unreadable record: the 3 s default
     c = np.ascontiguousarray(a[::-1])  # a third pattern
     assert sup.plan_info(c, "dense", jit=0)["kind"] == "sparse"
