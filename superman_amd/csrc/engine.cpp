@@ -695,8 +695,8 @@ int device_count(int* n) {
     for (int p : m)
       if (p < 0 || p >= c) {
         *n = 0;
-        set_error("SUP_DEVICE_MAP names a device that does not exist (" + std::to_string(c) +
-                  " physical devices; expected a comma list of their ids)");
+        set_error("SUP_DEVICE_MAP must be a comma list of existing physical device ids (" + std::to_string(c) +
+                  " visible)");
         return SUP_ENODEV;
       }
     c = (int)m.size();
