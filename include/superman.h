@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SUP_ABI_VERSION 5
+#define SUP_ABI_VERSION 6
 
 /* ---- error codes ------------------------------------------------------ */
 #define SUP_OK            0
@@ -104,9 +104,17 @@ typedef struct {
   int verbose;        /* print per-device / per-chunk timing lines like the reference        */
   int jit;            /* segmented walk specialised for the matrix pattern (hiprtc, gfx950):  */
                       /*  -1 never; 0 auto: when its cost model wins and the predicted walk  */
-                      /*  time saved exceeds 3 s (plan 0.2-6 s + compile ~0.5 s, both once  */
-                      /*  per matrix: plans cached in memory, code objects also on disk); 1  */
-                      /*  whenever its cost model wins                                       */
+                      /*  time saved exceeds what the plan costs (3 s, or twice this host's  */
+                      /*  last cold plan; 0.1 s with the matrix's choices on disk; the first */
+                      /*  decision for a matrix holds for the process); 1 whenever its cost  */
+                      /*  model wins                                                         */
+  const char* checkpoint; /* SUP_SCHED_CHUNKS (-p6/-p8) only, NULL = none: file recording every */
+                      /*  finished queue item's partial (appended and flushed as items finish;*/
+                      /*  header: plan fingerprint, chunk range, item size).  A call given a  */
+                      /*  file with a matching header takes the items it lists instead of    */
+                      /*  walking them, so an interrupted run resumes; the result is bit-    */
+                      /*  identical to an uninterrupted one.  A mismatching header is         */
+                      /*  SUP_EINVAL.  (ABI version 6)                                        */
 } sup_opts;
 
 typedef struct {
@@ -126,6 +134,8 @@ typedef struct {
   int      leaves;          /* permanents computed: 1, or the leaf count of sup_perman_reduced   */
   double   est_ops_per_step;/* cost model: fp64 VALU ops per Gray step and lane                 */
   double   jit_ms;          /* hiprtc compile time spent by this call (0 when cached / unused)   */
+  int      items_resumed;   /* queue items taken from sup_opts.checkpoint instead of walked      */
+  int      reserved_;
 } sup_stats;
 
 /* Fill `o` with defaults. */

@@ -11,6 +11,7 @@ fallback.  ``perman_cpu`` is the explicit CPU algorithm of the CLI's ``-c``.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -81,7 +82,7 @@ def _mat(a, max_n: int = 64) -> tuple[np.ndarray, int, int]:
 
 
 def _opts(gpu_num=1, device_id=0, threads=16, cpu=False, walk_log2=0, chunk_log2=0, use_rccl=False,
-          verbose=False, jit=0) -> SupOpts:
+          verbose=False, jit=0, checkpoint=None) -> SupOpts:
     lib = _lib.load()
     o = SupOpts()
     lib.sup_opts_init(C.byref(o))
@@ -89,6 +90,8 @@ def _opts(gpu_num=1, device_id=0, threads=16, cpu=False, walk_log2=0, chunk_log2
     o.cpu_worker, o.walk_log2, o.chunk_log2 = int(bool(cpu)), int(walk_log2), int(chunk_log2)
     o.use_rccl, o.verbose = int(use_rccl), int(bool(verbose))  # use_rccl=2: RCCL even on one device
     o.jit = int(jit)  # segmented walk: -1 never, 0 auto, 1 whenever its cost model wins
+    # chunk queue (-p6/-p8): record / resume finished items (the struct keeps the bytes alive via _objects)
+    o.checkpoint = os.fsencode(checkpoint) if checkpoint else None
     return o
 
 
@@ -113,7 +116,8 @@ def layout(n: int) -> tuple[int, int, int]:
 
 def perman(mat, algo: int = 4, sparse: bool = False, gpu_num: int = 1, cpu: bool = False,
            threads: int = 16, device_id: int = 0, use_rccl: bool = False, walk_log2: int = 0,
-           chunk_log2: int = 0, return_stats: bool = False, jit: int = 0, kernel: str | None = None):
+           chunk_log2: int = 0, return_stats: bool = False, jit: int = 0, kernel: str | None = None,
+           checkpoint: str | None = None):
     """GPU exact permanent, dispatched by the reference algorithm id (main.cu:30-143).
 
     ``sparse`` selects the sparse table (SpaRyser ids 1-6, SkipPer 7/8).  Apply
@@ -121,6 +125,8 @@ def perman(mat, algo: int = 4, sparse: bool = False, gpu_num: int = 1, cpu: bool
     pattern-specialised segmented walk (-1 never, 0 auto, 1 when it is cheaper).
     ``kernel`` overrides the algorithm id's walk family ("dense", "sparse",
     "skip", "dense_plain", "seg") and keeps its device schedule.
+    ``checkpoint`` (chunk-queue ids 6 / 8 only): a file recording each finished
+    queue item; a later call with the same file resumes from it (same bits).
     """
     table = ALGOS_SPARSE if sparse else ALGOS_DENSE
     if algo not in table:
@@ -134,7 +140,7 @@ def perman(mat, algo: int = 4, sparse: bool = False, gpu_num: int = 1, cpu: bool
         gpu_num = 1
     a, dt, n = _mat(mat)
     lib = _lib.load()
-    o = _opts(gpu_num, device_id, threads, cpu, walk_log2, chunk_log2, use_rccl, jit=jit)
+    o = _opts(gpu_num, device_id, threads, cpu, walk_log2, chunk_log2, use_rccl, jit=jit, checkpoint=checkpoint)
     out, st = C.c_double(0.0), SupStats()
     _lib.check(lib.sup_perman(a.ctypes.data, dt, n, kern, sched, C.byref(o), C.byref(out), C.byref(st)),
                table[algo][0])

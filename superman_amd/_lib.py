@@ -57,7 +57,7 @@ class SupOpts(C.Structure):
         ("gpu_num", C.c_int), ("device_id", C.c_int), ("threads", C.c_int),
         ("cpu_worker", C.c_int), ("grid_dim", C.c_int), ("block_dim", C.c_int),
         ("walk_log2", C.c_int), ("chunk_log2", C.c_int), ("use_rccl", C.c_int),
-        ("verbose", C.c_int), ("jit", C.c_int),
+        ("verbose", C.c_int), ("jit", C.c_int), ("checkpoint", C.c_char_p),
     ]
 
 
@@ -90,11 +90,11 @@ class SupStats(C.Structure):
         ("devices_used", C.c_int), ("lane_bits", C.c_int), ("walk_bits", C.c_int),
         ("grid", C.c_int), ("chunks_done_cpu", C.c_int), ("partials", C.c_double * 16),
         ("walk_kind", C.c_int), ("leaves", C.c_int), ("est_ops_per_step", C.c_double),
-        ("jit_ms", C.c_double),
+        ("jit_ms", C.c_double), ("items_resumed", C.c_int), ("reserved_", C.c_int),
     ]
 
     def as_dict(self) -> dict:
-        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "partials"}
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f not in ("partials", "reserved_")}
         d["partials"] = list(self.partials[: max(1, self.devices_used)])
         return d
 
@@ -129,7 +129,7 @@ def load() -> C.CDLL:
             build()
         lib = C.CDLL(LIB_PATH)
         _declare(lib)
-        if lib.sup_abi_version() != 5:
+        if lib.sup_abi_version() != 6:
             raise RuntimeError("libsuperman_hip.so ABI version mismatch")
         _lib = lib
         return lib

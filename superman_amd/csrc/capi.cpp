@@ -62,6 +62,7 @@ void fill_stats(sup_stats* st, const Plan& P, const SchedResult& r, double wall_
   st->leaves = 1;
   st->est_ops_per_step = walk_cost(P);
   st->jit_ms = r.compile_ms;
+  st->items_resumed = r.items_resumed;
 }
 
 }  // namespace
@@ -364,23 +365,7 @@ int sup_plan_key(const void* mat, sup_dtype t, int n, sup_kernel kernel, const s
   Plan P;
   if ((rc = check_walk_opts(o))) return rc;
   if ((rc = plan_for(A.data(), n, kernel, layout_for(n, o), P, o.jit, o.gpu_num, o.device_id))) return rc;
-  // everything that decides which wave-chunk sums which subsets, in what
-  // order and with which operations: walk kind, layout, column map, the
-  // signed column table, the segmented walk's choices and its kernel source
-  uint64_t h = 1469598103934665603ull;
-  auto mix = [&h](const void* p, size_t bytes) {
-    const unsigned char* c = (const unsigned char*)p;
-    for (size_t i = 0; i < bytes; ++i) h = (h ^ c[i]) * 1099511628211ull;
-  };
-  const int32_t head[] = {P.n, (int32_t)P.kind, (int32_t)P.lds, P.lay.L, P.lay.m, P.lay.h, P.seg_cc, P.seg_b,
-                          P.seg_budget, P.seg_kp};
-  mix(head, sizeof head);
-  mix(P.colmap.data(), P.colmap.size() * sizeof(int));
-  mix(P.cols.data(), P.cols.size() * sizeof(double));
-  mix(P.x0.data(), P.x0.size() * sizeof(double));
-  mix(&P.jit_key, sizeof P.jit_key);
-  mix(P.jtab.data(), P.jtab.size() * sizeof(double));
-  *key = h;
+  *key = plan_fingerprint(P);
   return SUP_OK;
 }
 
@@ -626,6 +611,10 @@ int sup_perman_reduced(const void* mat, sup_dtype t, int n, sup_kernel kernel, s
   c.sched = sched;
   if (o_in) c.o = *o_in;
   else sup_opts_init(&c.o);
+  if (c.o.checkpoint && *c.o.checkpoint) {  // one file per computation; a reduction runs many
+    set_error("sup_perman_reduced: checkpoint files are for one permanent (sup_perman with SUP_SCHED_CHUNKS)");
+    return SUP_EUNSUPPORTED;
+  }
   c.on_cpu = on_cpu;
   sup_reduce_opts r;
   if (r_in) r = *r_in;

@@ -608,6 +608,26 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
   return SUP_OK;
 }
 
+uint64_t plan_fingerprint(const Plan& P) {
+  // everything that decides which wave-chunk sums which subsets, in what
+  // order and with which operations: walk kind, layout, column map, the
+  // signed column table, the segmented walk's choices and its kernel source
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&h](const void* p, size_t bytes) {
+    const unsigned char* c = (const unsigned char*)p;
+    for (size_t i = 0; i < bytes; ++i) h = (h ^ c[i]) * 1099511628211ull;
+  };
+  const int32_t head[] = {P.n, (int32_t)P.kind, (int32_t)P.lds, P.lay.L, P.lay.m, P.lay.h, P.seg_cc, P.seg_b,
+                          P.seg_budget, P.seg_kp};
+  mix(head, sizeof head);
+  mix(P.colmap.data(), P.colmap.size() * sizeof(int));
+  mix(P.cols.data(), P.cols.size() * sizeof(double));
+  mix(P.x0.data(), P.x0.size() * sizeof(double));
+  mix(&P.jit_key, sizeof P.jit_key);
+  mix(P.jtab.data(), P.jtab.size() * sizeof(double));
+  return h;
+}
+
 double pairwise_host(const std::vector<double>& v) {
   if (v.empty()) return 0.0;
   size_t p = 1;
@@ -1107,6 +1127,79 @@ static int rccl_allreduce_slots(RcclSlots& r, std::vector<double>& merged) {
   return SUP_OK;
 }
 
+// ------------------------------------------------------------ checkpoint --
+// sup_opts::checkpoint: a text file, header "supckpt 1 <plan fingerprint>
+// <c0> <c1> <item> <nitems>", then one line "<item> <partial bits> <visited>"
+// per finished queue item, appended and flushed (fsync) as items finish.  On
+// open, an existing file with the same header lends its items (a torn last
+// line from an interrupted write is dropped) and is rewritten clean; another
+// header is refused.  Item partials are exact fp64 bit patterns and the items
+// are folded by the same pairwise tree, so a resumed run returns the
+// uninterrupted run's bits.
+struct Checkpoint {
+  FILE* f = nullptr;
+  std::mutex mu;
+  ~Checkpoint() {
+    if (f) std::fclose(f);
+  }
+};
+
+static int ckpt_open(const char* path, const char* head, uint64_t nitems, std::vector<double>& ipart,
+                     std::vector<char>& done, uint64_t& vis, int& resumed, Checkpoint& ck) {
+  std::string body = head;
+  if (FILE* in = std::fopen(path, "r")) {
+    char line[256];
+    const bool same = std::fgets(line, sizeof line, in) && std::strcmp(line, head) == 0;
+    while (same && std::fgets(line, sizeof line, in)) {
+      const size_t len = std::strlen(line);
+      unsigned long long i = 0, bits = 0, v = 0;
+      char tail = 0;
+      if (len == 0 || line[len - 1] != '\n' || std::sscanf(line, "%llu %llx %llu%c", &i, &bits, &v, &tail) != 4 ||
+          i >= nitems)
+        break;  // torn or foreign line: stop at it
+      if (done[i]) continue;
+      done[i] = 1;
+      std::memcpy(&ipart[i], &bits, sizeof bits);
+      vis += v;
+      ++resumed;
+      body += line;
+    }
+    std::fclose(in);
+    if (!same) {
+      set_error(std::string("checkpoint ") + path + " belongs to another computation (plan, chunk range or item "
+                "size differ); remove it or pass another file");
+      return SUP_EINVAL;
+    }
+  }
+  // rewrite header + the lines kept, then append from there
+  const std::string tmp = std::string(path) + ".tmp" + std::to_string(::getpid());
+  FILE* w = std::fopen(tmp.c_str(), "w");
+  if (!w || std::fwrite(body.data(), 1, body.size(), w) != body.size() || std::fflush(w) != 0 ||
+      ::fsync(fileno(w)) != 0 || std::fclose(w) != 0 || std::rename(tmp.c_str(), path) != 0) {
+    set_error(std::string("checkpoint ") + path + ": cannot write it");
+    return SUP_EIO;
+  }
+  if (!(ck.f = std::fopen(path, "a"))) {
+    set_error(std::string("checkpoint ") + path + ": cannot append to it");
+    return SUP_EIO;
+  }
+  return SUP_OK;
+}
+
+static int ckpt_record(Checkpoint& ck, uint64_t it, double part, uint64_t visited) {
+  if (!ck.f) return SUP_OK;
+  uint64_t bits;
+  std::memcpy(&bits, &part, sizeof bits);
+  std::lock_guard<std::mutex> g(ck.mu);
+  if (std::fprintf(ck.f, "%llu %016llx %llu\n", (unsigned long long)it, (unsigned long long)bits,
+                   (unsigned long long)visited) < 0 ||
+      std::fflush(ck.f) != 0 || ::fsync(fileno(ck.f)) != 0) {
+    set_error("checkpoint: write failed");
+    return SUP_EIO;
+  }
+  return SUP_OK;
+}
+
 // ------------------------------------------------------------ schedulers --
 int run_item_queue(uint64_t nitems, int takers, const std::function<int(int, uint64_t)>& take) {
   std::atomic<uint64_t> next{0};
@@ -1170,6 +1263,10 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   const bool want_visited = true;
 
   const bool rccl = (G > 1 && o.use_rccl) || o.use_rccl == 2;  // 2: also on one device (exercises RCCL)
+  if (sched != SUP_SCHED_CHUNKS && o.checkpoint && *o.checkpoint) {
+    set_error("a checkpoint file needs the chunk queue (-p6 / -p8, SUP_SCHED_CHUNKS)");
+    return SUP_EUNSUPPORTED;
+  }
   if (sched != SUP_SCHED_CHUNKS) {
     // Single device, a static contiguous split (-p5: G equal pieces, piece g
     // on device g), or the reference's manual distribution (-p66,
@@ -1252,12 +1349,31 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     while (item * 2 <= total && total / (item * 2) >= target_items) item <<= 1;
   }
   const uint64_t nitems = (total + item - 1) / item;
+  std::vector<double> ipart(nitems, 0.0);
+  // items an earlier, interrupted call recorded (sup_opts::checkpoint)
+  std::vector<char> done(nitems, 0);
+  uint64_t resumed_vis = 0;
+  Checkpoint ck;
+  const bool ckpt = o.checkpoint && *o.checkpoint;
+  if (ckpt) {
+    char head[200];
+    std::snprintf(head, sizeof head, "supckpt 1 %016llx %llu %llu %llu %llu\n",
+                  (unsigned long long)plan_fingerprint(P), (unsigned long long)c0, (unsigned long long)c1,
+                  (unsigned long long)item, (unsigned long long)nitems);
+    if ((rc = ckpt_open(o.checkpoint, head, nitems, ipart, done, resumed_vis, out.items_resumed, ck))) return rc;
+    if (o.verbose)
+      std::printf("Checkpoint %s: %d of %llu items resumed\n", o.checkpoint, out.items_resumed,
+                  (unsigned long long)nitems);
+  }
+  std::vector<uint64_t> pending;
+  for (uint64_t it = 0; it < nitems; ++it)
+    if (!done[it]) pending.push_back(it);
   // -R: device g writes the partial of every item it takes into slot `item`
-  // of its own buffer (the CPU worker's items have no device: host combine)
-  const bool rccl_items = rccl && !o.cpu_worker;
+  // of its own buffer (the CPU worker's items, and items resumed from a
+  // checkpoint, have no device: host combine)
+  const bool rccl_items = rccl && !o.cpu_worker && !ckpt;
   RcclSlots slots;
   if (rccl_items && (rc = rccl_slots_init(devs, nitems, slots))) return rc;
-  std::vector<double> ipart(nitems, 0.0);
   std::vector<double> dev_ms(G + 1, 0.0), dev_jit(G, 0.0);
   std::vector<uint64_t> dev_vis(G + 1, 0);
   std::vector<int> dev_grid(G + 1, 0);
@@ -1268,21 +1384,25 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     const uint64_t a = c0 + it * item;
     const uint64_t b = std::min(c1, a + item);
     auto t0 = std::chrono::steady_clock::now();
+    uint64_t vis = 0;
     if (g == G) {
       ipart[it] = cpu_walk_range(P, a, b, std::max(1, o.threads));
-      dev_vis[G] += (b - a) << (P.lay.L + P.lay.m);
+      vis = (b - a) << (P.lay.L + P.lay.m);
+      dev_vis[G] += vis;
       cpu_items.fetch_add(1);
     } else {
       RangeResult r;
       const int e = run_range(devs[g], P, a, b, want_visited, r, rccl_items ? slots.buf[g] + it : nullptr);
       if (e) return e;
       ipart[it] = r.partial;
+      vis = r.visited;
       dev_sum[g] += r.partial;
       dev_ms[g] += r.kernel_ms;
       dev_jit[g] += r.compile_ms;
       dev_vis[g] += r.visited;
       dev_grid[g] = std::max(dev_grid[g], r.grid);
     }
+    if (const int e = ckpt_record(ck, it, ipart[it], vis)) return e;
     if (o.verbose) {
       const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       if (g == G) std::printf("ChunkID %llu is DONE by CPU in %f\n", (unsigned long long)it, sec);
@@ -1290,9 +1410,12 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     }
     return SUP_OK;
   };
-  if ((rc = run_item_queue(nitems, G + (o.cpu_worker ? 1 : 0), take))) return rc;
+  if ((rc = run_item_queue(pending.size(), G + (o.cpu_worker ? 1 : 0),
+                          [&](int g, uint64_t q) { return take(g, pending[q]); })))
+    return rc;
   out.devices = G;
   out.cpu_items = cpu_items.load();
+  out.visited = resumed_vis;
   for (int g = 0; g < G; ++g) worker_jit_ms = std::max(worker_jit_ms, dev_jit[g]);
   for (int g = 0; g <= G; ++g) {
     out.kernel_ms = std::max(out.kernel_ms, dev_ms[g]);

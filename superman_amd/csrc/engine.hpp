@@ -249,10 +249,14 @@ struct SchedResult {
   int grid = 0;
   int cpu_items = 0;
   double compile_ms = 0.0;  // summed over devices
+  int items_resumed = 0;    // queue items taken from the checkpoint file (sup_opts::checkpoint)
   std::vector<double> dev_partials;
 };
 int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uint64_t c1,
              SchedResult& out);
+// 64-bit fingerprint of everything that decides a plan's sum and its rounding
+// (sup_plan_key; the checkpoint file's header)
+uint64_t plan_fingerprint(const Plan& P);
 
 // All-reduce (sum, fp64) over RCCL, in one process, of per-device vectors with
 // disjoint supports (exact in any order); merged = the slot-wise sum.

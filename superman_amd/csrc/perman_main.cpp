@@ -42,7 +42,7 @@ struct Cli {
   int scale_intervals = 4, scale_times = 5, gridm = 36, gridn = 36;
   unsigned long long seed = 1;
   int jit = 0;
-  std::string filename;
+  std::string filename, checkpoint;
 };
 
 int fail(const char* what) {
@@ -141,7 +141,8 @@ int main(int argc, char** argv) {
                                         {"seed", 1, NULL, 'S'},          {"jit", 1, NULL, 'J'},
                                         {"exact", 0, NULL, 'E'},         {"quad", 0, NULL, 'q'},
                                         {"halfCalc", 0, NULL, 'h'},      {"halfStore", 0, NULL, 'w'},
-                                        {"gridMultip", 1, NULL, 'e'},    {NULL, 0, NULL, 0}};
+                                        {"gridMultip", 1, NULL, 'e'},    {"checkpoint", 1, NULL, 'C'},
+                                        {NULL, 0, NULL, 0}};
   int opt;
   auto need_arg = [&](char o) -> bool {
     if (optarg[0] == '-') {
@@ -169,6 +170,7 @@ int main(int argc, char** argv) {
       case 'n': if (!need_arg('n')) return 1; c.gridn = std::atoi(optarg); break;
       case 'S': if (!need_arg('S')) return 1; c.seed = std::strtoull(optarg, nullptr, 10); break;
       case 'J': c.jit = std::atoi(optarg); break;  // may be negative: no need_arg
+      case 'C': if (!need_arg('C')) return 1; c.checkpoint = optarg; break;  // -p6 / -p8: resumable
       case 'i': c.grid_graph = true; break;
       case 'l': if (!need_arg('l')) return 1; c.device = std::atoi(optarg); break;
       case 'k': if (!need_arg('k')) return 1; c.reps = std::max(1, std::atoi(optarg)); break;
@@ -244,6 +246,7 @@ int main(int argc, char** argv) {
   o.use_rccl = c.rccl ? 1 : 0;
   o.verbose = c.verbose ? 1 : 0;
   o.jit = c.jit;
+  o.checkpoint = c.checkpoint.empty() ? nullptr : c.checkpoint.c_str();
 
   if (c.exact) {  // exact integer permanent (any -p: the sum does not depend on the kernel)
     if (c.scaling > 0.0) {
