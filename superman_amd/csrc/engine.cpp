@@ -1149,8 +1149,9 @@ static int ckpt_open(const char* path, const char* head, uint64_t nitems, std::v
   std::string body = head;
   if (FILE* in = std::fopen(path, "r")) {
     char line[256];
-    const bool same = std::fgets(line, sizeof line, in) && std::strcmp(line, head) == 0;
-    while (same && std::fgets(line, sizeof line, in)) {
+    const bool empty = !std::fgets(line, sizeof line, in);  // an empty file starts afresh
+    const bool same = empty || std::strcmp(line, head) == 0;
+    while (same && !empty && std::fgets(line, sizeof line, in)) {
       const size_t len = std::strlen(line);
       unsigned long long i = 0, bits = 0, v = 0;
       char tail = 0;

@@ -64,6 +64,10 @@ def test_checkpoint_records_and_resumes(sup, tmp_path):
         sup.perman(0.5 * a, 6, checkpoint=ck)
     with pytest.raises(sup.SupError, match="chunk queue"):
         sup.perman(a, 4, checkpoint=str(tmp_path / "other.ckpt"))
+    # an empty file (created beforehand) starts afresh
+    open(ck, "w").close()
+    r4, st4 = sup.perman(a, 6, checkpoint=ck, return_stats=True)
+    assert r4 == full and st4["items_resumed"] == 0 and _read(ck)[1] == parts
 
 
 def test_checkpoint_sparse_skipper_and_hybrid(sup, tmp_path):
