@@ -75,15 +75,19 @@ def test_checkpoint_sparse_skipper_and_hybrid(sup, tmp_path):
     k = sup.skip_order(a)[0]
     want = sup.perman(k, 8, sparse=True, jit=-1)
     ck = str(tmp_path / "skip.ckpt")
-    assert sup.perman(k, 8, sparse=True, jit=-1, checkpoint=ck) == want
+    # the item size is part of the header: fix it (2^9 wave-chunks, 16 items at n = 30) to resume on
+    # another device count (the default size follows the device count)
+    assert sup.perman(k, 8, sparse=True, jit=-1, checkpoint=ck, chunk_log2=9) == want
     lines, parts, _ = _read(ck)
     with open(ck, "w") as f:
         f.write("\n".join(lines[:3]) + "\n")
     # resumed by the devices and the hybrid CPU worker together (two logical devices on GPU 0)
     os.environ["SUP_DEVICE_MAP"] = "0,0"
     try:
-        got, st = sup.perman(k, 8, sparse=True, jit=-1, checkpoint=ck, gpu_num=2, cpu=True, threads=4,
-                             return_stats=True)
+        got, st = sup.perman(k, 8, sparse=True, jit=-1, checkpoint=ck, chunk_log2=9, gpu_num=2, cpu=True,
+                             threads=4, return_stats=True)
+        with pytest.raises(sup.SupError, match="another computation"):  # default item size for 2 devices
+            sup.perman(k, 8, sparse=True, jit=-1, checkpoint=ck, gpu_num=2)
     finally:
         del os.environ["SUP_DEVICE_MAP"]
     assert got == want and st["items_resumed"] == 2
