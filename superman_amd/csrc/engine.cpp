@@ -1136,16 +1136,10 @@ static int rccl_allreduce_slots(RcclSlots& r, std::vector<double>& merged) {
 // header is refused.  Item partials are exact fp64 bit patterns and the items
 // are folded by the same pairwise tree, so a resumed run returns the
 // uninterrupted run's bits.
-struct Checkpoint {
-  FILE* f = nullptr;
-  std::mutex mu;
-  ~Checkpoint() {
-    if (f) std::fclose(f);
-  }
-};
-
-static int ckpt_open(const char* path, const char* head, uint64_t nitems, std::vector<double>& ipart,
+int ckpt_open(const char* path, const char* head, uint64_t nitems, std::vector<double>& ipart,
                      std::vector<char>& done, uint64_t& vis, int& resumed, Checkpoint& ck) {
+  vis = 0;
+  resumed = 0;
   std::string body = head;
   if (FILE* in = std::fopen(path, "r")) {
     char line[256];
@@ -1187,7 +1181,7 @@ static int ckpt_open(const char* path, const char* head, uint64_t nitems, std::v
   return SUP_OK;
 }
 
-static int ckpt_record(Checkpoint& ck, uint64_t it, double part, uint64_t visited) {
+int ckpt_record(Checkpoint& ck, uint64_t it, double part, uint64_t visited) {
   if (!ck.f) return SUP_OK;
   uint64_t bits;
   std::memcpy(&bits, &part, sizeof bits);

@@ -5,6 +5,8 @@
 // on the host on every call.
 #pragma once
 #include <stdint.h>
+#include <cstdio>
+#include <mutex>
 #include <functional>
 #include <string>
 #include <vector>
@@ -254,6 +256,21 @@ struct SchedResult {
 };
 int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uint64_t c1,
              SchedResult& out);
+// Checkpoint file of the chunk queue (sup_opts::checkpoint; engine.cpp):
+// ckpt_open loads the items a file with header `head` records (marking them
+// in `done`, their partials in `ipart`) and leaves it open for appending;
+// ckpt_record appends one finished item (thread-safe, flushed and fsynced).
+struct Checkpoint {
+  FILE* f = nullptr;
+  std::mutex mu;
+  ~Checkpoint() {
+    if (f) std::fclose(f);
+  }
+};
+int ckpt_open(const char* path, const char* head, uint64_t nitems, std::vector<double>& ipart,
+              std::vector<char>& done, uint64_t& vis, int& resumed, Checkpoint& ck);
+int ckpt_record(Checkpoint& ck, uint64_t it, double part, uint64_t visited);
+
 // 64-bit fingerprint of everything that decides a plan's sum and its rounding
 // (sup_plan_key; the checkpoint file's header)
 uint64_t plan_fingerprint(const Plan& P);

@@ -20,7 +20,10 @@
 #include <cstring>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <unistd.h>
 
 #include "../../include/superman.h"
 #include "../../superman_amd/csrc/engine.hpp"
@@ -83,6 +86,60 @@ static void test_queue() {
   });
   CHECK(rc == SUP_EHIP);
   CHECK(std::strcmp(sup_last_error(), "item 500 failed on purpose") == 0);
+}
+
+// Checkpoint file of the chunk queue: concurrent appends, reload, a torn last
+// line dropped, a foreign header refused (engine.cpp ckpt_open / ckpt_record).
+static void test_checkpoint() {
+  char path[] = "/tmp/sup_selftest_ckpt_XXXXXX";
+  const int fd = mkstemp(path);
+  CHECK(fd >= 0);
+  close(fd);
+  const char* head = "supckpt 1 0123456789abcdef 0 4096 64 64\n";
+  const uint64_t N = 64;
+  std::vector<double> want(N);
+  for (uint64_t i = 0; i < N; ++i) want[i] = std::ldexp((double)(i * 2654435761u % 1000003u), -(int)(i % 50)) - 7.5;
+  {
+    std::vector<double> ip(N, 0.0);
+    std::vector<char> done(N, 0);
+    uint64_t vis = 0;
+    int resumed = -1;
+    sup::Checkpoint ck;
+    CHECK(sup::ckpt_open(path, head, N, ip, done, vis, resumed, ck) == SUP_OK);  // empty file: fresh
+    CHECK(resumed == 0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < 8; ++t)
+      th.emplace_back([&, t] {
+        for (uint64_t i = t; i < N; i += 8) CHECK(sup::ckpt_record(ck, i, want[i], 100 + i) == SUP_OK);
+      });
+    for (auto& x : th) x.join();
+  }
+  {
+    FILE* f = std::fopen(path, "a");  // an interrupted append
+    std::fputs("7 3ff00000", f);
+    std::fclose(f);
+  }
+  std::vector<double> ip(N, 0.0);
+  std::vector<char> done(N, 0);
+  uint64_t vis = 0;
+  int resumed = 0;
+  {
+    sup::Checkpoint ck;
+    CHECK(sup::ckpt_open(path, head, N, ip, done, vis, resumed, ck) == SUP_OK);
+  }
+  CHECK(resumed == (int)N);
+  CHECK(std::memcmp(ip.data(), want.data(), N * sizeof(double)) == 0);
+  CHECK(vis == 100 * N + N * (N - 1) / 2);
+  {
+    std::vector<double> ip2(N, 0.0);
+    std::vector<char> done2(N, 0);
+    uint64_t vis2 = 0;
+    int resumed2 = 0;
+    sup::Checkpoint ck;
+    CHECK(sup::ckpt_open(path, "supckpt 1 fedcba9876543210 0 4096 64 64\n", N, ip2, done2, vis2, resumed2, ck) ==
+          SUP_EINVAL);
+  }
+  std::remove(path);
 }
 
 static void test_host_walks() {
@@ -209,6 +266,7 @@ static void test_io_and_reductions(const std::string& root) {
 int main(int argc, char** argv) {
   const std::string root = argc > 1 ? argv[1] : ".";
   test_queue();
+  test_checkpoint();
   test_host_walks();
   test_planning(root);
   test_io_and_reductions(root);
