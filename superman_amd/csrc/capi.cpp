@@ -1,6 +1,9 @@
 // capi.cpp — extern "C" boundary (include/superman.h).
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "dd.hpp"
 #include "engine.hpp"
@@ -531,8 +534,7 @@ struct LeafCtx {
   bool first = true;
 };
 
-int engine_leaf(const double* a, int n, void* user, double* out) {
-  LeafCtx& c = *(LeafCtx*)user;
+int leaf_compute(const LeafCtx& c, const double* a, int n, double* out, sup_stats* st) {
   std::vector<double> m(a, a + (size_t)n * n);
   std::vector<int> rp(n), cp(n);
   int rc = SUP_OK;
@@ -540,10 +542,11 @@ int engine_leaf(const double* a, int n, void* user, double* out) {
   if (c.preprocessing == 1) rc = sup_sort_order(m.data(), SUP_FLOAT64, n, cp.data());
   else if (c.preprocessing == 2) rc = sup_skip_order(m.data(), SUP_FLOAT64, n, rp.data(), cp.data());
   if (rc) return rc;
-  sup_stats st;
-  rc = c.on_cpu ? sup_perman_cpu(m.data(), SUP_FLOAT64, n, c.kernel, c.o.threads, out, &st)
-                : sup_perman(m.data(), SUP_FLOAT64, n, c.kernel, c.sched, &c.o, out, &st);
-  if (rc) return rc;
+  return c.on_cpu ? sup_perman_cpu(m.data(), SUP_FLOAT64, n, c.kernel, c.o.threads, out, st)
+                  : sup_perman(m.data(), SUP_FLOAT64, n, c.kernel, c.sched, &c.o, out, st);
+}
+
+void leaf_accumulate(LeafCtx& c, const sup_stats& st) {
   if (c.first) {
     c.acc = st;
     c.first = false;
@@ -556,8 +559,15 @@ int engine_leaf(const double* a, int n, void* user, double* out) {
     c.acc.visited_steps += prev.visited_steps;
     c.acc.leaves += prev.leaves;
   }
-  return SUP_OK;
 }
+
+// Concurrent GPU leaves of sup_perman_reduced (SUP_LEAF_WORKERS overrides; 1 =
+// one leaf at a time, as the reference's RunAlgo per leaf).
+int leaf_workers() {
+  const char* e = std::getenv("SUP_LEAF_WORKERS");
+  return e ? std::max(1, std::min(kCtxLanes, std::atoi(e))) : 4;
+}
+
 }  // namespace
 
 int sup_perman_reduced_quad(const void* mat, sup_dtype t, int n, const sup_opts* o_in, int on_cpu,
@@ -622,7 +632,31 @@ int sup_perman_reduced(const void* mat, sup_dtype t, int n, sup_kernel kernel, s
   c.preprocessing = r.preprocessing;
   std::memset(&c.acc, 0, sizeof(c.acc));
   int leaves = 0;
-  const int rc = sup_decompose(mat, t, n, &r, engine_leaf, &c, out, &leaves);
+  // GPU leaves: leaf_workers() host threads, each on its own context lane of
+  // the devices (stream, buffers), so one leaf's planning, uploads, launch
+  // gaps and sync overlap the others' walks; host leaves (-c) one at a time
+  // (each uses the -t threads).  Same result bits either way: the combine is
+  // folded in the sequential order (decompose_batched).
+  if (!mat || !out || n < 1 || n > SUP_MAX_READ_N) {
+    set_error("sup_perman_reduced: bad argument");
+    return SUP_EINVAL;
+  }
+  std::vector<double> A((size_t)n * n);
+  for (size_t i = 0; i < A.size(); ++i)
+    A[i] = t == SUP_INT32 ? (double)((const int32_t*)mat)[i]
+           : t == SUP_FLOAT32 ? (double)((const float*)mat)[i] : ((const double*)mat)[i];
+  std::mutex smu;
+  const int rc = decompose_batched(A.data(), n, r, c.on_cpu ? 1 : leaf_workers(),
+                                   [&c, &smu](int w, const double* a, int k, double* v) {
+                                     set_ctx_lane(w);
+                                     sup_stats st;
+                                     const int e = leaf_compute(c, a, k, v, &st);
+                                     if (e) return e;
+                                     std::lock_guard<std::mutex> g(smu);
+                                     leaf_accumulate(c, st);
+                                     return SUP_OK;
+                                   },
+                                   out, &leaves);
   if (rc) return rc;
   if (st) {
     *st = c.acc;

@@ -22,9 +22,14 @@
 //     main.cpp:1036-1045, and reorders intermediate matrices in place);
 //   * an empty row/column after singleton removal returns 0 (the reference
 //     prints "Perman is 0" and exits, main.cpp:1089-1093).
+#include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
 #include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "dd.hpp"
@@ -254,6 +259,30 @@ struct DdOps {
   static V div(V a, double d) { return dd_div_d(a, d); }
 };
 
+// Deferred combine (decompose_batched): the decomposition records the fold it
+// would perform — zero, leaf i, a + b, a / d — as nodes in creation order, and
+// hands each leaf matrix to a worker as soon as it appears; once every leaf
+// value is in, the nodes are evaluated in creation order (children before
+// parents), which is the recursive fold's order of fp64 operations on the same
+// operands: the result equals DblOps's bit for bit.
+struct ENode {
+  int32_t op;  // 0 zero, 1 leaf a, 2 add(a, b), 3 div(a, d)
+  int32_t a, b;
+  double d;
+};
+struct ExprOps {
+  typedef int32_t V;
+  static thread_local std::vector<ENode>* T;
+  static V push(const ENode& e) {
+    T->push_back(e);
+    return (V)(T->size() - 1);
+  }
+  static V zero() { return push({0, 0, 0, 0.0}); }
+  static V add(V a, V b) { return push({2, a, b, 0.0}); }
+  static V div(V a, double d) { return push({3, a, 0, d}); }
+};
+thread_local std::vector<ENode>* ExprOps::T = nullptr;
+
 template <class Ops>
 struct Decomposer {
   typedef typename Ops::V V;
@@ -344,6 +373,94 @@ int check_reduce_opts(const sup_reduce_opts& r, const char* who) {
 }
 
 }  // namespace
+
+int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
+                      const std::function<int(int, const double*, int, double*)>& leaf, double* out, int* n_leaves) {
+  set_error("");
+  if (int rc = check_reduce_opts(r, "sup_perman_reduced")) return rc;
+  workers = std::max(1, workers);
+  struct Job {
+    std::vector<double> a;
+    int n;
+    double* slot;
+  };
+  std::mutex mu;
+  std::condition_variable cv_put, cv_get;
+  std::deque<Job> q;
+  std::deque<double> vals;  // leaf values by leaf id (references stay valid as it grows)
+  bool closed = false, failed = false;
+  int frc = SUP_OK;
+  std::string ferr;
+  const size_t cap = (size_t)workers * 4;
+  auto work = [&](int w) {
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv_get.wait(lk, [&] { return !q.empty() || closed; });
+        if (q.empty()) return;
+        j = std::move(q.front());
+        q.pop_front();
+      }
+      cv_put.notify_one();
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        if (failed) continue;  // drain without computing
+      }
+      const int e = leaf(w, j.a.data(), j.n, j.slot);
+      if (e) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!failed) failed = true, frc = e, ferr = sup_last_error();
+        cv_put.notify_all();
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int w = 0; w < workers; ++w) th.emplace_back(work, w);
+  std::vector<ENode> nodes;
+  ExprOps::T = &nodes;
+  Decomposer<ExprOps> d;
+  d.r = r;
+  d.fn = [&](const double* a, int k, int32_t* v) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv_put.wait(lk, [&] { return q.size() < cap || failed; });
+    if (failed) {
+      set_error(ferr);
+      return frc;
+    }
+    const int32_t id = (int32_t)vals.size();
+    vals.push_back(0.0);
+    q.push_back(Job{std::vector<double>(a, a + (size_t)k * k), k, &vals.back()});
+    lk.unlock();
+    cv_get.notify_one();
+    *v = ExprOps::push({1, id, 0, 0.0});
+    return SUP_OK;
+  };
+  Mat m;
+  m.n = n;
+  m.a.assign(A, A + (size_t)n * n);
+  const int32_t root = d.run(m);
+  ExprOps::T = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    closed = true;
+  }
+  cv_get.notify_all();
+  for (auto& t : th) t.join();
+  if (failed) {
+    set_error(ferr);
+    return frc;
+  }
+  if (d.rc) return d.rc;
+  std::vector<double> val(nodes.size(), 0.0);
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    const ENode& e = nodes[i];
+    val[i] = e.op == 1 ? vals[e.a] : e.op == 2 ? val[e.a] + val[e.b] : e.op == 3 ? val[e.a] / e.d : 0.0;
+  }
+  *out = val[root];
+  if (n_leaves) *n_leaves = d.leaves;
+  return SUP_OK;
+}
 
 int decompose_dd(const double* A, int n, const sup_reduce_opts& r,
                  const std::function<int(const double*, int, dd*)>& leaf, dd* out, int* n_leaves) {

@@ -673,7 +673,15 @@ struct DeviceCtx {
 };
 
 static std::mutex g_ctx_mu;
-static std::vector<std::unique_ptr<DeviceCtx>> g_ctx;
+static std::vector<std::unique_ptr<DeviceCtx>> g_ctx;  // [logical device * kCtxLanes + lane]
+
+// Context lane of the calling thread (set_ctx_lane): host threads that run
+// independent permanents at once on one device (the -o leaves, engine_leaf)
+// each take their own lane — own stream, buffers and queue counter — so their
+// launches, copies and syncs overlap instead of queueing on one context.
+static thread_local int t_ctx_lane = 0;
+void set_ctx_lane(int lane) { t_ctx_lane = std::max(0, std::min(kCtxLanes - 1, lane)); }
+int ctx_lane() { return t_ctx_lane; }
 
 // Logical devices.  Every device id of the API (sup_opts::device_id, the
 // devices of a multi-device schedule) is a logical id; SUP_DEVICE_MAP (a
@@ -738,14 +746,15 @@ static int get_ctx(int dev, DeviceCtx** out) {
     return SUP_ENODEV;
   }
   const int pd = phys_device(dev);
+  const size_t slot = (size_t)dev * kCtxLanes + (size_t)t_ctx_lane;
   std::lock_guard<std::mutex> g(g_ctx_mu);
-  if (g_ctx.size() < (size_t)cnt) g_ctx.resize(cnt);
-  if (g_ctx[dev] && g_ctx[dev]->phys != pd) {
+  if (g_ctx.size() < (size_t)cnt * kCtxLanes) g_ctx.resize((size_t)cnt * kCtxLanes);
+  if (g_ctx[slot] && g_ctx[slot]->phys != pd) {
     set_error("logical device " + std::to_string(dev) + " moved to another physical device (SUP_DEVICE_MAP "
               "changed after first use)");
     return SUP_EINVAL;
   }
-  if (!g_ctx[dev]) {
+  if (!g_ctx[slot]) {
     auto c = std::make_unique<DeviceCtx>();
     c->dev = dev;
     c->phys = pd;
@@ -761,9 +770,9 @@ static int get_ctx(int dev, DeviceCtx** out) {
     SUP_HIP(hipMalloc(&c->d_rowmask, SUP_MAX_N * sizeof(uint64_t)));
     SUP_HIP(hipMalloc(&c->d_counter, 64));
     SUP_HIP(hipMalloc(&c->d_result, 64));
-    g_ctx[dev] = std::move(c);
+    g_ctx[slot] = std::move(c);
   }
-  *out = g_ctx[dev].get();
+  *out = g_ctx[slot].get();
   return SUP_OK;
 }
 
@@ -1201,7 +1210,9 @@ int run_item_queue(uint64_t nitems, int takers, const std::function<int(int, uin
   std::atomic<bool> failed{false};
   std::vector<int> rcs(takers, SUP_OK);
   std::vector<std::string> errs(takers);  // g_err is thread_local: carry worker messages back
+  const int lane = t_ctx_lane;            // so is the context lane: the takers keep the caller's
   auto worker = [&](int t) {
+    t_ctx_lane = lane;
     while (!failed.load()) {
       const uint64_t it = next.fetch_add(1);
       if (it >= nitems) return;
@@ -1280,7 +1291,9 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     std::vector<RangeResult> rr(npieces);
     std::vector<int> rcs(G, SUP_OK);
     std::vector<std::string> errs(G);  // g_err is thread_local: carry worker messages back
+    const int lane = t_ctx_lane;
     auto work = [&](int g) {
+      t_ctx_lane = lane;
       auto t0 = std::chrono::steady_clock::now();
       for (int q = 0; q < npieces && !rcs[g]; ++q) {
         if (owner[q] != g) continue;

@@ -240,6 +240,12 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
 double pairwise_host(const std::vector<double>& v);
 
 int device_count(int* n);
+// Context lanes: up to kCtxLanes device contexts per logical device; a host
+// thread picks its lane with set_ctx_lane (default 0) and the schedulers'
+// threads inherit the caller's.
+constexpr int kCtxLanes = 8;
+void set_ctx_lane(int lane);
+int ctx_lane();
 int phys_device(int dev);  // logical -> physical (SUP_DEVICE_MAP; identity when unset)
 
 // Schedulers (one host thread per device).
@@ -313,6 +319,12 @@ void cpu_dd_range(const Plan& P, const std::vector<double>& x0dd, uint64_t c0, u
 // -o / -u reductions with double-double leaves and combine
 // (sup_perman_reduced_quad); leaf(a, n, &v) computes one leaf.
 struct dd;
+// -o / -u with leaves computed concurrently (sup_perman_reduced): leaf(worker,
+// a, n, &value) is called from `workers` host threads as the decomposition
+// produces leaves; the combine is folded afterwards in the recursive order, so
+// the result equals the sequential sup_decompose's bit for bit.
+int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
+                      const std::function<int(int, const double*, int, double*)>& leaf, double* out, int* n_leaves);
 int decompose_dd(const double* A, int n, const sup_reduce_opts& r,
                  const std::function<int(const double*, int, dd*)>& leaf, dd* out, int* n_leaves);
 // Permanent in double-double (sup_perman_quad): *hi + *lo.

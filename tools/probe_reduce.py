@@ -12,16 +12,19 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import superman_amd as S  # noqa: E402
 
 FIX = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "fixtures", "mtx")
-names = sys.argv[1:] or ["chesapeake.mtx", "will57.mtx", "dwt_59.mtx"]
+names = sys.argv[1:] or ["chesapeake.mtx", "will57.mtx"]
 warm = S.read_mtx(os.path.join(FIX, "chesapeake.mtx"))[0]
 for algo, sparse in ((4, False), (4, True)):
     S.perman_reduced(warm, algo=algo, sparse=sparse)  # n = 30 kernels loaded once
 for name in names:
     a = S.read_mtx(os.path.join(FIX, name))[0]
     for algo, sparse in ((4, False), (4, True)):
-        t = time.perf_counter()
-        v, st = S.perman_reduced(a, algo=algo, sparse=sparse, return_stats=True)
-        wall = time.perf_counter() - t
-        print(f"{name} n={a.shape[0]} algo={algo}{' -s' if sparse else ''}: {st['leaves']} leaves, wall {wall:.3f} s, "
-              f"walk kernels {st['kernel_ms'] / 1e3:.3f} s ({st['kernel_ms'] / 1e3 / wall:.0%}), "
-              f"{st['gray_steps'] / wall:.3e} Gray steps/s, perm {v!r}", flush=True)
+        for workers in ("1", "4", "8"):  # concurrent GPU leaves (context lanes), SUP_LEAF_WORKERS
+            os.environ["SUP_LEAF_WORKERS"] = workers
+            t = time.perf_counter()
+            v, st = S.perman_reduced(a, algo=algo, sparse=sparse, return_stats=True)
+            wall = time.perf_counter() - t
+            print(f"{name} n={a.shape[0]} algo={algo}{' -s' if sparse else ''} workers={workers}: {st['leaves']} leaves, "
+                  f"wall {wall:.3f} s, walk kernels {st['kernel_ms'] / 1e3:.3f} s "
+                  f"({st['kernel_ms'] / 1e3 / wall:.0%}), {st['gray_steps'] / wall:.3e} Gray steps/s, perm {v!r}",
+                  flush=True)
