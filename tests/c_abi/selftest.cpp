@@ -231,6 +231,33 @@ static void test_io_and_reductions(const std::string& root) {
     CHECK(sup_perman_reduced_exact(R.data(), SUP_FLOAT64, m, &o, 1, &r, red, sizeof red, nullptr) == SUP_OK);
     CHECK(sup_perman_exact(R.data(), SUP_FLOAT64, m, &o, 1, dir, sizeof dir, nullptr) == SUP_OK);
     CHECK(std::strcmp(red, dir) == 0);
+    // the deferred combine with concurrent leaf workers (sup_perman_reduced's
+    // GPU form) against the sequential callback fold: the same bits
+    auto leaf = [](const double* a, int k, double* v) {
+      return sup_perman_cpu(a, SUP_FLOAT64, k, SUP_KERNEL_DENSE, 2, v, nullptr);
+    };
+    double seq = 0.0, par = 0.0;
+    int ls = 0, lp = 0;
+    CHECK(sup_decompose(R.data(), SUP_FLOAT64, m, &r,
+                        [](const double* a, int k, void*, double* v) {
+                          return sup_perman_cpu(a, SUP_FLOAT64, k, SUP_KERNEL_DENSE, 2, v, nullptr);
+                        },
+                        nullptr, &seq, &ls) == SUP_OK);
+    CHECK(sup::decompose_batched(R.data(), m, r, 6, [&](int, const double* a, int k, double* v) { return leaf(a, k, v); },
+                                 &par, &lp) == SUP_OK);
+    CHECK(ls == lp && ls > 4 && std::memcmp(&seq, &par, sizeof seq) == 0);
+    // a failing leaf stops the decomposition and its message survives the worker thread
+    std::atomic<int> calls{0};
+    CHECK(sup::decompose_batched(R.data(), m, r, 4,
+                                 [&](int, const double*, int, double*) {
+                                   if (calls.fetch_add(1) == 2) {
+                                     sup::set_error("leaf 2 failed on purpose");
+                                     return SUP_EHIP;
+                                   }
+                                   return SUP_OK;
+                                 },
+                                 &par, &lp) == SUP_EHIP);
+    CHECK(std::strcmp(sup_last_error(), "leaf 2 failed on purpose") == 0);
   }
   std::vector<double> A = random_matrix(24, 0.3, 5, false);
   int cnt = 0;
