@@ -45,7 +45,7 @@ def test_concurrent_leaves_bitwise(sup, name, algo, sparse, prep, scale):
         assert st["leaves"] == st1["leaves"] and st["gray_steps"] == st1["gray_steps"]
     # the callback path: the same leaves, one at a time through sup_decompose
     if scale is None and prep == 0 and not sparse:
-        via_cb = sup.decompose(a, lambda m: sup.perman(m, algo), compress=True)
+        via_cb = sup.decompose(a, lambda m: sup.perman(m, algo), compress=True)[0]
         assert via_cb == one
 
 
