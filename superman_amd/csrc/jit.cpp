@@ -1393,6 +1393,11 @@ struct Gen {
     if (const char* e = std::getenv("SUP_JIT_PHASE"))
       if (std::atoi(e) > 0)
         o << "  if (blockIdx.x & 1u) __builtin_amdgcn_s_sleep(" << std::min(127, std::atoi(e)) << ");\n";
+    // experiment (SUP_JIT_PRIO=1): static issue priority for the odd
+    // workgroups' waves, so each SIMD's two waves (one per workgroup) stop
+    // trading VALU slots by age (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+    if (const char* e = std::getenv("SUP_JIT_PRIO"))
+      if (std::atoi(e) > 0) o << "  if (blockIdx.x & 1u) __builtin_amdgcn_s_setprio(" << std::min(3, std::atoi(e)) << ");\n";
     // A group's chunk partials (and walked-step counts) wait in LDS, not in
     // registers held across the walk loop: two fewer VGPR values live in the
     // loop (LDS is otherwise unused; 3 KB per block).
