@@ -20,6 +20,7 @@
 #include <cstring>
 #include <string>
 #include <atomic>
+#include <mutex>
 #include <thread>
 
 #include "engine.hpp"
@@ -325,24 +326,7 @@ struct ReducedExact {
   bool on_cpu;
   Big pos, neg;
   double kms = 0.0;
-  std::string err;
 };
-int reduced_leaf(const double* a, int n, void* user, double* out) {
-  ReducedExact* R = (ReducedExact*)user;
-  std::string s;
-  double kms = 0.0;
-  int used = 0;
-  const int rc = exact_perman(a, n, *R->o, R->on_cpu, s, &kms, &used);
-  if (rc) {
-    R->err = last_error();
-    return rc;
-  }
-  R->kms += kms;
-  const bool negative = !s.empty() && s[0] == '-';
-  (negative ? R->neg : R->pos).add(Big::from_dec(s));
-  *out = std::strtod(s.c_str(), nullptr);
-  return SUP_OK;
-}
 }  // namespace
 
 int exact_perman_reduced(const double* A, int n, const sup_opts& o, bool on_cpu, const sup_reduce_opts& r,
@@ -358,11 +342,27 @@ int exact_perman_reduced(const double* A, int n, const sup_opts& o, bool on_cpu,
   rr.compress = 1;
   double approx = 0.0;
   int nl = 0;
-  const int rc = sup_decompose(A, SUP_FLOAT64, n, &rr, reduced_leaf, &R, &approx, &nl);
-  if (rc) {
-    if (!R.err.empty()) set_error(R.err);
-    return rc;
-  }
+  // GPU leaves several at a time, each worker on its own context lane (as
+  // sup_perman_reduced); the exact sum does not depend on the order
+  std::mutex mu;
+  const char* lw = std::getenv("SUP_LEAF_WORKERS");
+  const int workers = on_cpu ? 1 : lw ? std::max(1, std::min(kCtxLanes, std::atoi(lw))) : 4;
+  const int rc = decompose_batched(A, n, rr, workers, [&](int w, const double* a, int k, double* v) {
+    set_ctx_lane(w);
+    std::string s;
+    double kms = 0.0;
+    int used = 0;
+    const int e = exact_perman(a, k, *R.o, R.on_cpu, s, &kms, &used);
+    if (e) return e;
+    const bool negative = !s.empty() && s[0] == '-';
+    Big b = Big::from_dec(s);
+    *v = std::strtod(s.c_str(), nullptr);
+    std::lock_guard<std::mutex> g(mu);
+    R.kms += kms;
+    (negative ? R.neg : R.pos).add(b);
+    return SUP_OK;
+  }, &approx, &nl);
+  if (rc) return rc;
   if (R.pos.cmp(R.neg) >= 0) {
     R.pos.sub(R.neg);
     out = R.pos.dec();
