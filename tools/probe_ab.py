@@ -20,8 +20,9 @@ import superman_amd as S  # noqa: E402
 CASES = [("double__40_0.50_0", 0, "dense"), ("double__36_0.20_0", 1, "sparse"), ("double__32_0.50_0", 0, "dense"),
          ("double__40_0.20_0", 0, "dense"), ("synth44_0.15_int", 2, "skip")]
 settings = ["-"] + sys.argv[1:]
-if os.environ.get("PROBE_CASES"):
-    CASES = [c for c in CASES if c[0] in os.environ["PROBE_CASES"].split(",")]
+if os.environ.get("PROBE_CASES"):  # fixture names; ones not listed above run as dense requests
+    want = os.environ["PROBE_CASES"].split(",")
+    CASES = [c for c in CASES if c[0] in want] + [(w, 0, "dense") for w in want if w not in [c[0] for c in CASES]]
 for name, prep, kernel in CASES:
     a = S.read_matrix(os.path.join("tests", "fixtures", name))[0]
     if prep == 1:
