@@ -589,17 +589,21 @@ int sup_perman_reduced_quad(const void* mat, sup_dtype t, int n, const sup_opts*
   else sup_reduce_opts_init(&r);
   double kms = 0.0;
   int used = 0;
-  auto leaf = [&](const double* a, int k, dd* v) {
+  std::mutex mu;
+  // GPU leaves several at a time on their own context lanes (as sup_perman_reduced)
+  auto leaf = [&](int w, const double* a, int k, dd* v) {
+    set_ctx_lane(w);
     double ms = 0.0;
     int u = 0;
     const int rc = quad_perman(a, k, o, on_cpu != 0, &v->hi, &v->lo, &ms, &u);
+    std::lock_guard<std::mutex> g(mu);
     kms += ms;
     used = std::max(used, u);
     return rc;
   };
   dd v{0.0, 0.0};
   int leaves = 0;
-  const int rc = decompose_dd(A.data(), n, r, leaf, &v, &leaves);
+  const int rc = decompose_dd_batched(A.data(), n, r, on_cpu ? 1 : leaf_workers(), leaf, &v, &leaves);
   if (rc) return rc;
   *out_hi = v.hi;
   if (out_lo) *out_lo = v.lo;

@@ -245,7 +245,7 @@ Mat scaled(const Mat& m, const std::vector<double>& rv, const std::vector<double
 }
 
 // Leaf values and their combine: fp64 (sup_decompose's callback) or
-// double-double (decompose_dd: -o / -u with -q leaves).
+// double-double (decompose_dd_batched: -o / -u with -q leaves).
 struct DblOps {
   typedef double V;
   static V zero() { return 0.0; }
@@ -374,20 +374,24 @@ int check_reduce_opts(const sup_reduce_opts& r, const char* who) {
 
 }  // namespace
 
-int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
-                      const std::function<int(int, const double*, int, double*)>& leaf, double* out, int* n_leaves) {
+namespace {
+template <class Ops>
+int batched(const double* A, int n, const sup_reduce_opts& r, int workers,
+            const std::function<int(int, const double*, int, typename Ops::V*)>& leaf, typename Ops::V* out,
+            int* n_leaves, const char* who) {
+  typedef typename Ops::V V;
   set_error("");
-  if (int rc = check_reduce_opts(r, "sup_perman_reduced")) return rc;
+  if (int rc = check_reduce_opts(r, who)) return rc;
   workers = std::max(1, workers);
   struct Job {
     std::vector<double> a;
     int n;
-    double* slot;
+    V* slot;
   };
   std::mutex mu;
   std::condition_variable cv_put, cv_get;
   std::deque<Job> q;
-  std::deque<double> vals;  // leaf values by leaf id (references stay valid as it grows)
+  std::deque<V> vals;  // leaf values by leaf id (references stay valid as it grows)
   bool closed = false, failed = false;
   int frc = SUP_OK;
   std::string ferr;
@@ -429,7 +433,7 @@ int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int work
       return frc;
     }
     const int32_t id = (int32_t)vals.size();
-    vals.push_back(0.0);
+    vals.push_back(Ops::zero());
     q.push_back(Job{std::vector<double>(a, a + (size_t)k * k), k, &vals.back()});
     lk.unlock();
     cv_get.notify_one();
@@ -452,31 +456,26 @@ int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int work
     return frc;
   }
   if (d.rc) return d.rc;
-  std::vector<double> val(nodes.size(), 0.0);
+  std::vector<V> val(nodes.size(), Ops::zero());
   for (size_t i = 0; i < nodes.size(); ++i) {
     const ENode& e = nodes[i];
-    val[i] = e.op == 1 ? vals[e.a] : e.op == 2 ? val[e.a] + val[e.b] : e.op == 3 ? val[e.a] / e.d : 0.0;
+    val[i] = e.op == 1 ? vals[e.a] : e.op == 2 ? Ops::add(val[e.a], val[e.b]) : e.op == 3 ? Ops::div(val[e.a], e.d)
+                                                                                           : Ops::zero();
   }
   *out = val[root];
   if (n_leaves) *n_leaves = d.leaves;
   return SUP_OK;
 }
+}  // namespace
 
-int decompose_dd(const double* A, int n, const sup_reduce_opts& r,
-                 const std::function<int(const double*, int, dd*)>& leaf, dd* out, int* n_leaves) {
-  set_error("");
-  if (int rc = check_reduce_opts(r, "sup_perman_reduced_quad")) return rc;
-  Decomposer<DdOps> d;
-  d.r = r;
-  d.fn = leaf;
-  Mat m;
-  m.n = n;
-  m.a.assign(A, A + (size_t)n * n);
-  const dd v = d.run(m);
-  if (d.rc) return d.rc;
-  *out = v;
-  if (n_leaves) *n_leaves = d.leaves;
-  return SUP_OK;
+int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
+                      const std::function<int(int, const double*, int, double*)>& leaf, double* out, int* n_leaves) {
+  return batched<DblOps>(A, n, r, workers, leaf, out, n_leaves, "sup_perman_reduced");
+}
+
+int decompose_dd_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
+                         const std::function<int(int, const double*, int, dd*)>& leaf, dd* out, int* n_leaves) {
+  return batched<DdOps>(A, n, r, workers, leaf, out, n_leaves, "sup_perman_reduced_quad");
 }
 
 }  // namespace sup

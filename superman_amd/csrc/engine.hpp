@@ -316,17 +316,17 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
                  double* parts, double* kernel_ms);
 void cpu_dd_range(const Plan& P, const std::vector<double>& x0dd, uint64_t c0, uint64_t c1, int threads,
                   double* parts);
-// -o / -u reductions with double-double leaves and combine
-// (sup_perman_reduced_quad); leaf(a, n, &v) computes one leaf.
 struct dd;
-// -o / -u with leaves computed concurrently (sup_perman_reduced): leaf(worker,
-// a, n, &value) is called from `workers` host threads as the decomposition
-// produces leaves; the combine is folded afterwards in the recursive order, so
-// the result equals the sequential sup_decompose's bit for bit.
+// -o / -u with leaves computed concurrently (sup_perman_reduced,
+// sup_perman_reduced_exact; decompose_dd_batched: double-double leaves and
+// combine, sup_perman_reduced_quad): leaf(worker, a, n, &value) is called from
+// `workers` host threads as the decomposition produces leaves; the combine is
+// folded afterwards in the recursive order, so the result equals the
+// sequential fold's bit for bit.
 int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
                       const std::function<int(int, const double*, int, double*)>& leaf, double* out, int* n_leaves);
-int decompose_dd(const double* A, int n, const sup_reduce_opts& r,
-                 const std::function<int(const double*, int, dd*)>& leaf, dd* out, int* n_leaves);
+int decompose_dd_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
+                         const std::function<int(int, const double*, int, dd*)>& leaf, dd* out, int* n_leaves);
 // Permanent in double-double (sup_perman_quad): *hi + *lo.
 int quad_perman(const double* A, int n, const sup_opts& o, bool on_cpu, double* hi, double* lo, double* kernel_ms,
                 int* devices_used);
