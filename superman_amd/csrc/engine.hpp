@@ -323,8 +323,11 @@ struct dd;
 // `workers` host threads as the decomposition produces leaves; the combine is
 // folded afterwards in the recursive order, so the result equals the
 // sequential fold's bit for bit.
+// memo: a leaf equal to an earlier one takes its value without a call (off
+// when the callback must see every leaf, e.g. to sum exact values itself).
 int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
-                      const std::function<int(int, const double*, int, double*)>& leaf, double* out, int* n_leaves);
+                      const std::function<int(int, const double*, int, double*)>& leaf, double* out, int* n_leaves,
+                      bool memo = true);
 int decompose_dd_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
                          const std::function<int(int, const double*, int, dd*)>& leaf, dd* out, int* n_leaves);
 // Permanent in double-double (sup_perman_quad): *hi + *lo.

@@ -361,7 +361,7 @@ int exact_perman_reduced(const double* A, int n, const sup_opts& o, bool on_cpu,
     R.kms += kms;
     (negative ? R.neg : R.pos).add(b);
     return SUP_OK;
-  }, &approx, &nl);
+  }, &approx, &nl, false);  // every leaf (repeats included) adds its exact value
   if (rc) return rc;
   if (R.pos.cmp(R.neg) >= 0) {
     R.pos.sub(R.neg);

@@ -172,3 +172,26 @@ def test_reduction_option_bounds(sup, orc):
     got, _ = sup.decompose(a, lambda m: float(orc.exact_perman(m.astype(np.int64))), compress=True, min_n=4,
                            max_deg=5)
     assert got == want
+
+
+def test_repeated_leaves_memo(sup):
+    """The batched decomposition (sup_perman_reduced) gives a leaf equal to an
+    earlier one that leaf's value without computing it again: the result is
+    the callback fold's bit for bit, and the exact form (which sums every leaf,
+    repeats included) still equals the direct exact permanent."""
+    import collections
+    rng = np.random.default_rng(25)
+    n = 26
+    a = np.where(rng.random((n, n)) < 0.14, rng.integers(1, 3, (n, n)), 0).astype(np.float64)
+    a[np.arange(n), rng.permutation(n)] = 1
+    seen = collections.Counter()
+
+    def leaf(m):
+        seen[hashlib.sha1(m.tobytes()).hexdigest()] += 1
+        return sup.perman_cpu(m, threads=2)
+
+    via_cb, _ = sup.decompose(a, leaf, compress=True, min_n=10)
+    assert sum(seen.values()) > len(seen)  # this reduction repeats a leaf
+    got, st = sup.perman_reduced(a, cpu=True, threads=2, compress=True, min_n=10, return_stats=True)
+    assert got == via_cb and st["leaves"] == sum(seen.values())
+    assert sup.perman_reduced_exact(a, cpu=True, threads=2, min_n=10) == sup.perman_exact(a, cpu=True, threads=2)
