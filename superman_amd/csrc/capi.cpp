@@ -561,11 +561,13 @@ void leaf_accumulate(LeafCtx& c, const sup_stats& st) {
   }
 }
 
-// Concurrent GPU leaves of sup_perman_reduced (SUP_LEAF_WORKERS overrides; 1 =
-// one leaf at a time, as the reference's RunAlgo per leaf).
+// Concurrent GPU leaves of sup_perman_reduced: one per context lane (8; dwt_59's
+// 145,798 n = 30 leaves: 85 s one at a time, 41 s with 4, 39 s with 8,
+// profiles/r3/probe_reduce_memo.log).  SUP_LEAF_WORKERS overrides; 1 = one leaf
+// at a time, as the reference's RunAlgo per leaf.
 int leaf_workers() {
   const char* e = std::getenv("SUP_LEAF_WORKERS");
-  return e ? std::max(1, std::min(kCtxLanes, std::atoi(e))) : 4;
+  return e ? std::max(1, std::min(kCtxLanes, std::atoi(e))) : kCtxLanes;
 }
 
 }  // namespace

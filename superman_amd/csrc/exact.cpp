@@ -346,7 +346,7 @@ int exact_perman_reduced(const double* A, int n, const sup_opts& o, bool on_cpu,
   // sup_perman_reduced); the exact sum does not depend on the order
   std::mutex mu;
   const char* lw = std::getenv("SUP_LEAF_WORKERS");
-  const int workers = on_cpu ? 1 : lw ? std::max(1, std::min(kCtxLanes, std::atoi(lw))) : 4;
+  const int workers = on_cpu ? 1 : lw ? std::max(1, std::min(kCtxLanes, std::atoi(lw))) : kCtxLanes;
   const int rc = decompose_batched(A, n, rr, workers, [&](int w, const double* a, int k, double* v) {
     set_ctx_lane(w);
     std::string s;
