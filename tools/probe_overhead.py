@@ -26,3 +26,21 @@ for n, jit in ((16, -1), (24, -1), (30, -1), (30, 1), (32, 1)):
     wall = (time.perf_counter() - t) / reps * 1e6
     print(f"n={n} jit={jit}: {wall:.1f} us per call, kernel {kms / reps * 1e3:.1f} us, "
           f"host/launch overhead {wall - kms / reps * 1e3:.1f} us", flush=True)
+
+# a new matrix every call, as the -o leaves are: planning + table upload each time
+# (tables staged through pinned memory; SUP_PAGEABLE_UPLOAD=1: copied from pageable memory)
+for n, pageable in ((24, 1), (24, 0), (30, 1), (30, 0)):
+    if pageable:
+        os.environ["SUP_PAGEABLE_UPLOAD"] = "1"
+    else:
+        os.environ.pop("SUP_PAGEABLE_UPLOAD", None)
+    mats = [rng.random((n, n)) * (rng.random((n, n)) < 0.4) + np.eye(n) for _ in range(200)]
+    S.perman(mats[0])
+    kms = 0.0
+    t = time.perf_counter()
+    for a in mats:
+        _, st = S.perman(a, return_stats=True)
+        kms += st["kernel_ms"]
+    wall = (time.perf_counter() - t) / len(mats) * 1e6
+    print(f"n={n} new matrix per call, {'pageable' if pageable else 'pinned'} upload: {wall:.1f} us per call, kernel {kms / len(mats) * 1e3:.1f} us, "
+          f"host/launch overhead {wall - kms / len(mats) * 1e3:.1f} us", flush=True)
