@@ -668,12 +668,6 @@ struct DeviceCtx {
   unsigned* d_counter = nullptr;
   double* d_result = nullptr;
   uint64_t tables_uid = 0;  // Plan::uid whose cols / x0 / nblk / rowmask / jtab the device holds
-  // pinned host memory: the plan tables are staged here and uploaded by DMA
-  // straight from it (pageable copies stage through the runtime, ~10 us
-  // each), and the 8-byte result comes back into h_result
-  char* h_stage = nullptr;
-  size_t h_stage_cap = 0;
-  double* h_result = nullptr;
   std::mutex mu;
   int occ[3][SUP_MAX_N + 1] = {};  // AOT kernels; segmented walk: jit_occupancy
 };
@@ -776,7 +770,6 @@ static int get_ctx(int dev, DeviceCtx** out) {
     SUP_HIP(hipMalloc(&c->d_rowmask, SUP_MAX_N * sizeof(uint64_t)));
     SUP_HIP(hipMalloc(&c->d_counter, 64));
     SUP_HIP(hipMalloc(&c->d_result, 64));
-    SUP_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_result), 64, hipHostMallocDefault));
     g_ctx[slot] = std::move(c);
   }
   *out = g_ctx[slot].get();
@@ -830,38 +823,13 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   // cached plan, buffers not reallocated) — repeated calls on one matrix
   // (bench steps, -p6 items, reduction leaves) skip five H2D copies
   if (P.uid == 0 || P.uid != c->tables_uid || c->d_cols != cols_before || c->d_jtab != jtab_before) {
-    // staged in the context's pinned buffer (free again: every call ends with
-    // a stream sync), then one DMA per table
-    struct Up {
-      void* dst;
-      const void* src;
-      size_t bytes;
-    } up[] = {{c->d_jtab, P.jtab.data(), seg ? P.jtab.size() * sizeof(double) : 0},
-              {c->d_cols, P.cols.data(), P.cols.size() * sizeof(double)},
-              {c->d_x0, P.x0.data(), P.x0.size() * sizeof(double)},
-              {c->d_nblk, P.nblk.data(), P.nblk.size() * sizeof(int)},
-              {c->d_rowmask, P.rowmask.data(), P.rowmask.size() * sizeof(uint64_t)}};
-    size_t total = 0;
-    for (const Up& u : up) total += (u.bytes + 255) & ~(size_t)255;
-    if (total > c->h_stage_cap) {
-      if (c->h_stage) SUP_HIP(hipHostFree(c->h_stage));
-      c->h_stage = nullptr;
-      c->h_stage_cap = 0;
-      SUP_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->h_stage), total, hipHostMallocDefault));
-      c->h_stage_cap = total;
-    }
-    size_t off = 0;
-    const bool pageable = std::getenv("SUP_PAGEABLE_UPLOAD") != nullptr;  // experiments: the copies before staging
-    for (const Up& u : up) {
-      if (!u.bytes) continue;
-      if (pageable) {
-        SUP_HIP(hipMemcpyAsync(u.dst, u.src, u.bytes, hipMemcpyHostToDevice, s));
-        continue;
-      }
-      std::memcpy(c->h_stage + off, u.src, u.bytes);
-      SUP_HIP(hipMemcpyAsync(u.dst, c->h_stage + off, u.bytes, hipMemcpyHostToDevice, s));
-      off += (u.bytes + 255) & ~(size_t)255;
-    }
+    if (seg)
+      SUP_HIP(hipMemcpyAsync(c->d_jtab, P.jtab.data(), P.jtab.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    SUP_HIP(hipMemcpyAsync(c->d_cols, P.cols.data(), P.cols.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    SUP_HIP(hipMemcpyAsync(c->d_x0, P.x0.data(), P.x0.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    SUP_HIP(hipMemcpyAsync(c->d_nblk, P.nblk.data(), P.nblk.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    SUP_HIP(hipMemcpyAsync(c->d_rowmask, P.rowmask.data(), P.rowmask.size() * sizeof(uint64_t),
+                           hipMemcpyHostToDevice, s));
     c->tables_uid = P.uid;
   }
   SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
@@ -945,14 +913,14 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   SUP_HIP(hipEventRecord(c->ev1, s));
   SUP_HIP(launch_pairwise_reduce(c->d_chunk, count, c->d_scratch, c->d_result, s));
   if (slot) SUP_HIP(hipMemcpyAsync(slot, c->d_result, sizeof(double), hipMemcpyDeviceToDevice, s));
-  SUP_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
+  double result = 0.0;
+  SUP_HIP(hipMemcpyAsync(&result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
   std::vector<unsigned> vis;
   if (visited) {
     vis.resize(count);
     SUP_HIP(hipMemcpyAsync(vis.data(), c->d_visited, count * sizeof(unsigned), hipMemcpyDeviceToHost, s));
   }
   SUP_HIP(hipStreamSynchronize(s));
-  const double result = *c->h_result;
   float ms = 0.f;
   SUP_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   r.partial = result;

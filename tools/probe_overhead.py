@@ -28,12 +28,10 @@ for n, jit in ((16, -1), (24, -1), (30, -1), (30, 1), (32, 1)):
           f"host/launch overhead {wall - kms / reps * 1e3:.1f} us", flush=True)
 
 # a new matrix every call, as the -o leaves are: planning + table upload each time
-# (tables staged through pinned memory; SUP_PAGEABLE_UPLOAD=1: copied from pageable memory)
-for n, pageable in ((24, 1), (24, 0), (30, 1), (30, 0)):
-    if pageable:
-        os.environ["SUP_PAGEABLE_UPLOAD"] = "1"
-    else:
-        os.environ.pop("SUP_PAGEABLE_UPLOAD", None)
+# (round 3: staging the uploads through pinned memory measured no difference,
+# 158 against 160 us at n = 24 and 269 against 274 us at n = 30 — the time is
+# the host's planning, profiles/r3/probe_overhead_newmatrix.log)
+for n in (24, 30):
     mats = [rng.random((n, n)) * (rng.random((n, n)) < 0.4) + np.eye(n) for _ in range(200)]
     S.perman(mats[0])
     kms = 0.0
@@ -42,5 +40,5 @@ for n, pageable in ((24, 1), (24, 0), (30, 1), (30, 0)):
         _, st = S.perman(a, return_stats=True)
         kms += st["kernel_ms"]
     wall = (time.perf_counter() - t) / len(mats) * 1e6
-    print(f"n={n} new matrix per call, {'pageable' if pageable else 'pinned'} upload: {wall:.1f} us per call, kernel {kms / len(mats) * 1e3:.1f} us, "
+    print(f"n={n} new matrix per call: {wall:.1f} us per call, kernel {kms / len(mats) * 1e3:.1f} us, "
           f"host/launch overhead {wall - kms / len(mats) * 1e3:.1f} us", flush=True)
