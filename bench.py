@@ -52,7 +52,9 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 (vector = matrix), MI355X_MICROARCH.md / 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU). Without WORLD_SIZE in the environment and N > 1, this process "
+                         "starts torch.distributed.run with N ranks as a child and forwards its output")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--matrix", default=os.path.join(ROOT, "tests", "fixtures", "double__40_0.50_0"))
@@ -339,11 +341,51 @@ def cpu_reference_config1(S, threads: int):
             "port_rel_diff": abs(port_perm - ref_perm) / abs(ref_perm)}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """`bench.py --gpus N` started by hand (no WORLD_SIZE): start N ranks, one
+    process per GPU, with torch.distributed.run as a CHILD process and return
+    its exit code.  Nothing here touches the GPU (torch.cuda.device_count()
+    does not initialise it on this image; `superman_amd` is not imported), so
+    the ranks own their devices; no exec.  Rank 0's JSON line reaches our
+    stdout unchanged (inherited file descriptors)."""
+    import subprocess
+    if not args.rehearse:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} asks for {n} ranks, one per GPU, but this node has {have} GPU(s); "
+                  f"use --rehearse to put all ranks on device 0", file=sys.stderr, flush=True)
+            return 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or n) // n)))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     global args
     args = parse()
     if args.pmc_child:
         return pmc_child(args)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and args.gpus is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: the launcher and the flag disagree",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.gpus is not None and args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr, flush=True)
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -375,6 +417,8 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    plan_keys = []  # every timed walk's per-rank plan fingerprints (all equal, or check_plans_agree raised)
+
     def timed(a, kernel=None, jit=None):
         """W untimed + K timed steps of one whole permanent of `a`; returns
         (elapsed max over ranks, permanent, mean walk-kernel ms, stats, compile ms)."""
@@ -386,7 +430,8 @@ def main():
         # plan + (segmented walk) hiprtc compile, once, before the timed region;
         # gpu_num = world so that --jit 0 decides as the N-rank plan would
         prep = S.prepare(a, kernel, jit=jit, gpu_num=world, device_id=dev)
-        check_plans_agree(S.plan_key(a, kernel, jit=jit, gpu_num=world, device_id=dev), rank, world, tdev)
+        keys = check_plans_agree(S.plan_key(a, kernel, jit=jit, gpu_num=world, device_id=dev), rank, world, tdev)
+        plan_keys.append([hex(k) for k in keys])
 
         def step():
             part, st = S.perman_shard(a, rank, world, kernel=kernel, device_id=dev, return_stats=True,
@@ -546,6 +591,7 @@ def main():
         "roofline": roof,
         "permanent": perm,
         "kernel_ms_per_rank": rank_kms,
+        "plan_keys_per_rank": plan_keys[0],
         "densities": also,
         "configs": configs,
     }

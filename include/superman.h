@@ -145,6 +145,11 @@ void sup_opts_init(sup_opts* o);
 int         sup_abi_version(void);
 const char* sup_last_error(void);     /* thread-local message of the last failing call */
 int         sup_device_count(int* count);
+/* The physical HIP device of logical devices 0..ndev-1 as the -R RCCL combine
+ * uses them (its communicators, slot buffers and streams); SUP_DEVICE_MAP may
+ * permute or repeat physical ids, and SUP_ERCCL is returned when two logical
+ * devices share one GPU (RCCL needs distinct devices).  No HIP call. */
+int         sup_rccl_devices(int ndev, int* phys);
 
 /* ------------------------------------------------------------------------ *
  * Generic entry point.  `mat` is n x n row-major of type `t` (already

@@ -22,7 +22,7 @@ from ._lib import (KERNEL_DENSE, KERNEL_SKIPPER, KERNEL_SPARYSER, LEAF_FN, SCHED
 __all__ = [
     "perman", "perman_cpu", "partial", "perman_shard", "plan_info", "plan_key", "prepare", "read_matrix", "read_mtx", "sort_order",
     "skip_order", "compress", "decompose", "perman_reduced", "approx", "grid_graph", "ALGOS_APPROX",
-    "nw_start", "device_count", "layout", "SupError", "ALGOS_DENSE", "ALGOS_SPARSE",
+    "nw_start", "device_count", "rccl_devices", "layout", "SupError", "ALGOS_DENSE", "ALGOS_SPARSE",
     "gpu_perman64_xshared_coalescing_mshared",
     "gpu_perman64_xshared_coalescing_mshared_multigpu",
     "gpu_perman64_xshared_coalescing_mshared_multigpucpu_chunks",
@@ -100,6 +100,15 @@ def device_count() -> int:
     c = C.c_int(0)
     rc = lib.sup_device_count(C.byref(c))
     return c.value if rc == 0 else 0
+
+
+def rccl_devices(ndev: int) -> list:
+    """Physical devices the -R RCCL combine uses for logical devices
+    0..ndev-1 (SUP_DEVICE_MAP); raises SupError when two share a GPU."""
+    lib = _lib.load()
+    out = (C.c_int * max(1, ndev))()
+    _lib.check(lib.sup_rccl_devices(ndev, out), "rccl_devices")
+    return list(out[:ndev])
 
 
 def layout(n: int) -> tuple[int, int, int]:

@@ -87,6 +87,14 @@ int sup_device_count(int* count) {
   if (!count) return SUP_EINVAL;
   return device_count(count);
 }
+int sup_rccl_devices(int ndev, int* phys) {
+  if (ndev < 1 || ndev > 1024 || !phys) return SUP_EINVAL;
+  std::vector<int> devs(ndev), p;
+  for (int g = 0; g < ndev; ++g) devs[g] = g;
+  if (int rc = rccl_physical_devices(devs, p)) return rc;
+  std::copy(p.begin(), p.end(), phys);
+  return SUP_OK;
+}
 
 int sup_nw_start(const void* mat, sup_dtype t, int n, double* x0, double* p0) {
   if (!x0 || !p0) {

@@ -17,6 +17,8 @@
 #include <thread>
 #include <tuple>
 
+#include <elf.h>
+#include <link.h>  // dl_iterate_phdr: the library build id (checkpoint header)
 #include <unistd.h>  // environ
 
 namespace sup {
@@ -188,7 +190,19 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
     // bits the rest in matrix order.
     int segb = 0;
     std::vector<int> order;
-    if (kind == kWalkSeg && choice && (int)choice->order.size() == m + L) {
+    // a recorded order (plan choices on disk) is taken only when it is a set of
+    // m + L distinct flippable columns: a corrupted or foreign record would
+    // index past the matrix or give a column map that is not a permutation
+    auto valid_order = [&](const std::vector<int>& o) {
+      if ((int)o.size() != m + L) return false;
+      std::vector<char> seen(nb, 0);
+      for (int v : o) {
+        if (v < 0 || v >= nb || seen[v]) return false;
+        seen[v] = 1;
+      }
+      return true;
+    };
+    if (kind == kWalkSeg && choice && valid_order(choice->order) && choice->b >= 0 && choice->b <= m) {
       order = choice->order;
       segb = choice->b;
     } else {
@@ -1079,22 +1093,35 @@ struct RcclSlots {
   }
 };
 
-static int rccl_slots_init(const std::vector<int>& devs, size_t len, RcclSlots& r) {
-  r.devs.clear();
-  for (int d : devs) r.devs.push_back(phys_device(d));  // RCCL ranks are physical devices
-  std::vector<int> uniq = r.devs;
+// The physical device of each logical device in `devs` (RCCL ranks are
+// physical devices); a map that puts two of them on one GPU is refused.
+int rccl_physical_devices(const std::vector<int>& devs, std::vector<int>& phys) {
+  phys.clear();
+  for (int d : devs) phys.push_back(phys_device(d));
+  std::vector<int> uniq = phys;
   std::sort(uniq.begin(), uniq.end());
   if (std::adjacent_find(uniq.begin(), uniq.end()) != uniq.end()) {
-    r.devs.clear();
+    phys.clear();
     set_error("RCCL combine (-R) needs distinct physical devices; SUP_DEVICE_MAP puts several logical devices on "
               "one (use the host combine)");
     return SUP_ERCCL;
   }
-  r.len = len;
+  return SUP_OK;
+}
+
+static int rccl_slots_init(const std::vector<int>& devs, size_t len, RcclSlots& r) {
   r.buf.assign(devs.size(), nullptr);
   r.st.assign(devs.size(), nullptr);
-  for (size_t g = 0; g < devs.size(); ++g) {
-    SUP_HIP(hipSetDevice(devs[g]));
+  if (int rc = rccl_physical_devices(devs, r.devs)) {
+    r.buf.clear();
+    r.st.clear();
+    return rc;
+  }
+  r.len = len;
+  // buffers and streams on the communicator's (physical) device: r.devs, not
+  // the logical ids, which a permuted SUP_DEVICE_MAP ("1,0") maps elsewhere
+  for (size_t g = 0; g < r.devs.size(); ++g) {
+    SUP_HIP(hipSetDevice(r.devs[g]));
     SUP_HIP(hipMalloc(&r.buf[g], std::max<size_t>(len, 1) * sizeof(double)));
     SUP_HIP(hipStreamCreateWithFlags(&r.st[g], hipStreamNonBlocking));
     SUP_HIP(hipMemsetAsync(r.buf[g], 0, std::max<size_t>(len, 1) * sizeof(double), r.st[g]));
@@ -1138,14 +1165,56 @@ static int rccl_allreduce_slots(RcclSlots& r, std::vector<double>& merged) {
 }
 
 // ------------------------------------------------------------ checkpoint --
-// sup_opts::checkpoint: a text file, header "supckpt 1 <plan fingerprint>
-// <c0> <c1> <item> <nitems>", then one line "<item> <partial bits> <visited>"
+// sup_opts::checkpoint: a text file, header "supckpt 2 <plan fingerprint>
+// <library build id> <toolchain hash> <c0> <c1> <item> <nitems>", then one line "<item> <partial bits> <visited>"
 // per finished queue item, appended and flushed (fsync) as items finish.  On
 // open, an existing file with the same header lends its items (a torn last
 // line from an interrupted write is dropped) and is rewritten clean; another
 // header is refused.  Item partials are exact fp64 bit patterns and the items
 // are folded by the same pairwise tree, so a resumed run returns the
 // uninterrupted run's bits.
+// Identity of this library build: the ELF build-id note (--build-id=sha1, a
+// hash of the linked object: host code and every gfx950 code object in it)
+// of the shared object holding this function, folded to 64 bits; 0 if absent.
+static int build_id_cb(struct dl_phdr_info* info, size_t, void* data) {
+  auto* io = static_cast<std::pair<uintptr_t, uint64_t>*>(data);
+  bool mine = false;
+  for (int i = 0; i < info->dlpi_phnum && !mine; ++i) {
+    const ElfW(Phdr)& ph = info->dlpi_phdr[i];
+    const uintptr_t lo = info->dlpi_addr + ph.p_vaddr;
+    mine = ph.p_type == PT_LOAD && io->first >= lo && io->first < lo + ph.p_memsz;
+  }
+  if (!mine) return 0;
+  for (int i = 0; i < info->dlpi_phnum; ++i) {
+    const ElfW(Phdr)& ph = info->dlpi_phdr[i];
+    if (ph.p_type != PT_NOTE) continue;
+    const char* p = (const char*)(info->dlpi_addr + ph.p_vaddr);
+    const char* end = p + ph.p_memsz;
+    while (p + sizeof(ElfW(Nhdr)) <= end) {
+      const ElfW(Nhdr)* nh = (const ElfW(Nhdr)*)p;
+      const char* name = p + sizeof(ElfW(Nhdr));
+      const char* desc = name + ((nh->n_namesz + 3) & ~3u);
+      if (nh->n_type == NT_GNU_BUILD_ID && nh->n_namesz == 4 && std::memcmp(name, "GNU", 4) == 0) {
+        uint64_t h = 0xcbf29ce484222325ull;
+        for (unsigned k = 0; k < nh->n_descsz; ++k) h = (h ^ (unsigned char)desc[k]) * 1099511628211ull;
+        io->second = h;
+        return 1;
+      }
+      p = desc + ((nh->n_descsz + 3) & ~3u);
+    }
+  }
+  return 1;
+}
+
+uint64_t library_build_id() {
+  static const uint64_t id = [] {
+    std::pair<uintptr_t, uint64_t> io{(uintptr_t)(void*)&build_id_cb, 0};
+    dl_iterate_phdr(build_id_cb, &io);
+    return io.second;
+  }();
+  return id;
+}
+
 int ckpt_open(const char* path, const char* head, uint64_t nitems, std::vector<double>& ipart,
                      std::vector<char>& done, uint64_t& vis, int& resumed, Checkpoint& ck) {
   vis = 0;
@@ -1365,9 +1434,13 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   Checkpoint ck;
   const bool ckpt = o.checkpoint && *o.checkpoint;
   if (ckpt) {
-    char head[200];
-    std::snprintf(head, sizeof head, "supckpt 1 %016llx %llu %llu %llu %llu\n",
-                  (unsigned long long)plan_fingerprint(P), (unsigned long long)c0, (unsigned long long)c1,
+    // the plan's fingerprint, the library build (every ahead-of-time kernel's
+    // code object) and the hiprtc toolchain: partials from another binary are
+    // not mixed into a resumed run
+    char head[240];
+    std::snprintf(head, sizeof head, "supckpt 2 %016llx %016llx %016llx %llu %llu %llu %llu\n",
+                  (unsigned long long)plan_fingerprint(P), (unsigned long long)library_build_id(),
+                  (unsigned long long)jit_toolchain_hash(), (unsigned long long)c0, (unsigned long long)c1,
                   (unsigned long long)item, (unsigned long long)nitems);
     if ((rc = ckpt_open(o.checkpoint, head, nitems, ipart, done, resumed_vis, out.items_resumed, ck))) return rc;
     if (o.verbose)

@@ -247,6 +247,8 @@ constexpr int kCtxLanes = 8;
 void set_ctx_lane(int lane);
 int ctx_lane();
 int phys_device(int dev);  // logical -> physical (SUP_DEVICE_MAP; identity when unset)
+// physical devices of the RCCL combine over logical `devs`; SUP_ERCCL if two share a GPU
+int rccl_physical_devices(const std::vector<int>& devs, std::vector<int>& phys);
 
 // Schedulers (one host thread per device).
 struct SchedResult {

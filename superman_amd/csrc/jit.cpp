@@ -84,6 +84,7 @@
 #include <map>
 #include <queue>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <sstream>
 #include <tuple>
@@ -109,6 +110,36 @@ thread_local double t_compile_ms = 0.0;
 std::atomic<bool> g_jit_failed{false};
 // Budget candidates compiled at once (host threads) by the compiler check.
 constexpr size_t kMaxParallelCompiles = 8;
+// Process-wide gate on hiprtcCompileProgram: at most kMaxParallelCompiles
+// compiles run at once across every caller (budget ladders, -o leaf workers,
+// per-device threads of a multi-device schedule), and only one at a time once
+// any compile has failed — the batch limit alone did not bound compiles that
+// several callers start concurrently.
+class CompileGate {
+ public:
+  void enter() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return busy_ < (g_jit_failed.load() ? 1u : (unsigned)kMaxParallelCompiles); });
+    ++busy_;
+  }
+  void leave() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      --busy_;
+    }
+    cv_.notify_all();
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  unsigned busy_ = 0;
+};
+CompileGate g_compile_gate;
+struct CompileSlot {
+  CompileSlot() { g_compile_gate.enter(); }
+  ~CompileSlot() { g_compile_gate.leave(); }
+};
 // A kernel with no scratch at all is preferred over one whose spills stay in
 // the chunk start unless that one saves more than this fraction of the ops.
 constexpr double kScratchTolerance = 0.01;
@@ -1956,12 +1987,22 @@ int compile(const Plan& P, std::shared_ptr<std::vector<char>>& code) {
     const std::vector<std::string> opts = jit_opts();
     std::vector<const char*> optp;
     for (const std::string& x : opts) optp.push_back(x.c_str());
-    const hiprtcResult cr = hiprtcCompileProgram(prog, (int)optp.size(), optp.data());
+    hiprtcResult cr;
+    std::string log;
+    {
+      CompileSlot slot;  // process-wide limit on concurrent compiles (CompileGate)
+      cr = hiprtcCompileProgram(prog, (int)optp.size(), optp.data());
+      if (cr != HIPRTC_SUCCESS) {
+        size_t ls = 0;
+        hiprtcGetProgramLogSize(prog, &ls);
+        log.assign(ls, '\0');
+        if (ls) hiprtcGetProgramLog(prog, &log[0]);
+        // a failure other than the register retry below: serialise from here on,
+        // set before this slot frees so no further compile starts beside it
+        if (kp <= 1 || log.find("ran out of registers") == std::string::npos) g_jit_failed.store(true);
+      }
+    }
     if (cr == HIPRTC_SUCCESS) break;
-    size_t ls = 0;
-    hiprtcGetProgramLogSize(prog, &ls);
-    std::string log(ls, '\0');
-    if (ls) hiprtcGetProgramLog(prog, &log[0]);
     hiprtcDestroyProgram(&prog);
     if (kp > 1 && log.find("ran out of registers") != std::string::npos) {
       Plan Q = P;

@@ -95,7 +95,7 @@ static void test_checkpoint() {
   const int fd = mkstemp(path);
   CHECK(fd >= 0);
   close(fd);
-  const char* head = "supckpt 1 0123456789abcdef 0 4096 64 64\n";
+  const char* head = "supckpt 2 0123456789abcdef 0 0 0 4096 64 64\n";
   const uint64_t N = 64;
   std::vector<double> want(N);
   for (uint64_t i = 0; i < N; ++i) want[i] = std::ldexp((double)(i * 2654435761u % 1000003u), -(int)(i % 50)) - 7.5;
@@ -136,7 +136,7 @@ static void test_checkpoint() {
     uint64_t vis2 = 0;
     int resumed2 = 0;
     sup::Checkpoint ck;
-    CHECK(sup::ckpt_open(path, "supckpt 1 fedcba9876543210 0 4096 64 64\n", N, ip2, done2, vis2, resumed2, ck) ==
+    CHECK(sup::ckpt_open(path, "supckpt 2 fedcba9876543210 0 0 0 4096 64 64\n", N, ip2, done2, vis2, resumed2, ck) ==
           SUP_EINVAL);
   }
   std::remove(path);

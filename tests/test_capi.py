@@ -159,3 +159,22 @@ def test_cli_sparse_cpu_ids(sup):
         assert r.returncode == 0 and r.stdout.startswith(f"Result: {name} "), r.stdout + r.stderr
         outs[p] = float(r.stdout.splitlines()[1].split()[1])
     assert abs(outs[1] - outs[3]) <= 1e-12 * abs(outs[1])
+
+
+def test_rccl_devices_follow_a_permuted_map():
+    """The -R combine's communicators, slot buffers and streams all sit on the
+    physical device of each logical one (the slot buffers were
+    allocated on the logical ids).  A permuted SUP_DEVICE_MAP maps through;
+    a repeated physical id is refused; no map is the identity.  The map is read
+    per call, so each case runs in a fresh process."""
+    import subprocess
+    import sys
+    code = ("import superman_amd as S, sys\n"
+            "try:\n    print(S.rccl_devices(int(sys.argv[1])))\n"
+            "except S.SupError as e:\n    print('err', e.code)\n")
+    cases = [("1,0", 2, "[1, 0]"), ("2,3,0,1", 4, "[2, 3, 0, 1]"), ("", 3, "[0, 1, 2]"), ("0,0", 2, "err -4")]
+    for m, g, want in cases:
+        env = dict(os.environ, SUP_DEVICE_MAP=m, PYTHONPATH=ROOT)
+        r = subprocess.run([sys.executable, "-c", code, str(g)], capture_output=True, text=True, env=env,
+                           timeout=60)
+        assert r.stdout.strip() == want, (m, r.stdout, r.stderr)

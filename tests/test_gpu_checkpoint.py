@@ -19,8 +19,8 @@ pytestmark = pytest.mark.gpu
 def _read(path):
     lines = open(path).read().splitlines()
     head = lines[0].split()
-    assert head[:2] == ["supckpt", "1"]
-    nitems = int(head[6])
+    assert head[:2] == ["supckpt", "2"]  # plan key, library build id, toolchain, c0, c1, item, nitems
+    nitems = int(head[8])
     parts, vis = [None] * nitems, [0] * nitems
     for ln in lines[1:]:
         i, bits, v = ln.split()
@@ -106,4 +106,20 @@ def test_checkpoint_cli(sup, tmp_path):
     plain = run()
     assert run("--checkpoint", ck) == plain
     assert run("--checkpoint", ck, "-v") == plain  # every item resumed from the file
-    assert open(ck).read().startswith("supckpt 1 ")
+    assert open(ck).read().startswith("supckpt 2 ")
+
+
+def test_checkpoint_from_another_build_refused(sup, tmp_path):
+    """The header names the library build (ELF build id) and the hiprtc
+    toolchain beside the plan: a file written by another binary is refused
+    rather than mixed into a run that claims the uninterrupted bits."""
+    a, _, _ = sup.read_matrix(fixture_path("double__30_0.50_0"))
+    ck = str(tmp_path / "run.ckpt")
+    sup.perman(a, 6, checkpoint=ck)
+    lines = open(ck).read().splitlines()
+    head = lines[0].split()
+    assert int(head[3], 16) != 0  # the library carries a build id
+    head[3] = "%016x" % (int(head[3], 16) ^ 1)
+    open(ck, "w").write("\n".join([" ".join(head)] + lines[1:]) + "\n")
+    with pytest.raises(sup.SupError):
+        sup.perman(a, 6, checkpoint=ck)

@@ -68,3 +68,49 @@ def test_gpu_shards_allreduce_bitwise(world):
     assert steps * world == whole_steps == 1 << 31
     assert total == whole  # power-of-two shards are subtrees of the fixed pairwise tree
     assert all(res[r][0] == total for r in range(world))
+
+
+def _bench(args, env=None):
+    import json
+    import subprocess
+    import sys
+    e = dict(os.environ, **(env or {}))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=300, env=e)
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, lines
+
+
+_QUICK = ["--steps", "1", "--warmup", "0", "--configs", "0", "--cpu-seconds", "0", "--pmc", "0", "--cold", "0",
+          "--also", ""]
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`python3 bench.py --gpus 2` from plain python (no torchrun, no
+    WORLD_SIZE) starts the 2 ranks itself (torch.distributed.run as a child):
+    one JSON line with n_gpus 2, the ranks' plan keys equal, the permanent
+    bit-equal to the one-rank run."""
+    r2, out2 = _bench(["--gpus", "2", "--rehearse", *_QUICK])
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    assert len(out2) == 1, r2.stdout
+    rec2 = out2[0]
+    assert rec2["n_gpus"] == 2
+    keys = rec2["plan_keys_per_rank"]
+    assert len(keys) == 2 and keys[0] == keys[1]
+    r1, out1 = _bench(["--gpus", "1", *_QUICK])
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    assert len(out1) == 1 and out1[0]["n_gpus"] == 1
+    assert out1[0]["plan_keys_per_rank"] == [keys[0]]
+    assert rec2["permanent"] == out1[0]["permanent"]
+
+
+def test_bench_gpus_flag_refuses_missing_gpus():
+    """Without --rehearse, --gpus N on a node with fewer GPUs fails loudly
+    instead of measuring one rank."""
+    import torch
+    n = torch.cuda.device_count() + 1
+    r, out = _bench(["--gpus", str(n), *_QUICK])
+    assert r.returncode != 0 and not out
+    assert "GPU" in r.stderr
