@@ -135,7 +135,8 @@ typedef struct {
   double   est_ops_per_step;/* cost model: fp64 VALU ops per Gray step and lane                 */
   double   jit_ms;          /* hiprtc compile time spent by this call (0 when cached / unused)   */
   int      items_resumed;   /* queue items taken from sup_opts.checkpoint instead of walked      */
-  int      reserved_;
+  int16_t  seg_cached_bits; /* segmented walk (walk_kind 3): cached walk bits of the plan run    */
+  int16_t  seg_pair_bits;   /* segmented walk: specialised pair bits (0 for other walks)          */
 } sup_stats;
 
 /* Fill `o` with defaults. */

@@ -90,11 +90,12 @@ class SupStats(C.Structure):
         ("devices_used", C.c_int), ("lane_bits", C.c_int), ("walk_bits", C.c_int),
         ("grid", C.c_int), ("chunks_done_cpu", C.c_int), ("partials", C.c_double * 16),
         ("walk_kind", C.c_int), ("leaves", C.c_int), ("est_ops_per_step", C.c_double),
-        ("jit_ms", C.c_double), ("items_resumed", C.c_int), ("reserved_", C.c_int),
+        ("jit_ms", C.c_double), ("items_resumed", C.c_int), ("seg_cached_bits", C.c_int16),
+        ("seg_pair_bits", C.c_int16),
     ]
 
     def as_dict(self) -> dict:
-        d = {f: getattr(self, f) for f, _ in self._fields_ if f not in ("partials", "reserved_")}
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "partials"}
         d["partials"] = list(self.partials[: max(1, self.devices_used)])
         return d
 

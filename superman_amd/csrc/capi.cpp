@@ -66,6 +66,10 @@ void fill_stats(sup_stats* st, const Plan& P, const SchedResult& r, double wall_
   st->est_ops_per_step = walk_cost(P);
   st->jit_ms = r.compile_ms;
   st->items_resumed = r.items_resumed;
+  if (P.kind == kWalkSeg) {
+    st->seg_cached_bits = (int16_t)P.seg_cc;
+    st->seg_pair_bits = (int16_t)P.seg_b;
+  }
 }
 
 }  // namespace

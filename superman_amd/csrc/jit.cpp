@@ -1291,10 +1291,17 @@ struct Gen {
     auto load = [&](size_t r) {
       for (int pc : rp[r]) o << ind << "  jdbl8 " << pname(r, pc) << " = " << pieces[pc] << ";\n";
     };
+    // Pin at most kp pieces: a region holds one item that needs more (a
+    // near-dense D product reads up to 8 pieces, 128 SGPRs) — pinning all of
+    // them, beside the next region's prefetched pieces, asks for more SGPRs
+    // than a wave has ("inline assembly requires more registers than
+    // available", dense d = 0.9 at n >= 46).  The rest load unpinned; the
+    // operations and their order do not change.
     auto pin = [&](size_t r) {
       if (rp[r].empty()) return;
       o << ind << "  asm volatile(\"\" :";
-      for (size_t q = 0; q < rp[r].size(); ++q) o << (q ? ", " : " ") << "\"+s\"(" << pname(r, rp[r][q]) << ")";
+      const size_t np = std::min(rp[r].size(), (size_t)std::max(1, kp));
+      for (size_t q = 0; q < np; ++q) o << (q ? ", " : " ") << "\"+s\"(" << pname(r, rp[r][q]) << ")";
       o << ");\n";
     };
     o << ind << "{\n";
