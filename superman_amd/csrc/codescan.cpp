@@ -112,6 +112,9 @@ bool is_f64_valu(const std::string& t) {
   return starts(t, "v_add_f64") || starts(t, "v_mul_f64") || starts(t, "v_fma_f64") || starts(t, "v_fmac_f64");
 }
 bool is_scratch(const std::string& t) { return starts(t, "scratch_") || starts(t, "buffer_"); }
+// SGPR spill reloads: the allocator parks SGPRs in VGPR lanes (v_writelane) and
+// reads them back with v_readlane, a VALU instruction in the fp64 stream
+bool is_readlane(const std::string& t) { return starts(t, "v_readlane"); }
 
 }  // namespace
 
@@ -189,10 +192,11 @@ int scan_code_object(const std::vector<char>& co, const char* kernel, CodeScan* 
   }
   const int B = (int)bstart.size();
   std::vector<std::vector<int>> succ(B), pred(B);
-  std::vector<int> bf64(B, 0), bscr(B, 0), blen(B, 0);
+  std::vector<int> bf64(B, 0), bscr(B, 0), blen(B, 0), brl(B, 0);
   for (int b = 0; b < B; ++b) {
     const int lo = bstart[b], hi = b + 1 < B ? bstart[b + 1] : (int)ins.size();
-    for (int i = lo; i < hi; ++i) bf64[b] += is_f64_valu(ins[i].text), bscr[b] += is_scratch(ins[i].text);
+    for (int i = lo; i < hi; ++i)
+      bf64[b] += is_f64_valu(ins[i].text), bscr[b] += is_scratch(ins[i].text), brl[b] += is_readlane(ins[i].text);
     blen[b] = hi - lo;
     const Inst& last = ins[hi - 1];
     auto add = [&](int to) {
@@ -285,8 +289,9 @@ int scan_code_object(const std::vector<char>& co, const char* kernel, CodeScan* 
     r.loop_f64 = f64[walk];
     r.loop_scratch = 0;
     r.loop_insts = 0;
+    r.loop_readlane = 0;
     for (int b = 0; b < B; ++b)
-      if (body[b]) r.loop_scratch += bscr[b], r.loop_insts += blen[b];
+      if (body[b]) r.loop_scratch += bscr[b], r.loop_insts += blen[b], r.loop_readlane += brl[b];
   }
   *out = r;
   return SUP_OK;

@@ -551,6 +551,32 @@ static double auto_min_saving(const double* A, int n, const Layout& lay, int jit
   return c > 0.0 ? std::min(kJitMinSavingSec, std::max(kJitColdBarMin, 2.0 * c)) : kJitMinSavingSec;
 }
 
+// Auto mode's first decision per matrix and request, on disk (round 4).  The
+// bar above moves with the cache: a cold run keeps the ahead-of-time walk
+// where the search + compile would cost more than they save, and once a plan's
+// choices are recorded (a --jit 1 run, another rank) the same command would
+// specialise — a different operation order, so different last bits of an fp64
+// result between two runs of one command.  So auto mode records what it
+// decided the first time and later processes follow it (cold and warm runs
+// print the same bits; --jit 1 / -1 pick a walk explicitly).  Recorded only
+// where the decision can depend on the cache: auto mode (jit = 0) and a walk
+// long enough to save the warm bar (n >= 37 dense: the -o leaves never write).
+struct AutoRecord {
+  uint64_t key = 0;
+  int recorded = -1;  // -1: none (or not recordable), 0 / 1 as recorded
+  bool active = false;
+  AutoRecord(const double* A, int n, const Layout& lay, sup_kernel kernel, int ndev, int jit, double walk_s) {
+    active = jit == 0 && n >= kJitWarmMinN && walk_s >= kJitWarmSavingSec;
+    if (!active) return;
+    key = seg_disk_key(A, n, lay) ^ (0x9e3779b97f4a7c15ull * (uint64_t)(1 + (int)kernel)) ^
+          ((uint64_t)std::max(ndev, 1) << 48);
+    recorded = auto_decision_load(key);
+  }
+  void store(bool seg) const {
+    if (active && recorded < 0) auto_decision_store(key, seg ? 1 : 0);
+  }
+};
+
 static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit,
                              int ndev, int dev, double min_saving) {
   // candidates in preference order; the cheapest by walk_cost wins
@@ -570,20 +596,31 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
       for (size_t i = 0; i < (size_t)n * n && integral; ++i) integral = A[i] == std::floor(A[i]);
       const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
       double skip_cost = walk_cost(P) / (integral ? kSkipEfficiency : 1.0);  // f <= 1
-      // auto mode: no segmented plan (its search takes ~0.1-1 s) where even a
-      // free walk could not save the compile
-      if (jit < 1 && steps * skip_cost / kLaneOpsPerSec < min_saving) return SUP_OK;
+      const AutoRecord rec(A, n, lay, kernel, ndev, jit, steps * skip_cost / kLaneOpsPerSec);
+      if (rec.recorded == 0) return SUP_OK;
       Plan s;
-      if (make_seg(s) != SUP_OK) return SUP_OK;
-      if (walk_cost_eff(s) >= skip_cost) return SUP_OK;
-      if (jit < 1 && steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec < min_saving) return SUP_OK;
-      if (integral) {
-        const double f = skip_visited_fraction(P, dev);
-        if (f < 0.0) return SUP_OK;
-        skip_cost *= f;
+      if (rec.recorded == 1) {  // the recorded decision: the segmented walk (choices on disk)
+        if (make_seg(s) == SUP_OK) P = std::move(s);
+        return SUP_OK;
       }
-      const double saved = steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec;
-      if (walk_cost_eff(s) < skip_cost && (jit >= 1 || saved >= min_saving)) P = std::move(s);
+      auto decide = [&]() -> bool {
+        // auto mode: no segmented plan (its search takes ~0.1-1 s) where even a
+        // free walk could not save the compile
+        if (jit < 1 && steps * skip_cost / kLaneOpsPerSec < min_saving) return false;
+        if (make_seg(s) != SUP_OK) return false;
+        if (walk_cost_eff(s) >= skip_cost) return false;
+        if (jit < 1 && steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec < min_saving) return false;
+        if (integral) {
+          const double f = skip_visited_fraction(P, dev);
+          if (f < 0.0) return false;
+          skip_cost *= f;
+        }
+        const double saved = steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec;
+        return walk_cost_eff(s) < skip_cost && (jit >= 1 || saved >= min_saving);
+      };
+      const bool seg = decide();
+      if (seg) P = std::move(s);
+      rec.store(seg);
       return SUP_OK;
     }
     case SUP_KERNEL_DENSE_PLAIN: return make_plan(A, n, kWalkDense, false, lay, P);
@@ -609,14 +646,24 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
     Plan c;
     if (make_plan(A, n, kinds[i], false, lay, c) == SUP_OK && walk_cost(c) < walk_cost(best)) best = std::move(c);
   }
-  const bool may_save = std::ldexp(1.0, n - 1) / std::max(ndev, 1) * walk_cost(best) / kLaneOpsPerSec >=
-                        min_saving;  // auto mode: skip the segmented plan's search where it cannot pay
-  if (jit >= 0 && n >= 8 && lay.m >= 3 && (jit >= 1 || may_save)) {
+  const double best_s = std::ldexp(1.0, n - 1) / std::max(ndev, 1) * walk_cost(best) / kLaneOpsPerSec;
+  const bool may_save = best_s >= min_saving;  // auto mode: skip the segmented plan's search where it cannot pay
+  if (jit >= 0 && n >= 8 && lay.m >= 3) {
+    const AutoRecord rec(A, n, lay, kernel, ndev, jit, best_s);
     Plan s;
-    if (make_seg(s) == SUP_OK && walk_cost_eff(s) < walk_cost(best)) {
-      const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
-      const double saved = steps * (walk_cost(best) - walk_cost_eff(s)) / kLaneOpsPerSec;
-      if (jit >= 1 || saved >= min_saving) best = std::move(s);
+    if (rec.recorded == 1) {  // the recorded decision: the segmented walk (choices on disk)
+      if (make_seg(s) == SUP_OK) best = std::move(s);
+    } else if (rec.recorded < 0 && (jit >= 1 || may_save)) {
+      bool seg = false;
+      if (make_seg(s) == SUP_OK && walk_cost_eff(s) < walk_cost(best)) {
+        const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
+        const double saved = steps * (walk_cost(best) - walk_cost_eff(s)) / kLaneOpsPerSec;
+        seg = jit >= 1 || saved >= min_saving;
+        if (seg) best = std::move(s);
+      }
+      rec.store(seg);
+    } else if (rec.recorded < 0) {
+      rec.store(false);
     }
   }
   P = std::move(best);

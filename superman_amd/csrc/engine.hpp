@@ -164,6 +164,10 @@ bool seg_choice_exists(uint64_t key);
 double seg_cost_load();             // seconds of the last cold segmented plan on this host, -1 if none
 void seg_cost_store(double seconds);
 void seg_choice_store(uint64_t key, int m, const SegChoice& c);
+// Auto mode's (jit = 0) first decision for a matrix and request, recorded next
+// to the plan choices: 1 segmented walk, 0 ahead-of-time walk, -1 none yet.
+int auto_decision_load(uint64_t key);
+void auto_decision_store(uint64_t key, int seg);
 uint64_t jit_toolchain_hash();
 // Default specialised pair bits, min(m - 1, 5) (the walk loop is unrolled by
 // 2^b pair steps; walk bits > b share one straight-line step).  Plans choose
@@ -190,6 +194,7 @@ struct CodeScan {
   int vgprs = -1, vgpr_spills = -1, scratch_bytes = -1;  // .vgpr_count, .vgpr_spill_count, private segment
   int insts = 0, scratch_insts = 0, loops = 0;           // whole kernel
   int loop_scratch = -1, loop_f64 = 0, loop_insts = 0;   // the walk loop (-1: none found)
+  int loop_readlane = 0;                                 // its v_readlane (SGPR spill reloads)
 };
 int scan_code_object(const std::vector<char>& code, const char* kernel, CodeScan* out);
 // Compile (or fetch) P's kernel and scan it.

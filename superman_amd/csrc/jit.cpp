@@ -1398,7 +1398,11 @@ struct Gen {
         int same = -1;
         for (int c2 = 0; c2 < c && same < 0; ++c2)
           if (!cls_consts[c].empty() && cls_consts[c2] == cls_consts[c]) same = c2;
-        std::fprintf(stderr, ", class %d: %zu%s", c, cls_consts[c].size(), same >= 0 ? " (= earlier)" : "");
+        std::vector<double> u = cls_consts[c];
+        std::sort(u.begin(), u.end());
+        const size_t nd = (size_t)(std::unique(u.begin(), u.end()) - u.begin());
+        std::fprintf(stderr, ", class %d: %zu (%zu distinct)%s", c, cls_consts[c].size(), nd,
+                     same >= 0 ? " (= earlier)" : "");
       }
       std::fprintf(stderr, "\n");
     }
@@ -1876,9 +1880,9 @@ int build_seg(Plan& P, int fixed_budget) {
     if (std::getenv("SUP_JIT_VERBOSE"))
       for (size_t i : idx)
         if (done[i])
-          std::fprintf(stderr, "  budget %d: ops %.4f rc %d vgprs %d spills %d scratch %dB (loop %d of %d insts)%s\n",
+          std::fprintf(stderr, "  budget %d: ops %.4f rc %d vgprs %d spills %d scratch %dB (loop %d of %d insts, %d readlane)%s\n",
                        budgets[i], cand[i].seg_ops, src[i], scans[i].vgprs, scans[i].vgpr_spills,
-                       scans[i].scratch_bytes, scans[i].loop_scratch, scans[i].loop_insts,
+                       scans[i].scratch_bytes, scans[i].loop_scratch, scans[i].loop_insts, scans[i].loop_readlane,
                        (int)i == best ? "  <- chosen" : "");
     if (best < 0) {
       set_error("segmented walk: every budget's kernel touches scratch inside its walk loop (or fails to compile)");
@@ -2170,6 +2174,30 @@ void seg_choice_store(uint64_t key, int m, const SegChoice& c) {
   o << '\n';
   const std::string str = o.str();
   write_file_atomic(dir, "plan_" + key_hex(key) + ".txt", std::vector<char>(str.begin(), str.end()));
+}
+
+// Auto mode's decision: "supauto 1 <0|1>" in auto_<key>.txt.  Its bar moves
+// with the cache (a recorded plan makes specialising cheap), so the first
+// decision is kept: later processes running the same command walk the same
+// plan and print the same bits.
+int auto_decision_load(uint64_t key) {
+  const std::string dir = cache_dir();
+  if (dir.empty()) return -1;
+  std::vector<char> buf;
+  if (!read_file(dir + "/auto_" + key_hex(key) + ".txt", buf)) return -1;
+  buf.push_back('\0');
+  std::istringstream in(buf.data());
+  std::string tag;
+  int ver = 0, v = -1;
+  if (!(in >> tag >> ver >> v) || tag != "supauto" || ver != 1 || (v != 0 && v != 1)) return -1;
+  return v;
+}
+
+void auto_decision_store(uint64_t key, int seg) {
+  const std::string dir = cache_dir();
+  if (dir.empty()) return;
+  const std::string str = std::string("supauto 1 ") + (seg ? "1" : "0") + "\n";
+  write_file_atomic(dir, "auto_" + key_hex(key) + ".txt", std::vector<char>(str.begin(), str.end()));
 }
 
 // What a cold segmented plan (walk-order search + the compiler check's

@@ -264,3 +264,26 @@ def test_seg_config5_shards_balanced_gpu(sup):
     while len(parts) > 1:
         parts = [parts[i] + parts[i + 1] for i in range(0, len(parts), 2)]
     assert parts[0] == full
+
+
+def test_cli_auto_mode_same_bits_cold_and_warm(tmp_path):
+    """`perman -f double/40_0.50_0 -g -p4` (auto mode) with an empty cache,
+    then a --jit 1 run (records the segmented plan's choices), then the first
+    command again: the auto-mode runs print the same bits (the first decision
+    is recorded)."""
+    import os
+    import subprocess
+    from conftest import ROOT
+    exe = os.path.join(ROOT, "superman_amd", "bin", "perman")
+    env = dict(os.environ, SUP_JIT_CACHE_DIR=str(tmp_path))
+
+    def run(*extra):
+        out = subprocess.run([exe, "-f", fixture_path("double__40_0.50_0"), "-g", "-p4", *extra], capture_output=True,
+                             text=True, timeout=300, env=env, check=True).stdout
+        return [ln for ln in out.splitlines() if ln.startswith("Permanent:")][0]
+
+    cold = run()
+    jit1 = run("--jit", "1")
+    warm = run()
+    assert cold == warm
+    assert rel(float(jit1.split()[1]), float(cold.split()[1])) < 1e-9

@@ -6,7 +6,9 @@ at the edges (n = 10 and 64, a zero walk column, no rest rows)."""
 import numpy as np
 import pytest
 
-from conftest import fixture_path, rel
+import os
+
+from conftest import ROOT, fixture_path, rel
 
 
 def _rand(n, d, seed, ints=True):
@@ -94,15 +96,48 @@ def test_auto_cold_bar_follows_recorded_plan_cost(sup, tmp_path, monkeypatch):
     assert len(cost) == 1
     tag, ver, sec = cost[0].read_text().split()
     assert (tag, ver) == ("supcost", "1") and 0 < float(sec) < 600
-    # (each check on a new matrix of b's pattern: a matrix keeps its first auto-mode decision in a process)
+    # each check on a new zero pattern: auto mode's first decision for a pattern is recorded on
+    # disk and kept (test_auto_decision_recorded_across_processes)
     cost[0].write_text("supcost 1 5.0\n")  # a slow host: the bar stays at its 3 s cap
-    assert sup.plan_info(0.5 * b, "dense", jit=0)["kind"] == "sparse"
+    assert sup.plan_info(np.ascontiguousarray(a[::-1]), "dense", jit=0)["kind"] == "sparse"
     cost[0].write_text("supcost 1 0.01\n")  # a fast host: bar 0.25 s < the ~0.5 s the walk saves
-    assert sup.plan_info(0.25 * b, "dense", jit=0)["kind"] == "seg"
-    assert sup.plan_info(b, "dense", jit=0)["kind"] == "sparse"  # b's own first decision stands
+    assert sup.plan_info(np.ascontiguousarray(a[:, ::-1]), "dense", jit=0)["kind"] == "seg"
+    assert sup.plan_info(0.25 * b, "dense", jit=0)["kind"] == "sparse"  # b's pattern: its first decision stands
     cost[0].write_text("garbage\n")  # unreadable record: the 3 s default
-    c = np.ascontiguousarray(a[::-1])  # a third pattern
+    c = np.ascontiguousarray(a[::-1].T)  # another pattern
     assert sup.plan_info(c, "dense", jit=0)["kind"] == "sparse"
+
+
+def test_auto_decision_recorded_across_processes(tmp_path):
+    """Auto mode (jit = 0) decides from the cache's state; it records its first
+    decision per matrix and request, so the same command gives the same walk —
+    and the same bits — cold and warm.  Cold: no record,
+    the 3 s bar, the ahead-of-time walk.  A --jit 1 run then records the
+    segmented plan's choices, which would lower the bar to 0.1 s; the next auto
+    process still walks the ahead-of-time plan.  Where a --jit 1 run came
+    first, auto mode's first decision is the segmented walk, and it stays.
+    Each step is its own process (a process keeps its plans in memory)."""
+    import subprocess
+    import sys
+    code = ("import sys, numpy as np, superman_amd as S\n"
+            "a = S.read_matrix(sys.argv[1])[0]\n"
+            "if sys.argv[2] == 'T': a = np.ascontiguousarray(a.T)\n"
+            "print(S.plan_info(a, 'dense', jit=int(sys.argv[3]))['kind'])\n")
+    env = dict(os.environ, SUP_JIT_CACHE_DIR=str(tmp_path), SUP_JIT_BUDGET="190", PYTHONPATH=ROOT)
+
+    def kind(tr, jit):
+        r = subprocess.run([sys.executable, "-c", code, fixture_path("double__40_0.50_0"), tr, str(jit)],
+                           capture_output=True, text=True, env=env, timeout=300)
+        assert r.returncode == 0, r.stderr
+        return r.stdout.strip()
+
+    assert kind("N", 0) == "sparse"  # cold
+    assert kind("N", 1) == "seg"     # records the segmented plan's choices
+    assert kind("N", 0) == "sparse"  # warm: the recorded first decision, not the 0.1 s bar
+    assert len(list(tmp_path.glob("auto_*.txt"))) == 1
+    assert kind("T", 1) == "seg"     # another pattern, --jit 1 first
+    assert kind("T", 0) == "seg"     # warm bar: the first auto decision is the segmented walk
+    assert kind("T", 0) == "seg"
 
 
 def test_seg_cost_model_reported(sup):
