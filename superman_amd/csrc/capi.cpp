@@ -134,12 +134,13 @@ int sup_perman(const void* mat, sup_dtype t, int n, sup_kernel kernel, sup_sched
   else sup_opts_init(&o);
   std::vector<double> A;
   if ((rc = to_double(mat, t, n, A))) return rc;
-  Plan P;
   if ((rc = check_walk_opts(o))) return rc;
   const Layout lay = layout_for(n, o);
-  if ((rc = plan_for(A.data(), n, kernel, lay, P, o.jit, sched == SUP_SCHED_SINGLE ? 1 : o.gpu_num,
-                     o.device_id)))
+  std::shared_ptr<const Plan> sp;
+  if ((rc = plan_for_shared(A.data(), n, kernel, lay, sp, o.jit, sched == SUP_SCHED_SINGLE ? 1 : o.gpu_num,
+                            o.device_id)))
     return rc;
+  const Plan& P = *sp;
   SchedResult r;
   if ((rc = schedule(P, sched, o, 0, P.lay.chunks(), r))) return rc;
   *out = (double)(4 * (n & 1) - 2) * r.total;  // gpu_exact_dense.cu:698
@@ -227,8 +228,9 @@ int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int
   if ((rc = check_walk_opts(o))) return rc;
   std::vector<double> A;
   if ((rc = to_double(mat, t, n, A))) return rc;
-  Plan P;
-  if ((rc = plan_for(A.data(), n, kernel, layout_for(n, o), P, o.jit, nshards, o.device_id))) return rc;
+  std::shared_ptr<const Plan> sp;
+  if ((rc = plan_for_shared(A.data(), n, kernel, layout_for(n, o), sp, o.jit, nshards, o.device_id))) return rc;
+  const Plan& P = *sp;
   const uint64_t C = P.lay.chunks();
   const uint64_t c0 = C * (uint64_t)shard / (uint64_t)nshards, c1 = C * (uint64_t)(shard + 1) / (uint64_t)nshards;
   SchedResult r;

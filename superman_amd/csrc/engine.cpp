@@ -456,7 +456,9 @@ struct PlanKey {
   }
 };
 std::mutex g_plan_mu;
-std::map<PlanKey, std::pair<std::vector<double>, Plan>> g_plans;
+// cached plans are shared, not copied: a cached call takes a reference (the
+// segmented plan's source, tables and trees are ~200 KB at n = 40)
+std::map<PlanKey, std::pair<std::vector<double>, std::shared_ptr<const Plan>>> g_plans;
 constexpr size_t kPlanCacheMax = 32;
 
 // Hash of every SUP_JIT_* variable that shapes a plan or its generated source
@@ -478,7 +480,8 @@ uint64_t knob_hash() {
 
 static uint64_t knob_hash_env() { return knob_hash(); }
 
-int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit, int ndev, int dev) {
+int plan_for_shared(const double* A, int n, sup_kernel kernel, const Layout& lay, std::shared_ptr<const Plan>& out,
+                    int jit, int ndev, int dev) {
   const size_t nn = (size_t)n * n;
   uint64_t h = 1469598103934665603ull;
   for (size_t i = 0; i < nn; ++i) {
@@ -492,25 +495,34 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
     std::lock_guard<std::mutex> g(g_plan_mu);
     auto it = g_plans.find(key);
     if (it != g_plans.end() && std::equal(A, A + nn, it->second.first.begin())) {
-      P = it->second.second;
+      out = it->second.second;
       return SUP_OK;
     }
   }
-  const int rc = plan_for_uncached(A, n, kernel, lay, P, jit, ndev, dev, auto_min_saving(A, n, lay, jit));
+  auto P = std::make_shared<Plan>();
+  const int rc = plan_for_uncached(A, n, kernel, lay, *P, jit, ndev, dev, auto_min_saving(A, n, lay, jit));
   if (rc) return rc;
   std::lock_guard<std::mutex> g(g_plan_mu);
   {
     auto it = g_plans.find(key);  // another thread planned the same request meanwhile: its plan stands
     if (it != g_plans.end() && std::equal(A, A + nn, it->second.first.begin())) {
-      P = it->second.second;
+      out = it->second.second;
       return SUP_OK;
     }
   }
   if (g_plans.size() >= kPlanCacheMax) g_plans.clear();
   static uint64_t next_uid = 0;
-  P.uid = ++next_uid;
-  g_plans[key] = {std::vector<double>(A, A + nn), P};
+  P->uid = ++next_uid;
+  out = P;
+  g_plans[key] = {std::vector<double>(A, A + nn), out};
   return SUP_OK;
+}
+
+int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit, int ndev, int dev) {
+  std::shared_ptr<const Plan> sp;
+  const int rc = plan_for_shared(A, n, kernel, lay, sp, jit, ndev, dev);
+  if (rc == SUP_OK) P = *sp;
+  return rc;
 }
 
 // SkipPer evaluates only the states without an exactly-zero row; its jumps
@@ -729,6 +741,7 @@ struct DeviceCtx {
   size_t visited_cap = 0;
   unsigned* d_counter = nullptr;
   double* d_result = nullptr;
+  double* h_result = nullptr;  // pinned host slot: the result's D2H without a pageable staging copy
   uint64_t tables_uid = 0;  // Plan::uid whose cols / x0 / nblk / rowmask / jtab the device holds
   std::mutex mu;
   int occ[3][SUP_MAX_N + 1] = {};  // AOT kernels; segmented walk: jit_occupancy
@@ -832,6 +845,7 @@ static int get_ctx(int dev, DeviceCtx** out) {
     SUP_HIP(hipMalloc(&c->d_rowmask, SUP_MAX_N * sizeof(uint64_t)));
     SUP_HIP(hipMalloc(&c->d_counter, 64));
     SUP_HIP(hipMalloc(&c->d_result, 64));
+    SUP_HIP(hipHostMalloc(&c->h_result, 64, hipHostMallocDefault));
     g_ctx[slot] = std::move(c);
   }
   *out = g_ctx[slot].get();
@@ -975,8 +989,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   SUP_HIP(hipEventRecord(c->ev1, s));
   SUP_HIP(launch_pairwise_reduce(c->d_chunk, count, c->d_scratch, c->d_result, s));
   if (slot) SUP_HIP(hipMemcpyAsync(slot, c->d_result, sizeof(double), hipMemcpyDeviceToDevice, s));
-  double result = 0.0;
-  SUP_HIP(hipMemcpyAsync(&result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
+  SUP_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
   std::vector<unsigned> vis;
   if (visited) {
     vis.resize(count);
@@ -985,7 +998,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   SUP_HIP(hipStreamSynchronize(s));
   float ms = 0.f;
   SUP_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-  r.partial = result;
+  r.partial = *c->h_result;
   r.kernel_ms = ms;
   r.grid = (int)grid;
   if (visited) {

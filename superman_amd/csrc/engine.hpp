@@ -6,6 +6,7 @@
 #pragma once
 #include <stdint.h>
 #include <cstdio>
+#include <memory>
 #include <mutex>
 #include <functional>
 #include <string>
@@ -218,6 +219,10 @@ double walk_cost(const Plan& P);
 // fraction on (the decision itself does not depend on it).
 int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan& P, int jit = -1, int ndev = 1,
              int dev = 0);
+// The same, sharing the cached plan instead of copying it (the per-call path
+// of sup_perman / sup_perman_shard).
+int plan_for_shared(const double* A, int n, sup_kernel kernel, const Layout& lay, std::shared_ptr<const Plan>& P,
+                    int jit = -1, int ndev = 1, int dev = 0);
 
 struct RangeResult {
   double partial = 0.0;     // pairwise sum over the range's wave-chunks

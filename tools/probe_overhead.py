@@ -42,3 +42,23 @@ for n in (24, 30):
     wall = (time.perf_counter() - t) / len(mats) * 1e6
     print(f"n={n} new matrix per call: {wall:.1f} us per call, kernel {kms / len(mats) * 1e3:.1f} us, "
           f"host/launch overhead {wall - kms / len(mats) * 1e3:.1f} us", flush=True)
+
+# the bench's own call on config 2 (double/32_0.50_0, sup_perman_shard, segmented walk):
+# VERDICT r3 next-7 asks ms_per_step - kernel_ms <= 25 us
+a = S.read_matrix(os.path.join(ROOT, "tests", "fixtures", "double__32_0.50_0"))[0]
+S.prepare(a, "dense", jit=1)
+for _ in range(5):
+    S.perman_shard(a, 0, 1, jit=1)
+for label, stats in (("return_stats", True), ("value only", False)):
+    reps, kms = 300, 0.0
+    t = time.perf_counter()
+    for _ in range(reps):
+        if stats:
+            _, st = S.perman_shard(a, 0, 1, jit=1, return_stats=True)
+            kms += st["kernel_ms"]
+        else:
+            S.perman_shard(a, 0, 1, jit=1)
+    wall = (time.perf_counter() - t) / reps * 1e6
+    k = kms / reps * 1e3 if stats else float("nan")
+    print(f"config 2 perman_shard ({label}): {wall:.1f} us per call, kernel {k:.1f} us, "
+          f"host/launch overhead {wall - k:.1f} us", flush=True)
