@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SUP_ABI_VERSION 6
+#define SUP_ABI_VERSION 7  /* 7: sup_rccl_devices, sup_stats.seg_cached_bits / seg_pair_bits (round 4) */
 
 /* ---- error codes ------------------------------------------------------ */
 #define SUP_OK            0

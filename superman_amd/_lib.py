@@ -130,7 +130,7 @@ def load() -> C.CDLL:
             build()
         lib = C.CDLL(LIB_PATH)
         _declare(lib)
-        if lib.sup_abi_version() != 6:
+        if lib.sup_abi_version() != 7:
             raise RuntimeError("libsuperman_hip.so ABI version mismatch")
         _lib = lib
         return lib
