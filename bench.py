@@ -341,6 +341,33 @@ def cpu_reference_config1(S, threads: int):
             "port_rel_diff": abs(port_perm - ref_perm) / abs(ref_perm)}
 
 
+def reference_metric_run(matrix: str):
+    """The reference's own CPU code on the whole metric workload — committed,
+    not re-run here: oracle/_ref/ref_v2 (parallel_perman64<double,double>,
+    rev/cpu_algos.hpp:761-873, compiled from the reference sources) walked all
+    2^(n-1) steps of this file once in the build container (8 cores;
+    tests/golden/make_golden.py), ~68 min at n = 40.  Its result beside the
+    exact permanent shows the reference's own fp64 error at this size."""
+    name = os.path.basename(matrix)
+    try:
+        gold = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+        ex = json.load(open(os.path.join(ROOT, "tests", "golden", "exact_corpus.json")))
+    except (OSError, ValueError):
+        return None
+    key = f"{name}|dense|r0|b0|t8"
+    if key not in gold or key + "|seconds" not in gold:
+        return None
+    n = int(open(matrix).readline().split()[0])
+    sec = gold[key + "|seconds"]
+    out = {"value": float(1 << (n - 1)) / sec, "unit": "gray-steps/s", "cores": 8, "kind": "reference",
+           "seconds": sec, "permanent": gold[key],
+           "sample": f"all 2^{n - 1} steps of {name}, once, in the build container (8 cores, niced beside builds; "
+                     "committed in tests/golden/golden.json, not timed on this box)"}
+    if name in ex:
+        out["rel_err_vs_exact"] = abs(gold[key] - ex[name]) / abs(ex[name])
+    return out
+
+
 def _free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -623,6 +650,7 @@ def main():
         rec["cpu_baseline"] = cb_rec
         rec["rel_err_vs_cpu"] = err
         rec["cpu_baseline_reference_config1"] = cpu_reference_config1(S, cb_rec["cores"])
+        rec["cpu_reference_metric_matrix"] = reference_metric_run(args.matrix)
     else:
         rec["cpu_baseline"] = None
     if rank == 0 and world == 1 and args.cold:

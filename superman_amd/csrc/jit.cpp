@@ -1011,6 +1011,12 @@ struct Gen {
   std::vector<double> ctab;          // appended to P.jtab at cbase
   size_t cbase = 0;
   std::vector<int> kofs;             // per step class: offset (doubles, from cbase) of its stream
+  // per step class: position (doubles, from cbase) of its idx-th constant —
+  // kofs[c] + idx, or a place in another class's stream that holds the same
+  // value (share_streams: a class whose constants another stream already
+  // holds, in an order that costs no extra pieces, emits no stream of its own)
+  std::vector<std::vector<int>> cpos;
+  std::vector<char> own_stream;
   std::vector<std::vector<Stmt>> cls_stmts;
   std::vector<std::vector<double>> cls_consts;
   // which tree item holds row r: (tree 0 outer / 1 inner, item)
@@ -1207,8 +1213,14 @@ struct Gen {
         }
         const size_t e = t.find('@', q + 1);
         const int idx = std::atoi(t.substr(q + 1, e - q - 1).c_str());
-        const int pc = piece("((cjdbl8*)(jt + " + std::to_string((cbase + kofs[c]) * 8 + (idx / 8) * 64) + "u))[0]");
-        it.text += pref(pc, idx % 8);
+        const int pos = cpos[c][idx];
+        // a class reading another class's stream loads each piece through a
+        // fresh opaque base: otherwise LLVM merges the two steps' loads of the
+        // same piece and keeps them live across the block (SGPR spills)
+        static const bool fresh = std::getenv("SUP_JIT_FRESHBASE") && std::atoi(std::getenv("SUP_JIT_FRESHBASE"));
+        const std::string jb = own_stream[c] && !fresh ? "jt" : "(const char*)opaque_c(p.jtab, 0u)";
+        const int pc = piece("((cjdbl8*)(" + jb + " + " + std::to_string((cbase + pos - pos % 8) * 8) + "u))[0]");
+        it.text += pref(pc, pos % 8);
         if (std::find(it.pieces.begin(), it.pieces.end(), pc) == it.pieces.end()) it.pieces.push_back(pc);
         q = e;
       }
@@ -1366,10 +1378,83 @@ struct Gen {
     std::vector<double> t = ctab;
     t.resize((t.size() + 7) & ~(size_t)7, 0.0);
     for (size_t c = 0; c < cls_consts.size(); ++c) {
+      if (!own_stream[c]) continue;
       t.insert(t.end(), cls_consts[c].begin(), cls_consts[c].end());
       t.resize((t.size() + 7) & ~(size_t)7, 0.0);
     }
     return t;
+  }
+
+  // Positions in `pool` of the constants of `need`, in order: each is matched
+  // to the first occurrence of its value at or after the previous match
+  // (wrapping to the first occurrence), so a sequence that follows the pool's
+  // order reads it front to back.  Empty if some value is missing.  Matching
+  // by value is exact: the operand is that double either way.
+  static std::vector<int> match_stream(const std::vector<double>& need, const std::vector<double>& pool) {
+    std::map<uint64_t, std::vector<int>> where;
+    for (size_t i = 0; i < pool.size(); ++i) {
+      uint64_t k;
+      std::memcpy(&k, &pool[i], 8);
+      where[k].push_back((int)i);
+    }
+    std::vector<int> at;
+    int prev = -1;
+    for (double v : need) {
+      uint64_t k;
+      std::memcpy(&k, &v, 8);
+      auto it = where.find(k);
+      if (it == where.end()) return {};
+      const std::vector<int>& w = it->second;
+      auto nx = std::upper_bound(w.begin(), w.end(), prev);
+      prev = nx != w.end() ? *nx : w.front();
+      at.push_back(prev);
+    }
+    return at;
+  }
+  // Distinct 8-double pieces a run of positions touches, counted per run of
+  // consecutive equal pieces (what the step regions load).
+  static int piece_runs(const std::vector<int>& pos) {
+    int runs = 0, last = -1;
+    for (int p : pos)
+      if (p / 8 != last) ++runs, last = p / 8;
+    return runs;
+  }
+  // Stream sharing (round 4): a step class whose every constant another
+  // class's stream holds — near-dense walks re-form almost every copy on the
+  // top specialised step and on the shared step, the same constants in nearly
+  // the same order (double/40_0.90_0: 716 of them, 5.7 KB) — reads that
+  // stream instead of its own when that costs at most 1/8 more piece loads.
+  // The hot constant set then fits the 16 KB scalar cache better.  Same
+  // values, same operations: the results do not change.
+  void share_streams(std::vector<int>& host) const {
+    const int b = P.seg_b;
+    std::vector<int> order;
+    for (int c = 0; c <= b; ++c)
+      if (!cls_consts[c].empty()) order.push_back(c);
+    // larger streams host smaller ones
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int x, int y) { return cls_consts[x].size() > cls_consts[y].size(); });
+    for (size_t i = 1; i < order.size(); ++i) {
+      const int c = order[i];
+      for (size_t j = 0; j < i; ++j) {
+        const int h = order[j];
+        if (host[h] >= 0) continue;  // hosts keep their own stream
+        const std::vector<int> at = match_stream(cls_consts[c], cls_consts[h]);
+        if (at.empty()) continue;
+        std::vector<int> own(cls_consts[c].size());
+        for (size_t q = 0; q < own.size(); ++q) own[q] = (int)q;
+        // the host's pieces must be read front to back: a piece read again
+        // after others is one load to LLVM (same address, constant memory),
+        // held in SGPRs across the step (measured: 730 v_readlane spill
+        // reloads in the d = 0.9 walk loop when it was allowed)
+        bool forward = true;
+        for (size_t q = 1; q < at.size() && forward; ++q) forward = at[q] / 8 >= at[q - 1] / 8;
+        if (forward && 8 * piece_runs(at) <= 9 * piece_runs(own)) {
+          host[c] = h;
+          break;
+        }
+      }
+    }
   }
 
   std::string source() {
@@ -1385,11 +1470,27 @@ struct Gen {
     cls_consts.assign(b + 1, {});
     for (int c = cc; c <= b; ++c) build_class(c);
     kofs.assign(b + 1, 0);
+    own_stream.assign(b + 1, 1);
+    std::vector<int> host(b + 1, -1);  // class whose stream class c reads (-1: its own)
+    if (!std::getenv("SUP_JIT_NOSHARE")) share_streams(host);
     {
       size_t off = (ctab.size() + 7) & ~(size_t)7;
       for (int c = 0; c <= b; ++c) {
+        if (host[c] >= 0) {
+          own_stream[c] = 0;
+          continue;
+        }
         kofs[c] = (int)off;
         off = (off + cls_consts[c].size() + 7) & ~(size_t)7;
+      }
+    }
+    cpos.assign(b + 1, {});
+    for (int c = 0; c <= b; ++c) {
+      if (host[c] < 0) {
+        for (size_t i = 0; i < cls_consts[c].size(); ++i) cpos[c].push_back(kofs[c] + (int)i);
+      } else {
+        const std::vector<int> at = match_stream(cls_consts[c], cls_consts[host[c]]);
+        for (int i : at) cpos[c].push_back(kofs[host[c]] + i);
       }
     }
     if (std::getenv("SUP_JIT_VERBOSE")) {
@@ -1401,8 +1502,15 @@ struct Gen {
         std::vector<double> u = cls_consts[c];
         std::sort(u.begin(), u.end());
         const size_t nd = (size_t)(std::unique(u.begin(), u.end()) - u.begin());
-        std::fprintf(stderr, ", class %d: %zu (%zu distinct)%s", c, cls_consts[c].size(), nd,
-                     same >= 0 ? " (= earlier)" : "");
+        size_t shared = 0;  // constants an earlier class's stream also holds
+        for (double v : cls_consts[c]) {
+          bool f = false;
+          for (int c2 = 0; c2 < c && !f; ++c2)
+            f = std::find(cls_consts[c2].begin(), cls_consts[c2].end(), v) != cls_consts[c2].end();
+          shared += f;
+        }
+        std::fprintf(stderr, ", class %d: %zu (%zu distinct, %zu in earlier streams)%s%s", c, cls_consts[c].size(), nd,
+                     shared, same >= 0 ? " (= earlier)" : "", own_stream[c] ? "" : " [reads another class's stream]");
       }
       std::fprintf(stderr, "\n");
     }

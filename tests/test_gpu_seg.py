@@ -287,3 +287,19 @@ def test_cli_auto_mode_same_bits_cold_and_warm(tmp_path):
     warm = run()
     assert cold == warm
     assert rel(float(jit1.split()[1]), float(cold.split()[1])) < 1e-9
+
+
+@pytest.mark.parametrize("n,d,seed", [(28, 0.9, 1), (30, 0.7, 1)])
+def test_seg_shared_streams_bitexact_gpu(sup, orc, monkeypatch, n, d, seed):
+    """Near-dense patterns (d = 0.7, 0.9) whose top specialised step and shared
+    step re-form the same copies: one class reads the other's constant stream
+    (jit.cpp share_streams, round 4).  Storage only: GPU == host twin ==
+    oracle mirror bit for bit, and the same bits with sharing disabled."""
+    rng = np.random.default_rng(seed)  # patterns where sharing applies (SUP_JIT_VERBOSE shows it)
+    a = np.where(rng.random((n, n)) < d, rng.random((n, n)) * 5, 0.0)
+    a[np.arange(n), rng.permutation(n)] = 1.0 + rng.random(n)
+    got = sup.perman(a, algo=4, kernel="seg")
+    assert got == orc.engine_perman_as(sup, a, "seg", threads=16)
+    assert got == sup.perman_cpu(a, "seg", threads=16)
+    monkeypatch.setenv("SUP_JIT_NOSHARE", "1")
+    assert sup.perman(a, algo=4, kernel="seg") == got

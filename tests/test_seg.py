@@ -148,8 +148,8 @@ def test_seg_cost_model_reported(sup):
     assert 0 < st_seg["est_ops_per_step"] < st_blk["est_ops_per_step"]
 
 
-@pytest.mark.parametrize("case", ["n10", "n64", "zero_walk_col", "no_rest"])
-def test_generated_kernel_compiles(sup, case, tmp_path, monkeypatch):
+@pytest.mark.parametrize("case", ["n10", "n64", "zero_walk_col", "no_rest", "shared_streams"])
+def test_generated_kernel_compiles(sup, case, tmp_path, monkeypatch, capfd):
     monkeypatch.setenv("SUP_JIT_CACHE_DIR", str(tmp_path))
     if case == "n10":
         a = _rand(10, 0.5, 7)
@@ -158,6 +158,11 @@ def test_generated_kernel_compiles(sup, case, tmp_path, monkeypatch):
     elif case == "zero_walk_col":
         a = _rand(24, 0.3, 9)
         a[:, 3] = 0.0  # a column with no nonzero: its steps only accumulate
+    elif case == "shared_streams":  # one step class reads another's constant stream (share_streams)
+        rng = np.random.default_rng(1)
+        a = np.where(rng.random((28, 28)) < 0.9, rng.random((28, 28)) * 5, 0.0)
+        a[np.arange(28), rng.permutation(28)] = 1.0 + rng.random(28)
+        monkeypatch.setenv("SUP_JIT_VERBOSE", "1")
     else:
         a = _rand(24, 0.9, 10)  # every row touched by the walk columns: no rest segment
     info = sup.prepare(a, "seg")
@@ -166,6 +171,8 @@ def test_generated_kernel_compiles(sup, case, tmp_path, monkeypatch):
     assert len(list(tmp_path.glob("seg_*.co"))) >= 1  # disk cache written (one per budget the plan compiled)
     again = sup.prepare(a, "seg")
     assert again["compile_ms"] == 0.0  # in-memory cache
+    if case == "shared_streams":
+        assert "reads another class's stream" in capfd.readouterr().err
 
 
 def test_dense_lds_plan_and_cpu(sup, orc):
