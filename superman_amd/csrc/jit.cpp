@@ -2089,6 +2089,12 @@ int compile(const Plan& P, std::shared_ptr<std::vector<char>>& code) {
     FILE* f = std::fopen((std::string(d) + "/seg_" + key_hex(P.jit_key) + ".hip").c_str(), "w");
     if (f) std::fputs(P.jit_src.c_str(), f), std::fclose(f);
   }
+  if (const char* e = std::getenv("SUP_JIT_FAIL"))  // tests: a compile hiprtc refuses (the fallback paths)
+    if (std::atoi(e)) {
+      g_jit_failed.store(true);
+      set_error("hiprtc compile of the segmented walk failed: refused on request (SUP_JIT_FAIL)");
+      return SUP_EHIP;
+    }
   auto t0 = std::chrono::steady_clock::now();
   hiprtcProgram prog;
   const char* hdr[] = {kWalkCommonSrc, kWalkParamsSrc};

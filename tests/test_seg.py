@@ -60,15 +60,18 @@ def test_planner_choice(sup, tmp_path, monkeypatch):
     assert sup.plan_info(a, "dense", jit=0)["kind"] == "sparse"
     assert sup.plan_info(a, "dense", jit=0, gpu_num=8)["kind"] == "sparse"
     assert sup.plan_info(a, "dense", jit=1)["kind"] == "seg"
-    # warm: the jit = 1 plan left its choices (and kernel) in the disk cache,
-    # rebuilding costs ~ms, so auto mode now takes the segmented walk
-    # (another matrix of the same zero pattern: the choices are keyed by the pattern; `a` itself keeps its
-    # first auto-mode decision for the life of the process)
+    # the jit = 1 plan left its choices (and kernel) in the disk cache, but auto mode's first decision for
+    # this pattern is recorded too (round 4, AutoRecord): `a` and another matrix of its zero pattern keep it
     assert any(p.name.startswith("plan_") for p in tmp_path.iterdir())
     assert sup.plan_info(a, "dense", jit=0)["kind"] == "sparse"
-    a2 = 0.5 * a
-    assert sup.plan_info(a2, "dense", jit=0)["kind"] == "seg"
-    assert sup.plan_key(a2, "dense", jit=0) == sup.plan_key(a2, "dense", jit=1)
+    assert sup.plan_info(0.5 * a, "dense", jit=0)["kind"] == "sparse"
+    # warm, no auto decision yet: a pattern whose choices a jit = 1 plan recorded first — rebuilding costs
+    # ~ms, so auto mode's bar is 0.1 s and it takes the segmented walk (and records that)
+    t = np.ascontiguousarray(a.T)
+    assert sup.plan_info(t, "dense", jit=1)["kind"] == "seg"
+    t2 = 0.5 * t
+    assert sup.plan_info(t2, "dense", jit=0)["kind"] == "seg"
+    assert sup.plan_key(t2, "dense", jit=0) == sup.plan_key(t2, "dense", jit=1)
     c, _, _ = sup.read_matrix(fixture_path("double__32_0.50_0"))
     assert sup.plan_info(c, "dense", jit=0)["kind"] == "sparse"  # 2^31 steps: ms saved
     b, _, _ = sup.read_matrix(fixture_path("synth44_0.15_int"))
@@ -310,21 +313,35 @@ def test_seg_skip_aware_plan(sup, monkeypatch):
 
 
 def test_seg_uncompilable_pattern_falls_back(sup, tmp_path, monkeypatch):
-    """A dense n = 60 pattern whose generated kernel hiprtc's register
-    allocator gives up on ("maximum depth for recoloring"): the plan check
-    (jit.cpp build_seg) refuses the segmented walk, a dense request runs the
-    ahead-of-time walk instead, an explicit segmented request fails loudly,
-    and later kernels still compile in the same process."""
+    """A kernel hiprtc refuses (SUP_JIT_FAIL stands in for a register
+    allocator that gives up): the plan check (jit.cpp build_seg) refuses the
+    segmented walk, a dense request runs the ahead-of-time walk instead, an
+    explicit segmented request fails loudly, and later kernels still compile
+    in the same process (one at a time after a failure)."""
+    monkeypatch.setenv("SUP_JIT_CACHE_DIR", str(tmp_path))
+    a = _rand(36, 0.9, 1029, ints=False)  # a walk of >= 10 ms: planning compiles and checks the kernel
+    monkeypatch.setenv("SUP_JIT_FAIL", "1")
+    assert sup.plan_info(a, "dense", jit=1)["kind"] in ("dense", "sparse")
+    with pytest.raises(sup.SupError):
+        sup.plan_info(a, "seg", jit=1)
+    monkeypatch.delenv("SUP_JIT_FAIL")
+    assert sup.prepare(_rand(24, 0.5, 11), "seg")["kind"] == "seg"
+
+
+def test_seg_near_dense_large_n_compiles(sup, tmp_path, monkeypatch):
+    """The dense n = 60, d = 0.9 pattern hiprtc refused until round 3 ("inline
+    assembly requires more registers than available": a region pinned all 8
+    SGPR pieces of a near-dense D product beside the next region's prefetch)
+    now gets a segmented plan whose walk loop has no scratch (the plan's
+    compiler check)."""
     monkeypatch.setenv("SUP_JIT_CACHE_DIR", str(tmp_path))
     rng = np.random.default_rng(1029)
     n = 60
     a = np.where(rng.random((n, n)) < 0.9, rng.random((n, n)) * 5, 0.0)
     a[np.arange(n), rng.permutation(n)] = 1.0
-    assert sup.plan_info(a, "dense", jit=1)["kind"] in ("dense", "sparse")
-    with pytest.raises(sup.SupError):
-        sup.plan_info(a, "seg", jit=1)
-    assert sup.prepare(_rand(24, 0.5, 11), "seg")["kind"] == "seg"
-
+    info = sup.plan_info(a, "seg", jit=1)
+    assert info["kind"] == "seg"
+    assert info["est_ops_per_step"] < sup.plan_info(a, "dense", jit=-1)["est_ops_per_step"]
 
 def test_seg_shards_balanced_under_chunk_skip(sup):
     """Config 5 (n = 44 d = 0.15 int, SkipOrder): the segmented walk skips 87 %
