@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "walk_batch.hpp"
 #include "walk_params.hpp"
 
 namespace sup {
@@ -23,6 +24,18 @@ SUP_DECL_RANGE(skip, 17)
 SUP_DECL_RANGE(skip, 33)
 SUP_DECL_RANGE(skip, 49)
 #undef SUP_DECL_RANGE
+#define SUP_DECL_BATCH(KIND, LO)                                                                       \
+  hipError_t launch_batch_##KIND##_##LO(int n, const WalkParams& p, const LeafBatch& b, int grid, hipStream_t s); \
+  hipError_t occupancy_batch_##KIND##_##LO(int n, int* blocks_per_cu);
+SUP_DECL_BATCH(dense, 1)
+SUP_DECL_BATCH(dense, 17)
+SUP_DECL_BATCH(dense, 33)
+SUP_DECL_BATCH(dense, 49)
+SUP_DECL_BATCH(sparse, 1)
+SUP_DECL_BATCH(sparse, 17)
+SUP_DECL_BATCH(sparse, 33)
+SUP_DECL_BATCH(sparse, 49)
+#undef SUP_DECL_BATCH
 #define SUP_DECL_EXACT(LO)                                                                                  \
   hipError_t launch_exact_##LO(int n, int g, const WalkParams& p, const ExactParams& e, int grid,        \
                                hipStream_t s);                                                        \
@@ -58,6 +71,11 @@ hipError_t launch_walk(WalkKind kind, int n, const WalkParams& p, int grid, hipS
 // Resident 256-thread blocks per CU for that kernel (occupancy API).
 hipError_t walk_occupancy(WalkKind kind, int n, int* blocks_per_cu);
 
+// A batch of leaves of one order and layout in one launch (walk_batch.hpp;
+// kWalkDense / kWalkSparse), and its occupancy.
+hipError_t launch_walk_batch(WalkKind kind, int n, const WalkParams& p, const LeafBatch& b, int grid, hipStream_t s);
+hipError_t walk_batch_occupancy(WalkKind kind, int n, int* blocks_per_cu);
+
 // LDS-staged dense walk (walk_lds.hip; 64-thread blocks, X in LDS).
 hipError_t launch_lds(int n, const WalkParams& p, int grid, hipStream_t s);
 hipError_t lds_occupancy(int n, int m, int* blocks_per_cu);
@@ -78,5 +96,11 @@ hipError_t dd_occupancy(int n, int* blocks_per_cu);
 hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scratch, double* out,
                                   hipStream_t s);
 uint64_t pairwise_scratch_size(uint64_t count);
+// The same tree over each of `nseg` consecutive segments of `count` doubles
+// (a leaf batch's chunk partials): out[i] is bit-identical to
+// launch_pairwise_reduce over segment i alone.  `scratch` holds nseg times
+// pairwise_scratch_size(count).
+hipError_t launch_pairwise_reduce_seg(const double* in, uint64_t count, uint64_t nseg, double* scratch, double* out,
+                                      hipStream_t s);
 
 }  // namespace sup

@@ -22,6 +22,22 @@ __global__ __launch_bounds__(kBlock) void pairwise64_pass(const double* __restri
   if (lane == 0) out[g] = s;
 }
 
+// One 64-way pass over each of nseg segments of `count` values: group g of
+// segment i reads that segment's values [64 g, 64 g + 64) (zero past its
+// end), the groups of one call to pairwise64_pass on the segment alone.
+__global__ __launch_bounds__(kBlock) void pairwise64_pass_seg(const double* __restrict__ in, uint64_t count,
+                                                              double* __restrict__ out, uint64_t groups,
+                                                              uint64_t nseg) {
+  const uint64_t gg = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  if (gg >= groups * nseg) return;  // wave-uniform
+  const uint64_t seg = gg / groups, g = gg - seg * groups;
+  const uint64_t i = g * 64u + lane;
+  const double v = (i < count) ? in[seg * count + i] : 0.0;
+  const double s = wave_sum(v);
+  if (lane == 0) out[seg * groups + g] = s;
+}
+
 uint64_t pairwise_scratch_size(uint64_t count) {
   uint64_t total = 0;
   while (count > 1) {
@@ -51,6 +67,28 @@ hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scra
   return hipSuccess;
 }
 
+hipError_t launch_pairwise_reduce_seg(const double* in, uint64_t count, uint64_t nseg, double* scratch, double* out,
+                                      hipStream_t s) {
+  if (nseg == 0) return hipSuccess;
+  if (count == 0) return hipMemsetAsync(out, 0, nseg * sizeof(double), s);
+  if (count == 1) return hipMemcpyAsync(out, in, nseg * sizeof(double), hipMemcpyDeviceToDevice, s);
+  const double* src = in;
+  double* dst = scratch;
+  while (count > 1) {
+    const uint64_t groups = (count + 63) / 64;
+    const uint64_t blocks = (groups * nseg + kWavesPerBlock - 1) / kWavesPerBlock;
+    double* target = (groups == 1) ? out : dst;
+    hipLaunchKernelGGL(pairwise64_pass_seg, dim3((unsigned)blocks), dim3(kBlock), 0, s, src, count, target, groups,
+                       nseg);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    src = target;
+    dst = target + groups * nseg;
+    count = groups;
+  }
+  return hipSuccess;
+}
+
 #define SUP_DISPATCH(KIND, FN, ...)                 \
   if (n <= 16) return FN##_##KIND##_1(__VA_ARGS__);   \
   if (n <= 32) return FN##_##KIND##_17(__VA_ARGS__);  \
@@ -75,6 +113,26 @@ hipError_t walk_occupancy(WalkKind kind, int n, int* blocks_per_cu) {
     case kWalkSparse: { SUP_DISPATCH(sparse, occupancy, n, blocks_per_cu) }
     case kWalkSkip: { SUP_DISPATCH(skip, occupancy, n, blocks_per_cu) }
     case kWalkSeg: break;  // jit_occupancy (jit.cpp)
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_walk_batch(WalkKind kind, int n, const WalkParams& p, const LeafBatch& b, int grid, hipStream_t s) {
+  if (n < 1 || n > 64) return hipErrorInvalidValue;
+  switch (kind) {
+    case kWalkDense: { SUP_DISPATCH(dense, launch_batch, n, p, b, grid, s) }
+    case kWalkSparse: { SUP_DISPATCH(sparse, launch_batch, n, p, b, grid, s) }
+    default: break;
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t walk_batch_occupancy(WalkKind kind, int n, int* blocks_per_cu) {
+  if (n < 1 || n > 64) return hipErrorInvalidValue;
+  switch (kind) {
+    case kWalkDense: { SUP_DISPATCH(dense, occupancy_batch, n, blocks_per_cu) }
+    case kWalkSparse: { SUP_DISPATCH(sparse, occupancy_batch, n, blocks_per_cu) }
+    default: break;
   }
   return hipErrorInvalidValue;
 }

@@ -17,6 +17,7 @@
 // a zero x_j simply makes the product 0 (the reference's zero_num logic
 // computes the same term).
 #include "walk_common.hpp"
+#include "walk_batch.hpp"
 #include "kernels.hpp"
 
 namespace sup {
@@ -70,6 +71,74 @@ __global__ __launch_bounds__(kBlock) void walk_sparse(WalkParams p) {
   }
 }
 
+// One wave-chunk `ga` of the prefix-blocked walk: the lane's signed sum
+// (parity of the chunk and lane applied), the batched kernel's copy of the
+// one-leaf kernel's chunk body (same operations in the same order: the same bits;
+// kept apart so the one-leaf kernel's code is untouched).
+template <int N>
+__device__ __forceinline__ double sparse_chunk(const WalkParams& p, uint64_t ga, uint32_t lane, uint32_t lane_par,
+                                               uint32_t T, uint32_t offL, int nb0) {
+  constexpr int NP = pad8(N);
+  constexpr int NB = Blocks<N>::NB;
+  double x[N];
+  chunk_start<N>(x, p, ga, lane);
+  double U[NB + 1];
+  suffix_all<N>(x, U);
+  double acc = U[0];
+  uint32_t t = 1;
+  for (; t + 1 < T; t += 2) {
+    // re-materialise nb0 in an SGPR every iteration: hoisted "nb0 > B"
+    // masks would be spilled to VGPR lanes and cost v_readlane (VALU) per step
+    int nbo = nb0;
+    asm volatile("" : "+s"(nbo));
+    sparse_step<N>(x, U, opaque_c(p.cols, offL + ((t >> 1) & 1u) * NP * 8u), nbo);
+    acc -= U[0];
+    const uint32_t u = t + 1;
+    const uint32_t k = (uint32_t)__builtin_ctz(u);
+    const uint32_t neg = (u >> (k + 1)) & 1u;
+    sparse_step<N>(x, U, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nb_of(p, k));
+    acc += U[0];
+  }
+  if (t < T) {
+    sparse_step<N>(x, U, opaque_c(p.cols, offL + ((t >> 1) & 1u) * NP * 8u), nb0);
+    acc -= U[0];
+  }
+  if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;
+  return acc;
+}
+
+// A batch of leaves (walk_batch.hpp): chunk a of the launch is chunk
+// a mod 2^h of leaf a >> h, with that leaf's tables; a group of chunks never
+// spans two leaves (groups are powers of two <= 2^h).
+template <int N>
+__global__ __launch_bounds__(kBlock) void walk_sparse_batch(WalkParams p, LeafBatch b) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool lane_valid = lane < (1u << p.L);
+  const uint32_t lane_par = __builtin_popcount(lane) & 1u;
+  const uint64_t cmask = (1ull << b.leaf_bits) - 1ull;
+  const uint32_t T = 1u << p.m;
+  const uint32_t offL = 2u * (uint32_t)p.L * pad8(N) * 8u;
+
+  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {
+    const uint64_t a0 = (uint64_t)g * p.group;
+    typedef const __attribute__((address_space(4))) LeafDesc cdesc;
+    cdesc* dp = (cdesc*)b.leaves + (a0 >> b.leaf_bits);  // scalar loads: the leaf is wave-uniform
+    WalkParams q = p;
+    q.cols = dp->cols, q.x0 = dp->x0, q.nb_lo = dp->nb_lo, q.nb_hi = dp->nb_hi;
+    const int nb0 = nb_of(q, 0);
+    double keep = 0.0;
+    for (uint32_t j = 0; j < (uint32_t)p.group; ++j) {
+      const uint64_t a = a0 + j;
+      if (a >= p.chunk_count) break;
+      const double acc = sparse_chunk<N>(q, a & cmask, lane, lane_par, T, offL, nb0);
+      const double part = wave_sum(lane_valid ? acc : 0.0);
+      keep = (lane == j) ? part : keep;
+    }
+    const uint64_t a = a0 + lane;
+    if (lane < (uint32_t)p.group && a < p.chunk_count) p.chunk_out[a] = keep;
+  }
+}
+
 template <int N, int HI>
 static hipError_t launch_rec(int n, const WalkParams& p, int grid, hipStream_t s) {
   if (n == N) {
@@ -87,6 +156,23 @@ static hipError_t occ_rec(int n, int* blocks_per_cu) {
   return hipErrorInvalidValue;
 }
 
+template <int N, int HI>
+static hipError_t launch_batch_rec(int n, const WalkParams& p, const LeafBatch& b, int grid, hipStream_t s) {
+  if (n == N) {
+    hipLaunchKernelGGL(walk_sparse_batch<N>, dim3(grid), dim3(kBlock), 0, s, p, b);
+    return hipGetLastError();
+  }
+  if constexpr (N < HI) return launch_batch_rec<N + 1, HI>(n, p, b, grid, s);
+  return hipErrorInvalidValue;
+}
+
+template <int N, int HI>
+static hipError_t occ_batch_rec(int n, int* blocks_per_cu) {
+  if (n == N) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_sparse_batch<N>, kBlock, 0);
+  if constexpr (N < HI) return occ_batch_rec<N + 1, HI>(n, blocks_per_cu);
+  return hipErrorInvalidValue;
+}
+
 #define SUP_CAT2(a, b) a##b
 #define SUP_CAT(a, b) SUP_CAT2(a, b)
 
@@ -95,6 +181,14 @@ hipError_t SUP_CAT(launch_sparse_, SUP_N_LO)(int n, const WalkParams& p, int gri
 }
 hipError_t SUP_CAT(occupancy_sparse_, SUP_N_LO)(int n, int* blocks_per_cu) {
   return occ_rec<SUP_N_LO, SUP_N_HI>(n, blocks_per_cu);
+}
+
+hipError_t SUP_CAT(launch_batch_sparse_, SUP_N_LO)(int n, const WalkParams& p, const LeafBatch& b, int grid,
+                                                  hipStream_t s) {
+  return launch_batch_rec<SUP_N_LO, SUP_N_HI>(n, p, b, grid, s);
+}
+hipError_t SUP_CAT(occupancy_batch_sparse_, SUP_N_LO)(int n, int* blocks_per_cu) {
+  return occ_batch_rec<SUP_N_LO, SUP_N_HI>(n, blocks_per_cu);
 }
 
 }  // namespace sup
