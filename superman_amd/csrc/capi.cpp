@@ -560,6 +560,82 @@ int leaf_compute(const LeafCtx& c, const double* a, int n, double* out, sup_stat
                   : sup_perman(m.data(), SUP_FLOAT64, n, c.kernel, c.sched, &c.o, out, st);
 }
 
+// Whether the leaves of this request may share launches (run_range_batch):
+// one device, the single-device schedule, a kernel request the batch kernels
+// serve, and no checkpoint.  Leaves whose plan turns out otherwise (a
+// segmented or SkipPer plan) still go one at a time.
+bool leaf_batching(const LeafCtx& c) {
+  const char* e = std::getenv("SUP_LEAF_BATCH");
+  if (e && std::atoi(e) <= 1) return false;
+  return !c.on_cpu && c.sched == SUP_SCHED_SINGLE && c.o.use_rccl == 0 &&
+         (c.kernel == SUP_KERNEL_DENSE || c.kernel == SUP_KERNEL_SPARYSER || c.kernel == SUP_KERNEL_DENSE_PLAIN);
+}
+int leaf_batch_max() {
+  const char* e = std::getenv("SUP_LEAF_BATCH");
+  return e ? std::max(1, std::min(kMaxBatchLeaves, std::atoi(e))) : 16;
+}
+
+// Several leaves of order n: each planned as sup_perman plans it (the same
+// plan, so the same bits), the batchable ones walked in one launch, the rest
+// one at a time through sup_perman.
+int leaf_compute_batch(const LeafCtx& c, const std::vector<const double*>& mats, int n,
+                       const std::vector<double*>& outs, sup_stats* st) {
+  auto t0 = std::chrono::steady_clock::now();
+  const size_t K = mats.size();
+  std::memset(st, 0, sizeof(*st));
+  std::vector<std::vector<double>> ms(K);
+  std::vector<std::shared_ptr<const Plan>> plans(K);
+  const Layout lay = layout_for(n, c.o);
+  int rc = check_walk_opts(c.o);
+  if (rc) return rc;
+  for (size_t i = 0; i < K; ++i) {
+    ms[i].assign(mats[i], mats[i] + (size_t)n * n);
+    std::vector<int> rp(n), cp(n);
+    if (c.preprocessing == 1) rc = sup_sort_order(ms[i].data(), SUP_FLOAT64, n, cp.data());
+    else if (c.preprocessing == 2) rc = sup_skip_order(ms[i].data(), SUP_FLOAT64, n, rp.data(), cp.data());
+    if (rc) return rc;
+    if ((rc = plan_for_shared(ms[i].data(), n, c.kernel, lay, plans[i], c.o.jit, 1, c.o.device_id))) return rc;
+  }
+  const double sign = (double)(4 * (n & 1) - 2);  // gpu_exact_dense.cu:698
+  std::vector<const Plan*> group;
+  std::vector<size_t> gi;
+  double kms = 0.0;
+  uint64_t steps = 0;
+  for (size_t i = 0; i < K; ++i) {
+    if (K > 1 && batchable(*plans[i], *plans[i])) {
+      if (group.empty() || batchable(*group[0], *plans[i])) {
+        group.push_back(plans[i].get());
+        gi.push_back(i);
+        continue;
+      }
+    }
+    sup_stats one;  // not batchable with the group: on its own, as before
+    if ((rc = sup_perman(ms[i].data(), SUP_FLOAT64, n, c.kernel, c.sched, &c.o, outs[i], &one))) return rc;
+    kms += one.kernel_ms;
+    steps += one.gray_steps;
+    st->walk_kind = one.walk_kind;
+  }
+  if (!group.empty()) {
+    std::vector<double> part;
+    double ms_b = 0.0;
+    if ((rc = run_range_batch(c.o.device_id, group, part, &ms_b))) return rc;
+    for (size_t q = 0; q < gi.size(); ++q) *outs[gi[q]] = sign * part[q];
+    kms += ms_b;
+    steps += (uint64_t)gi.size() << (n - 1);
+    st->walk_kind = (int)group[0]->kind;
+    st->lane_bits = group[0]->lay.L;
+    st->walk_bits = group[0]->lay.m;
+    st->est_ops_per_step = walk_cost(*group[0]);
+  }
+  st->kernel_ms = kms;
+  st->gray_steps = steps;
+  st->visited_steps = steps;
+  st->devices_used = 1;
+  st->leaves = (int)K;
+  st->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return SUP_OK;
+}
+
 void leaf_accumulate(LeafCtx& c, const sup_stats& st) {
   if (c.first) {
     c.acc = st;
@@ -666,17 +742,33 @@ int sup_perman_reduced(const void* mat, sup_dtype t, int n, sup_kernel kernel, s
     A[i] = t == SUP_INT32 ? (double)((const int32_t*)mat)[i]
            : t == SUP_FLOAT32 ? (double)((const float*)mat)[i] : ((const double*)mat)[i];
   std::mutex smu;
-  const int rc = decompose_batched(A.data(), n, r, c.on_cpu ? 1 : leaf_workers(),
-                                   [&c, &smu](int w, const double* a, int k, double* v) {
-                                     set_ctx_lane(w);
-                                     sup_stats st;
-                                     const int e = leaf_compute(c, a, k, v, &st);
-                                     if (e) return e;
-                                     std::lock_guard<std::mutex> g(smu);
-                                     leaf_accumulate(c, st);
-                                     return SUP_OK;
-                                   },
-                                   out, &leaves);
+  // leaves in batches of up to leaf_batch_max() per launch (run_range_batch),
+  // else one at a time; either way the same bits
+  const int rc =
+      leaf_batching(c)
+          ? decompose_batched_multi(A.data(), n, r, leaf_workers(), leaf_batch_max(),
+                                    [&c, &smu](int w, const std::vector<const double*>& as, int k,
+                                               const std::vector<double*>& vs) {
+                                      set_ctx_lane(w);
+                                      sup_stats st;
+                                      const int e = leaf_compute_batch(c, as, k, vs, &st);
+                                      if (e) return e;
+                                      std::lock_guard<std::mutex> g(smu);
+                                      leaf_accumulate(c, st);
+                                      return SUP_OK;
+                                    },
+                                    out, &leaves)
+          : decompose_batched(A.data(), n, r, c.on_cpu ? 1 : leaf_workers(),
+                              [&c, &smu](int w, const double* a, int k, double* v) {
+                                set_ctx_lane(w);
+                                sup_stats st;
+                                const int e = leaf_compute(c, a, k, v, &st);
+                                if (e) return e;
+                                std::lock_guard<std::mutex> g(smu);
+                                leaf_accumulate(c, st);
+                                return SUP_OK;
+                              },
+                              out, &leaves);
   if (rc) return rc;
   if (st) {
     *st = c.acc;

@@ -400,7 +400,9 @@ std::pair<uint64_t, uint64_t> leaf_key(const double* a, int k) {
 template <class Ops>
 int batched(const double* A, int n, const sup_reduce_opts& r, int workers,
             const std::function<int(int, const double*, int, typename Ops::V*)>& leaf, typename Ops::V* out,
-            int* n_leaves, const char* who, bool memo) {
+            int* n_leaves, const char* who, bool memo, int batch_max = 1,
+            const std::function<int(int, const std::vector<const double*>&, int,
+                                    const std::vector<typename Ops::V*>&)>* leaves = nullptr) {
   typedef typename Ops::V V;
   set_error("");
   if (int rc = check_reduce_opts(r, who)) return rc;
@@ -417,23 +419,37 @@ int batched(const double* A, int n, const sup_reduce_opts& r, int workers,
   bool closed = false, failed = false;
   int frc = SUP_OK;
   std::string ferr;
-  const size_t cap = (size_t)workers * 4;
+  batch_max = leaves ? std::max(1, batch_max) : 1;
+  const size_t cap = (size_t)workers * 4 * (size_t)batch_max;
   auto work = [&](int w) {
     for (;;) {
-      Job j;
+      std::vector<Job> js;
       {
         std::unique_lock<std::mutex> lk(mu);
         cv_get.wait(lk, [&] { return !q.empty() || closed; });
         if (q.empty()) return;
-        j = std::move(q.front());
+        // up to batch_max queued leaves of the first one's order (no waiting for more)
+        js.push_back(std::move(q.front()));
         q.pop_front();
+        while ((int)js.size() < batch_max && !q.empty() && q.front().n == js[0].n) {
+          js.push_back(std::move(q.front()));
+          q.pop_front();
+        }
       }
-      cv_put.notify_one();
+      cv_put.notify_all();
       {
         std::lock_guard<std::mutex> lk(mu);
         if (failed) continue;  // drain without computing
       }
-      const int e = leaf(w, j.a.data(), j.n, j.slot);
+      int e = SUP_OK;
+      if (leaves) {
+        std::vector<const double*> mats;
+        std::vector<V*> slots;
+        for (const Job& j : js) mats.push_back(j.a.data()), slots.push_back(j.slot);
+        e = (*leaves)(w, mats, js[0].n, slots);
+      } else {
+        e = leaf(w, js[0].a.data(), js[0].n, js[0].slot);
+      }
       if (e) {
         std::lock_guard<std::mutex> lk(mu);
         if (!failed) failed = true, frc = e, ferr = sup_last_error();
@@ -505,6 +521,14 @@ int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int work
                       const std::function<int(int, const double*, int, double*)>& leaf, double* out, int* n_leaves,
                       bool memo) {
   return batched<DblOps>(A, n, r, workers, leaf, out, n_leaves, "sup_perman_reduced", memo);
+}
+
+int decompose_batched_multi(const double* A, int n, const sup_reduce_opts& r, int workers, int batch_max,
+                            const LeafBatchFn& leaves, double* out, int* n_leaves) {
+  const std::function<int(int, const double*, int, double*)> one = [&](int w, const double* a, int k, double* v) {
+    return leaves(w, std::vector<const double*>{a}, k, std::vector<double*>{v});
+  };
+  return batched<DblOps>(A, n, r, workers, one, out, n_leaves, "sup_perman_reduced", true, batch_max, &leaves);
 }
 
 int decompose_dd_batched(const double* A, int n, const sup_reduce_opts& r, int workers,

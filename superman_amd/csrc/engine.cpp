@@ -742,6 +742,15 @@ struct DeviceCtx {
   unsigned* d_counter = nullptr;
   double* d_result = nullptr;
   double* h_result = nullptr;  // pinned host slot: the result's D2H without a pageable staging copy
+  // leaf batches (run_range_batch): packed tables, descriptors, results
+  double* d_batch = nullptr;
+  size_t batch_cap = 0;
+  LeafDesc* d_desc = nullptr;
+  size_t desc_cap = 0;
+  double* d_bres = nullptr;
+  size_t bres_cap = 0;
+  double* h_bres = nullptr;  // pinned, kMaxBatchLeaves doubles
+  int occ_batch[2][SUP_MAX_N + 1] = {};
   uint64_t tables_uid = 0;  // Plan::uid whose cols / x0 / nblk / rowmask / jtab the device holds
   std::mutex mu;
   int occ[3][SUP_MAX_N + 1] = {};  // AOT kernels; segmented walk: jit_occupancy
@@ -1008,6 +1017,105 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   } else {
     r.visited = count << (P.lay.L + P.lay.m);
   }
+  return SUP_OK;
+}
+
+// Several leaves (the -o / -u reduction's permanents) in one launch: plans of
+// one order, walk kind (plain or prefix-blocked) and layout.  Their tables are
+// packed into one device buffer, the batch kernel walks the K 2^h wave-chunks
+// as one queue (walk_batch.hpp), and each leaf's partials are folded by the
+// one-leaf pairwise tree: partial[i] is bit-identical to run_range over plan
+// i's whole range (tests/test_gpu_reduce_workers.py).  One launch instead of
+// K removes K - 1 launch tails, syncs and result copies.
+bool batchable(const Plan& a, const Plan& b) {
+  return (a.kind == kWalkDense || a.kind == kWalkSparse) && a.kind == b.kind && !a.lds && !b.lds && a.n == b.n &&
+         a.lay.L == b.lay.L && a.lay.m == b.lay.m && a.lay.h == b.lay.h && a.cols.size() == b.cols.size() &&
+         a.x0.size() == b.x0.size() && a.lay.chunks() >= 1;
+}
+
+int run_range_batch(int dev, const std::vector<const Plan*>& plans, std::vector<double>& partial, double* kernel_ms) {
+  const size_t K = plans.size();
+  partial.assign(K, 0.0);
+  if (kernel_ms) *kernel_ms = 0.0;
+  if (K == 0) return SUP_OK;
+  if (K > (size_t)kMaxBatchLeaves) {
+    set_error("leaf batch larger than kMaxBatchLeaves");
+    return SUP_EINVAL;
+  }
+  const Plan& P0 = *plans[0];
+  for (const Plan* q : plans)
+    if (!batchable(P0, *q)) {
+      set_error("leaf batch: plans of different order, walk or layout");
+      return SUP_EINVAL;
+    }
+  DeviceCtx* c = nullptr;
+  int rc = get_ctx(dev, &c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(c->mu);
+  SUP_HIP(hipSetDevice(c->phys));
+  const uint64_t C = P0.lay.chunks(), count = C * K;
+  const size_t colsz = P0.cols.size(), stride = colsz + P0.x0.size();
+  if ((rc = ensure(c->d_batch, c->batch_cap, K * stride))) return rc;
+  if ((rc = ensure(c->d_desc, c->desc_cap, K))) return rc;
+  if ((rc = ensure(c->d_chunk, c->chunk_cap, (size_t)count))) return rc;
+  if ((rc = ensure(c->d_scratch, c->scratch_cap, (size_t)(K * pairwise_scratch_size(C))))) return rc;
+  if ((rc = ensure(c->d_bres, c->bres_cap, K))) return rc;
+  if (!c->h_bres) SUP_HIP(hipHostMalloc(&c->h_bres, kMaxBatchLeaves * sizeof(double), hipHostMallocDefault));
+  std::vector<double> tab(K * stride);
+  std::vector<LeafDesc> desc(K);
+  for (size_t i = 0; i < K; ++i) {
+    const Plan& P = *plans[i];
+    std::copy(P.cols.begin(), P.cols.end(), tab.begin() + i * stride);
+    std::copy(P.x0.begin(), P.x0.end(), tab.begin() + i * stride + colsz);
+    desc[i].cols = c->d_batch + i * stride;
+    desc[i].x0 = c->d_batch + i * stride + colsz;
+    desc[i].nb_lo = desc[i].nb_hi = 0;
+    for (int k = 0; k < P.lay.m && k < 32 && P.kind == kWalkSparse; ++k) {
+      const uint64_t v = (uint64_t)(P.nblk[P.lay.L + k] & 15);
+      if (k < 16) desc[i].nb_lo |= v << (4 * k);
+      else desc[i].nb_hi |= v << (4 * (k - 16));
+    }
+  }
+  hipStream_t s = c->stream;
+  SUP_HIP(hipMemcpyAsync(c->d_batch, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice, s));
+  SUP_HIP(hipMemcpyAsync(c->d_desc, desc.data(), K * sizeof(LeafDesc), hipMemcpyHostToDevice, s));
+  SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
+  int& occ = c->occ_batch[P0.kind == kWalkSparse][P0.n];
+  if (occ == 0) {
+    int b = 0;
+    SUP_HIP(walk_batch_occupancy(P0.kind, P0.n, &b));
+    occ = b > 0 ? b : 1;
+  }
+  const uint64_t res_waves = (uint64_t)c->cus * (uint64_t)occ * kWavesPerBlock;
+  // groups as run_range picks them, and never larger than one leaf's chunks
+  unsigned group = 64;
+  while (group > 1 && (count / ((uint64_t)group * res_waves) < 32 || group > C)) group >>= 1;
+  const uint64_t waves_needed = (count + group - 1) / group;
+  uint64_t grid = (waves_needed + kWavesPerBlock - 1) / kWavesPerBlock;
+  grid = std::max<uint64_t>(1, std::min<uint64_t>(grid, (uint64_t)c->cus * (uint64_t)occ));
+  WalkParams p{};
+  p.cols = desc[0].cols;
+  p.x0 = desc[0].x0;
+  p.chunk_begin = 0;
+  p.chunk_count = count;
+  p.L = P0.lay.L;
+  p.m = P0.lay.m;
+  p.n = P0.n;
+  p.chunk_out = c->d_chunk;
+  p.counter = c->d_counter;
+  p.group = group;
+  p.tail_ticket = 0xffffffffu;
+  LeafBatch lb{c->d_desc, (unsigned)P0.lay.h, 0};
+  SUP_HIP(hipEventRecord(c->ev0, s));
+  SUP_HIP(launch_walk_batch(P0.kind, P0.n, p, lb, (int)grid, s));
+  SUP_HIP(hipEventRecord(c->ev1, s));
+  SUP_HIP(launch_pairwise_reduce_seg(c->d_chunk, C, K, c->d_scratch, c->d_bres, s));
+  SUP_HIP(hipMemcpyAsync(c->h_bres, c->d_bres, K * sizeof(double), hipMemcpyDeviceToHost, s));
+  SUP_HIP(hipStreamSynchronize(s));
+  float ms = 0.f;
+  SUP_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  for (size_t i = 0; i < K; ++i) partial[i] = c->h_bres[i];
+  if (kernel_ms) *kernel_ms = ms;
   return SUP_OK;
 }
 

@@ -245,6 +245,13 @@ int run_item_queue(uint64_t nitems, int takers, const std::function<int(int, uin
 // copied there on the device (the -R combine all-reduces those slots).
 int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visited, RangeResult& r,
               double* slot = nullptr);
+// Leaf batches (sup_perman_reduced's leaves): up to kMaxBatchLeaves plans of
+// one order, walk kind (plain / prefix-blocked) and layout in one launch on
+// device `dev`; partial[i] is bit-identical to run_range over plan i's whole
+// range.  batchable(): whether two plans can share a launch.
+constexpr int kMaxBatchLeaves = 32;
+bool batchable(const Plan& a, const Plan& b);
+int run_range_batch(int dev, const std::vector<const Plan*>& plans, std::vector<double>& partial, double* kernel_ms);
 
 // Combine partials with the same pairwise tree the device reduction uses.
 double pairwise_host(const std::vector<double>& v);
@@ -340,6 +347,12 @@ struct dd;
 int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
                       const std::function<int(int, const double*, int, double*)>& leaf, double* out, int* n_leaves,
                       bool memo = true);
+// The same with leaves handed out in batches: a worker takes up to
+// `batch_max` queued leaves of one order at once and calls
+// leaves(worker, mats, n, values) (sup_perman_reduced: one launch per batch).
+typedef std::function<int(int, const std::vector<const double*>&, int, const std::vector<double*>&)> LeafBatchFn;
+int decompose_batched_multi(const double* A, int n, const sup_reduce_opts& r, int workers, int batch_max,
+                            const LeafBatchFn& leaves, double* out, int* n_leaves);
 int decompose_dd_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
                          const std::function<int(int, const double*, int, dd*)>& leaf, dd* out, int* n_leaves);
 // Permanent in double-double (sup_perman_quad): *hi + *lo.
