@@ -38,6 +38,32 @@ __global__ __launch_bounds__(kBlock) void pairwise64_pass_seg(const double* __re
   if (lane == 0) out[seg * groups + g] = s;
 }
 
+// Two 64-way levels in one launch: block b folds level-1 groups
+// [64 b, 64 b + 64) (each group = 64 inputs, zero past `count`, folded by one
+// wave as pairwise64_pass folds it) and then those 64 group sums (zero past
+// the last group) as the next pairwise64_pass would: out[b] is bit-identical
+// to two consecutive pairwise64_pass launches (round 4: half the launches).
+__global__ __launch_bounds__(kBlock) void pairwise4096_pass(const double* __restrict__ in, uint64_t count,
+                                                            double* __restrict__ out, uint64_t groups1) {
+  __shared__ double g1[64];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint64_t base = (uint64_t)blockIdx.x * 64u;
+  for (uint32_t k = w; k < 64u; k += kWavesPerBlock) {
+    const uint64_t g = base + k;  // level-1 group
+    double v = 0.0;
+    if (g < groups1) {
+      const uint64_t i = g * 64u + lane;
+      v = wave_sum((i < count) ? in[i] : 0.0);
+    }
+    if (lane == 0) g1[k] = v;
+  }
+  __syncthreads();
+  if (w == 0) {
+    const double s = wave_sum(g1[lane]);
+    if (lane == 0) out[blockIdx.x] = s;
+  }
+}
+
 uint64_t pairwise_scratch_size(uint64_t count) {
   uint64_t total = 0;
   while (count > 1) {
@@ -55,6 +81,17 @@ hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scra
   double* dst = scratch;
   while (count > 1) {
     const uint64_t groups = (count + 63) / 64;
+    if (groups > 1) {  // two levels at once
+      const uint64_t groups2 = (groups + 63) / 64;
+      double* target = (groups2 == 1) ? out : dst;
+      hipLaunchKernelGGL(pairwise4096_pass, dim3((unsigned)groups2), dim3(kBlock), 0, s, src, count, target, groups);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      src = target;
+      dst = target + groups2;
+      count = groups2;
+      continue;
+    }
     const uint64_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
     double* target = (groups == 1) ? out : dst;
     hipLaunchKernelGGL(pairwise64_pass, dim3((unsigned)blocks), dim3(kBlock), 0, s, src, count, target, groups);

@@ -2,7 +2,7 @@
 file under profiles/r4/, keyed by the plan it measured (sup_plan_key for the
 same request, computed here with torch's hiprtc as bench.py plans it).
 
-    python tools/pmc_r4.py <pmc dir> <out.json> <matrix> [kernel jit prep]
+    python tools/pmc_r4.py <out.json> <matrix> <pmc dir> [<pmc dir> ...]   (request: dense, jit 1, no prep)
 
 Every counter of the walk kernel's dispatch is kept (summed over the
 dispatches of the pass, which is one launch: bench.py --pmc-child), with
@@ -44,36 +44,52 @@ def counters(d, walk=WALK):
 
 
 def main():
-    src, dst, matrix = sys.argv[1:4]
-    kernel = sys.argv[4] if len(sys.argv) > 4 else "dense"
-    jit = int(sys.argv[5]) if len(sys.argv) > 5 else 1
-    prep = int(sys.argv[6]) if len(sys.argv) > 6 else 0
+    dst, matrix = sys.argv[1:3]
+    dirs = sys.argv[3:]
+    kernel, jit, prep = "dense", 1, 0
     a = S.read_matrix(matrix)[0]
-    if prep == 1:
-        a = S.sort_order(a)[0]
-    elif prep == 2:
-        a = S.skip_order(a)[0]
     info = S.plan_info(a, kernel, jit=jit)
-    vals, ns = counters(src)
+    vals, ns = {}, []
+    for d in dirs:  # one pass per directory (counters that cannot share a pass)
+        v, t = counters(d)
+        vals.update(v)
+        ns += t
     if not vals:
-        sys.exit(f"no counters of {WALK} under {src}")
+        sys.exit(f"no counters of {WALK} under {dirs}")
     out = {"n": int(a.shape[0]), "matrix": os.path.basename(matrix), "kernel": WALK, "request": kernel, "jit": jit,
            "prep": prep, "plan_key": hex(S.plan_key(a, kernel, jit=jit)), "walk": info["kind"],
            "cached": info["cached"], "pair_bits": info["pair_bits"], "model_ops_per_gray_step": info["est_ops_per_step"],
-           "kernel_ns": max(ns) if ns else None, "counters": vals,
-           "source": f"rocprofv3 --pmc {' '.join(sorted(vals))} --kernel-trace, one launch (bench.py --pmc-child)"}
+           "kernel_ns_per_pass": ns, "counters": vals,
+           "source": "rocprofv3 --pmc <counters> --kernel-trace, one launch per pass (bench.py --pmc-child): "
+                     + ", ".join(os.path.relpath(d) for d in dirs)}
     if "SQ_WAVE_CYCLES" in vals and vals.get("GRBM_GUI_ACTIVE"):
         cycles = vals["GRBM_GUI_ACTIVE"] / 8.0
         out["waves_per_simd"] = 4.0 * vals["SQ_WAVE_CYCLES"] / (cycles * 1024.0)
-        out["clock_ghz"] = cycles / max(ns) if ns else None
+    if "MeanOccupancyPerCU" in vals:
+        out["mean_occupancy_waves_per_cu"] = vals["MeanOccupancyPerCU"]
     if "SQ_LDS_BANK_CONFLICT" in vals:
         out["lds_bank_conflict_per_lds_inst"] = vals["SQ_LDS_BANK_CONFLICT"] / max(vals.get("SQ_INSTS_LDS", 0.0), 1.0)
     if vals.get("SQC_DCACHE_REQ"):
         out["sqc_dcache_hit"] = vals.get("SQC_DCACHE_HITS", 0.0) / vals["SQC_DCACHE_REQ"]
+    if "FETCH_SIZE" in vals and "WRITE_SIZE" in vals:
+        # KB per launch; one fp64 partial per wave-chunk + the tables it reads
+        chunks = 1 << (a.shape[0] - 1 - info["L"] - info["m"])
+        np_ = (a.shape[0] + 7) // 8 * 8
+        alg = chunks * 8 + 2 * (a.shape[0] - 1) * np_ * 8 + np_ * 8
+        hbm = (vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+        out.update({"hbm_bytes_per_launch": hbm, "fetch_bytes": vals["FETCH_SIZE"] * 1024.0,
+                    "write_bytes": vals["WRITE_SIZE"] * 1024.0, "algorithmic_bytes_per_launch": alg,
+                    "hbm_over_algorithmic": hbm / alg})
+    if all(k in vals for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64")):
+        steps = float(1 << (a.shape[0] - 1))
+        f64 = vals["SQ_INSTS_VALU_ADD_F64"] + vals["SQ_INSTS_VALU_MUL_F64"] + vals["SQ_INSTS_VALU_FMA_F64"]
+        out.update({"flops_per_gray_step": 64.0 * (f64 + vals["SQ_INSTS_VALU_FMA_F64"]) / steps,
+                    "fp64_insts_per_lane_step": f64 / (steps / 64.0),
+                    "fma_share": vals["SQ_INSTS_VALU_FMA_F64"] / f64})
     os.makedirs(os.path.dirname(os.path.abspath(dst)), exist_ok=True)
     with open(dst, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
-    print(json.dumps({k: v for k, v in out.items() if k != "counters"}))
+    print(json.dumps({k: v for k, v in out.items() if k not in ("counters", "kernel_ns_per_pass")}))
 
 
 if __name__ == "__main__":

@@ -62,3 +62,25 @@ for label, stats in (("return_stats", True), ("value only", False)):
     k = kms / reps * 1e3 if stats else float("nan")
     print(f"config 2 perman_shard ({label}): {wall:.1f} us per call, kernel {k:.1f} us, "
           f"host/launch overhead {wall - k:.1f} us", flush=True)
+
+# where the config 2 per-call cost goes: Python wrapper vs the C ABI call (its own wall clock, sup_stats.wall_ms)
+# vs the walk kernel (hipEvents around the walk only)
+import ctypes as C  # noqa: E402
+from superman_amd import _lib  # noqa: E402
+lib = _lib.load()
+b, dt, n = S._mat(a)
+o = S._opts(jit=1)
+out, st = C.c_double(0.0), _lib.SupStats()
+args = (b.ctypes.data, dt, n, S._KERNELS["dense"], 0, 1, C.byref(o), C.byref(out), C.byref(st))
+for _ in range(5):
+    lib.sup_perman_shard(*args)
+reps, cw, kk = 300, 0.0, 0.0
+t = time.perf_counter()
+for _ in range(reps):
+    lib.sup_perman_shard(*args)
+    cw += st.wall_ms
+    kk += st.kernel_ms
+wall = (time.perf_counter() - t) / reps * 1e6
+print(f"config 2 bare ctypes call: {wall:.1f} us per call; C ABI wall {cw / reps * 1e3:.1f} us; walk kernel "
+      f"{kk / reps * 1e3:.1f} us; inside the C call but outside the walk {(cw - kk) / reps * 1e3:.1f} us; "
+      f"Python wrapper {wall - cw / reps * 1e3:.1f} us", flush=True)
