@@ -564,15 +564,25 @@ int leaf_compute(const LeafCtx& c, const double* a, int n, double* out, sup_stat
 // one device, the single-device schedule, a kernel request the batch kernels
 // serve, and no checkpoint.  Leaves whose plan turns out otherwise (a
 // segmented or SkipPer plan) still go one at a time.
+int leaf_workers();
+int leaf_batch_max();
 bool leaf_batching(const LeafCtx& c) {
-  const char* e = std::getenv("SUP_LEAF_BATCH");
-  if (e && std::atoi(e) <= 1) return false;
+  if (leaf_batch_max() <= 1) return false;
   return !c.on_cpu && c.sched == SUP_SCHED_SINGLE && c.o.use_rccl == 0 &&
          (c.kernel == SUP_KERNEL_DENSE || c.kernel == SUP_KERNEL_SPARYSER || c.kernel == SUP_KERNEL_DENSE_PLAIN);
 }
+// Default: batches of 16 when the leaves run one worker at a time, none with
+// several workers.  Measured on dwt_59 (145,798 n = 30 leaves, one MI355X,
+// profiles/r4/probe_reduce_batch.log): one worker 65.2 s -> 46.7 s with
+// batches of 16 (1.12e12 -> 1.56e12 leaf Gray steps/s); with 8 workers the
+// concurrent one-leaf launches already fill the GPU (37.8 s, 1.93e12, ~90 % of
+// the prefix-blocked walk's issue bound) and batches of 16 are slower (39.6 s:
+// the batch kernel holds its leaf's table pointers in SGPRs, 34 SGPR spills
+// against 12 in the one-leaf kernel at n = 30).
 int leaf_batch_max() {
   const char* e = std::getenv("SUP_LEAF_BATCH");
-  return e ? std::max(1, std::min(kMaxBatchLeaves, std::atoi(e))) : 16;
+  if (e) return std::max(1, std::min(kMaxBatchLeaves, std::atoi(e)));
+  return leaf_workers() == 1 ? 16 : 1;
 }
 
 // Several leaves of order n: each planned as sup_perman plans it (the same

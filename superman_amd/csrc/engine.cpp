@@ -740,8 +740,10 @@ struct DeviceCtx {
   size_t x0dd_cap = 0;
   size_t visited_cap = 0;
   unsigned* d_counter = nullptr;
+  bool counter_zero = false;  // d_counter known to be 0 (the last run_range's reduction zeroed it)
   double* d_result = nullptr;
-  double* h_result = nullptr;  // pinned host slot: the result's D2H without a pageable staging copy
+  double* h_result = nullptr;  // pinned host slot (mapped): the reduction writes the result here
+  double* m_result = nullptr;  // its device address (nullptr: copy from d_result instead)
   // leaf batches (run_range_batch): packed tables, descriptors, results
   double* d_batch = nullptr;
   size_t batch_cap = 0;
@@ -854,7 +856,11 @@ static int get_ctx(int dev, DeviceCtx** out) {
     SUP_HIP(hipMalloc(&c->d_rowmask, SUP_MAX_N * sizeof(uint64_t)));
     SUP_HIP(hipMalloc(&c->d_counter, 64));
     SUP_HIP(hipMalloc(&c->d_result, 64));
-    SUP_HIP(hipHostMalloc(&c->h_result, 64, hipHostMallocDefault));
+    // the result slot is host memory the device writes directly (mapped,
+    // coherent): the reduction's last pass stores the partial there, so no
+    // D2H copy is queued per call; d_result stays for the -R slot copy
+    SUP_HIP(hipHostMalloc(&c->h_result, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    if (hipHostGetDevicePointer((void**)&c->m_result, c->h_result, 0) != hipSuccess) c->m_result = nullptr;
     g_ctx[slot] = std::move(c);
   }
   *out = g_ctx[slot].get();
@@ -917,7 +923,9 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
                            hipMemcpyHostToDevice, s));
     c->tables_uid = P.uid;
   }
-  SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
+  // the queue head: zeroed by the previous run_range's reduction pass, else here
+  if (!c->counter_zero) SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
+  c->counter_zero = false;
 
   int occ_seg = 0, occ_lds = 0;
   if (seg && (rc = jit_occupancy(c->phys, P, &occ_seg, &r.compile_ms))) return rc;
@@ -996,15 +1004,19 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     SUP_HIP(launch_walk(P.kind, P.n, p, (int)grid, s));
   }
   SUP_HIP(hipEventRecord(c->ev1, s));
-  SUP_HIP(launch_pairwise_reduce(c->d_chunk, count, c->d_scratch, c->d_result, s));
+  // (the -R combine copies d_result into its slot on the device; one chunk is a copy, not a pass)
+  const bool direct = c->m_result && !slot && count > 1;
+  SUP_HIP(launch_pairwise_reduce(c->d_chunk, count, c->d_scratch, direct ? c->m_result : c->d_result, s,
+                                 c->d_counter));
   if (slot) SUP_HIP(hipMemcpyAsync(slot, c->d_result, sizeof(double), hipMemcpyDeviceToDevice, s));
-  SUP_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
+  if (!direct) SUP_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
   std::vector<unsigned> vis;
   if (visited) {
     vis.resize(count);
     SUP_HIP(hipMemcpyAsync(vis.data(), c->d_visited, count * sizeof(unsigned), hipMemcpyDeviceToHost, s));
   }
   SUP_HIP(hipStreamSynchronize(s));
+  c->counter_zero = count > 1;  // the reduction's first pass zeroed it (one chunk: a copy, no pass)
   float ms = 0.f;
   SUP_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   r.partial = *c->h_result;
@@ -1030,7 +1042,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
 bool batchable(const Plan& a, const Plan& b) {
   return (a.kind == kWalkDense || a.kind == kWalkSparse) && a.kind == b.kind && !a.lds && !b.lds && a.n == b.n &&
          a.lay.L == b.lay.L && a.lay.m == b.lay.m && a.lay.h == b.lay.h && a.cols.size() == b.cols.size() &&
-         a.x0.size() == b.x0.size() && a.lay.chunks() >= 1;
+         a.x0.size() == b.x0.size() && a.lay.chunks() >= 1 && a.lay.chunks() <= (1ull << 26);  // 32-bit chunk ids
 }
 
 int run_range_batch(int dev, const std::vector<const Plan*>& plans, std::vector<double>& partial, double* kernel_ms) {
@@ -1080,6 +1092,7 @@ int run_range_batch(int dev, const std::vector<const Plan*>& plans, std::vector<
   SUP_HIP(hipMemcpyAsync(c->d_batch, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemcpyAsync(c->d_desc, desc.data(), K * sizeof(LeafDesc), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
+  c->counter_zero = false;  // this walk leaves the queue head nonzero
   int& occ = c->occ_batch[P0.kind == kWalkSparse][P0.n];
   if (occ == 0) {
     int b = 0;
@@ -1154,6 +1167,7 @@ int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1,
   SUP_HIP(hipMemcpyAsync(c->d_cols, P.cols.data(), P.cols.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemcpyAsync(c->d_x0, P.x0.data(), P.x0.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
+  c->counter_zero = false;  // this walk leaves the queue head nonzero
   WalkParams p{};
   p.cols = c->d_cols;
   p.x0 = c->d_x0;
@@ -1215,6 +1229,7 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
   SUP_HIP(hipMemcpyAsync(c->d_cols, P.cols.data(), P.cols.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemcpyAsync(c->d_x0dd, x0dd.data(), x0dd.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
+  c->counter_zero = false;  // this walk leaves the queue head nonzero
   WalkParams p{};
   p.cols = c->d_cols;
   p.x0 = c->d_x0dd;

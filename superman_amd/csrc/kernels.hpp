@@ -93,8 +93,10 @@ hipError_t dd_occupancy(int n, int* blocks_per_cu);
 // Fixed-order pairwise reduction of `count` doubles into *out (64-way passes,
 // zero padded; mirrored by oracle/oracle.c orc_pairwise_reduce).  `scratch`
 // must hold ceil(count/64) + ceil(count/4096) + ... doubles.
+// reset_counter (optional): zeroed by the first pass, which runs after the
+// walk that used it (the next launch's queue then needs no memset).
 hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scratch, double* out,
-                                  hipStream_t s);
+                                  hipStream_t s, unsigned int* reset_counter = nullptr);
 uint64_t pairwise_scratch_size(uint64_t count);
 // The same tree over each of `nseg` consecutive segments of `count` doubles
 // (a leaf batch's chunk partials): out[i] is bit-identical to

@@ -12,9 +12,11 @@
 namespace sup {
 
 __global__ __launch_bounds__(kBlock) void pairwise64_pass(const double* __restrict__ in, uint64_t count,
-                                                          double* __restrict__ out, uint64_t groups) {
+                                                          double* __restrict__ out, uint64_t groups,
+                                                          unsigned int* reset) {
   const uint64_t g = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63u;
+  if (reset && blockIdx.x == 0 && threadIdx.x == 0) *reset = 0u;  // the walk before this pass is done with it
   if (g >= groups) return;  // whole wave exits together (g is wave-uniform)
   const uint64_t i = g * 64u + lane;
   const double v = (i < count) ? in[i] : 0.0;
@@ -44,9 +46,11 @@ __global__ __launch_bounds__(kBlock) void pairwise64_pass_seg(const double* __re
 // the last group) as the next pairwise64_pass would: out[b] is bit-identical
 // to two consecutive pairwise64_pass launches (round 4: half the launches).
 __global__ __launch_bounds__(kBlock) void pairwise4096_pass(const double* __restrict__ in, uint64_t count,
-                                                            double* __restrict__ out, uint64_t groups1) {
+                                                            double* __restrict__ out, uint64_t groups1,
+                                                            unsigned int* reset) {
   __shared__ double g1[64];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  if (reset && blockIdx.x == 0 && threadIdx.x == 0) *reset = 0u;
   const uint64_t base = (uint64_t)blockIdx.x * 64u;
   for (uint32_t k = w; k < 64u; k += kWavesPerBlock) {
     const uint64_t g = base + k;  // level-1 group
@@ -74,17 +78,20 @@ uint64_t pairwise_scratch_size(uint64_t count) {
 }
 
 hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scratch, double* out,
-                                  hipStream_t s) {
+                                  hipStream_t s, unsigned int* reset_counter) {
   if (count == 0) return hipMemsetAsync(out, 0, sizeof(double), s);
   if (count == 1) return hipMemcpyAsync(out, in, sizeof(double), hipMemcpyDeviceToDevice, s);
   const double* src = in;
   double* dst = scratch;
+  unsigned int* reset = reset_counter;  // zeroed by the first pass
   while (count > 1) {
     const uint64_t groups = (count + 63) / 64;
     if (groups > 1) {  // two levels at once
       const uint64_t groups2 = (groups + 63) / 64;
       double* target = (groups2 == 1) ? out : dst;
-      hipLaunchKernelGGL(pairwise4096_pass, dim3((unsigned)groups2), dim3(kBlock), 0, s, src, count, target, groups);
+      hipLaunchKernelGGL(pairwise4096_pass, dim3((unsigned)groups2), dim3(kBlock), 0, s, src, count, target, groups,
+                         reset);
+      reset = nullptr;
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
       src = target;
@@ -94,7 +101,8 @@ hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scra
     }
     const uint64_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
     double* target = (groups == 1) ? out : dst;
-    hipLaunchKernelGGL(pairwise64_pass, dim3((unsigned)blocks), dim3(kBlock), 0, s, src, count, target, groups);
+    hipLaunchKernelGGL(pairwise64_pass, dim3((unsigned)blocks), dim3(kBlock), 0, s, src, count, target, groups, reset);
+    reset = nullptr;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     src = target;

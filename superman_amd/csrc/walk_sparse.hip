@@ -115,27 +115,28 @@ __global__ __launch_bounds__(kBlock) void walk_sparse_batch(WalkParams p, LeafBa
   const uint32_t lane = threadIdx.x & 63u;
   const bool lane_valid = lane < (1u << p.L);
   const uint32_t lane_par = __builtin_popcount(lane) & 1u;
-  const uint64_t cmask = (1ull << b.leaf_bits) - 1ull;
   const uint32_t T = 1u << p.m;
   const uint32_t offL = 2u * (uint32_t)p.L * pad8(N) * 8u;
+  // a batch holds fewer than 2^32 chunks (run_range_batch): 32-bit indices
+  const uint32_t count = (uint32_t)p.chunk_count, group = (uint32_t)p.group;
 
-  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {
-    const uint64_t a0 = (uint64_t)g * p.group;
+  for (uint32_t g = next_chunk(p.counter); g * group < count; g = next_chunk(p.counter)) {
+    const uint32_t a0 = g * group;
     typedef const __attribute__((address_space(4))) LeafDesc cdesc;
     cdesc* dp = (cdesc*)b.leaves + (a0 >> b.leaf_bits);  // scalar loads: the leaf is wave-uniform
-    WalkParams q = p;
-    q.cols = dp->cols, q.x0 = dp->x0, q.nb_lo = dp->nb_lo, q.nb_hi = dp->nb_hi;
+    // only the fields the chunk walk reads (chunk_start: x0, cols, L, m; the step: cols, nblk)
+    WalkParams q{};
+    q.cols = dp->cols, q.x0 = dp->x0, q.nb_lo = dp->nb_lo, q.nb_hi = dp->nb_hi, q.L = p.L, q.m = p.m;
     const int nb0 = nb_of(q, 0);
+    const uint32_t c0 = a0 & ((1u << b.leaf_bits) - 1u);
     double keep = 0.0;
-    for (uint32_t j = 0; j < (uint32_t)p.group; ++j) {
-      const uint64_t a = a0 + j;
-      if (a >= p.chunk_count) break;
-      const double acc = sparse_chunk<N>(q, a & cmask, lane, lane_par, T, offL, nb0);
+    for (uint32_t j = 0; j < group; ++j) {
+      if (a0 + j >= count) break;
+      const double acc = sparse_chunk<N>(q, c0 + j, lane, lane_par, T, offL, nb0);
       const double part = wave_sum(lane_valid ? acc : 0.0);
       keep = (lane == j) ? part : keep;
     }
-    const uint64_t a = a0 + lane;
-    if (lane < (uint32_t)p.group && a < p.chunk_count) p.chunk_out[a] = keep;
+    if (lane < group && a0 + lane < count) p.chunk_out[a0 + lane] = keep;
   }
 }
 
