@@ -2254,7 +2254,7 @@ uint64_t jit_toolchain_hash() {
 }
 
 // Recorded segmented-walk choices: a small text file next to the code objects,
-// "supseg 2 <m> <b> <budget> <count> <order...>".
+// "supseg 3 <m> <b> <budget> <cc cap> <count> <order...>".
 bool seg_choice_load(uint64_t key, int* m, SegChoice* c) {
   const std::string dir = cache_dir();
   if (dir.empty()) return false;
