@@ -483,12 +483,24 @@ static uint64_t knob_hash_env() { return knob_hash(); }
 int plan_for_shared(const double* A, int n, sup_kernel kernel, const Layout& lay, std::shared_ptr<const Plan>& out,
                     int jit, int ndev, int dev) {
   const size_t nn = (size_t)n * n;
-  uint64_t h = 1469598103934665603ull;
-  for (size_t i = 0; i < nn; ++i) {
+  // in-process cache key only (the entry also keeps the matrix and compares
+  // it): four independent FNV-style lanes, so the multiply chain is a quarter
+  // as long (n = 32: 1.7 -> ~0.5 us per call)
+  uint64_t l[4] = {1469598103934665603ull, 0x9e3779b97f4a7c15ull, 0xc2b2ae3d27d4eb4full, 0x165667b19e3779f9ull};
+  size_t i = 0;
+  for (; i + 4 <= nn; i += 4)
+    for (int k = 0; k < 4; ++k) {
+      uint64_t b;
+      std::memcpy(&b, A + i + k, 8);
+      l[k] = (l[k] ^ b) * 1099511628211ull;
+    }
+  for (; i < nn; ++i) {
     uint64_t b;
     std::memcpy(&b, A + i, 8);
-    h = (h ^ b) * 1099511628211ull;
+    l[0] = (l[0] ^ b) * 1099511628211ull;
   }
+  uint64_t h = l[0];
+  for (int k = 1; k < 4; ++k) h = (h ^ l[k]) * 1099511628211ull;
   // ndev only feeds auto mode's compile-or-not decision
   const PlanKey key{h, n, (int)kernel, lay.L, lay.m, jit, jit == 0 ? ndev : 0, lay.fixed, knob_hash()};
   {
@@ -744,6 +756,9 @@ struct DeviceCtx {
   double* d_result = nullptr;
   double* h_result = nullptr;  // pinned host slot (mapped): the reduction writes the result here
   double* m_result = nullptr;  // its device address (nullptr: copy from d_result instead)
+  unsigned* h_flag = nullptr;  // beside h_result: the sequence number of the last call whose result is there
+  unsigned* m_flag = nullptr;
+  unsigned flag_seq = 0;
   // leaf batches (run_range_batch): packed tables, descriptors, results
   double* d_batch = nullptr;
   size_t batch_cap = 0;
@@ -861,10 +876,40 @@ static int get_ctx(int dev, DeviceCtx** out) {
     // D2H copy is queued per call; d_result stays for the -R slot copy
     SUP_HIP(hipHostMalloc(&c->h_result, 64, hipHostMallocMapped | hipHostMallocCoherent));
     if (hipHostGetDevicePointer((void**)&c->m_result, c->h_result, 0) != hipSuccess) c->m_result = nullptr;
+    c->h_flag = reinterpret_cast<unsigned*>(c->h_result + 1);
+    *c->h_flag = 0u;
+    c->m_flag = c->m_result ? reinterpret_cast<unsigned*>(c->m_result + 1) : nullptr;
     g_ctx[slot] = std::move(c);
   }
   *out = g_ctx[slot].get();
   return SUP_OK;
+}
+
+// Per-call completion (round 4, tools/probe_launch.hip, profiles/r4/probe_launch_b.log):
+// around a 500 us kernel, marker events + one more launch + hipStreamSynchronize
+// cost 18.9 us beyond the kernel; waiting instead for a sequence number the
+// last kernel stores in mapped host memory, 11.9 us.  (Events carried by the
+// launch itself, hipExtModuleLaunchKernel, measured worse: 23.7 / 15.5 us.)
+// So a call whose result lands in mapped host memory waits for the sequence
+// number the reduction's last pass stores after it; SUP_FLAG_WAIT=0 restores
+// the stream sync (A/B).
+static bool result_flag_wait() {
+  static const bool on = [] {
+    const char* e = std::getenv("SUP_FLAG_WAIT");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+// Spin on the flag for up to 2 ms (a short walk's wait); false: not seen yet
+// (a long walk, or a fault that stopped the stream) — the caller then blocks
+// in hipStreamSynchronize, which also reports the stream's error.
+static bool wait_flag(const unsigned* flag, unsigned seq) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned i = 1;; ++i) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return true;
+    __builtin_ia32_pause();
+    if ((i & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) return false;
+  }
 }
 
 template <class T>
@@ -1006,8 +1051,11 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   SUP_HIP(hipEventRecord(c->ev1, s));
   // (the -R combine copies d_result into its slot on the device; one chunk is a copy, not a pass)
   const bool direct = c->m_result && !slot && count > 1;
+  // a direct result also carries a sequence number the host can wait on
+  const bool flagged = direct && !visited && result_flag_wait();
+  const unsigned seq = ++c->flag_seq;
   SUP_HIP(launch_pairwise_reduce(c->d_chunk, count, c->d_scratch, direct ? c->m_result : c->d_result, s,
-                                 c->d_counter));
+                                 c->d_counter, flagged ? c->m_flag : nullptr, seq));
   if (slot) SUP_HIP(hipMemcpyAsync(slot, c->d_result, sizeof(double), hipMemcpyDeviceToDevice, s));
   if (!direct) SUP_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
   std::vector<unsigned> vis;
@@ -1015,10 +1063,18 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     vis.resize(count);
     SUP_HIP(hipMemcpyAsync(vis.data(), c->d_visited, count * sizeof(unsigned), hipMemcpyDeviceToHost, s));
   }
-  SUP_HIP(hipStreamSynchronize(s));
+  if (!flagged || !wait_flag(c->h_flag, seq)) SUP_HIP(hipStreamSynchronize(s));
   c->counter_zero = count > 1;  // the reduction's first pass zeroed it (one chunk: a copy, no pass)
   float ms = 0.f;
-  SUP_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  hipError_t ee = hipEventElapsedTime(&ms, c->ev0, c->ev1);
+  if (ee == hipErrorNotReady) {  // (after a flag wait the walk is done; its event may not show it yet)
+    SUP_HIP(hipEventSynchronize(c->ev1));
+    ee = hipEventElapsedTime(&ms, c->ev0, c->ev1);
+  }
+  if (ee != hipSuccess) {
+    set_error(std::string("hipEventElapsedTime: ") + hipGetErrorString(ee));
+    return SUP_EHIP;
+  }
   r.partial = *c->h_result;
   r.kernel_ms = ms;
   r.grid = (int)grid;

@@ -95,8 +95,11 @@ hipError_t dd_occupancy(int n, int* blocks_per_cu);
 // must hold ceil(count/64) + ceil(count/4096) + ... doubles.
 // reset_counter (optional): zeroed by the first pass, which runs after the
 // walk that used it (the next launch's queue then needs no memset).
+// flag (optional, count > 1): the last pass stores `seq` there after *out,
+// system-scope ordered (mapped host memory: the host waits on it).
 hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scratch, double* out,
-                                  hipStream_t s, unsigned int* reset_counter = nullptr);
+                                  hipStream_t s, unsigned int* reset_counter = nullptr, unsigned int* flag = nullptr,
+                                  unsigned seq = 0);
 uint64_t pairwise_scratch_size(uint64_t count);
 // The same tree over each of `nseg` consecutive segments of `count` doubles
 // (a leaf batch's chunk partials): out[i] is bit-identical to

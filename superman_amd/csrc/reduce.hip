@@ -13,7 +13,7 @@ namespace sup {
 
 __global__ __launch_bounds__(kBlock) void pairwise64_pass(const double* __restrict__ in, uint64_t count,
                                                           double* __restrict__ out, uint64_t groups,
-                                                          unsigned int* reset) {
+                                                          unsigned int* reset, unsigned int* flag, unsigned seq) {
   const uint64_t g = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   const uint32_t lane = threadIdx.x & 63u;
   if (reset && blockIdx.x == 0 && threadIdx.x == 0) *reset = 0u;  // the walk before this pass is done with it
@@ -21,7 +21,13 @@ __global__ __launch_bounds__(kBlock) void pairwise64_pass(const double* __restri
   const uint64_t i = g * 64u + lane;
   const double v = (i < count) ? in[i] : 0.0;
   const double s = wave_sum(v);
-  if (lane == 0) out[g] = s;
+  if (lane == 0) {
+    out[g] = s;
+    if (flag) {  // the last pass (one group): the call's result, then its sequence number
+      __threadfence_system();
+      __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // One 64-way pass over each of nseg segments of `count` values: group g of
@@ -47,7 +53,7 @@ __global__ __launch_bounds__(kBlock) void pairwise64_pass_seg(const double* __re
 // to two consecutive pairwise64_pass launches (round 4: half the launches).
 __global__ __launch_bounds__(kBlock) void pairwise4096_pass(const double* __restrict__ in, uint64_t count,
                                                             double* __restrict__ out, uint64_t groups1,
-                                                            unsigned int* reset) {
+                                                            unsigned int* reset, unsigned int* flag, unsigned seq) {
   __shared__ double g1[64];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   if (reset && blockIdx.x == 0 && threadIdx.x == 0) *reset = 0u;
@@ -64,7 +70,13 @@ __global__ __launch_bounds__(kBlock) void pairwise4096_pass(const double* __rest
   __syncthreads();
   if (w == 0) {
     const double s = wave_sum(g1[lane]);
-    if (lane == 0) out[blockIdx.x] = s;
+    if (lane == 0) {
+      out[blockIdx.x] = s;
+      if (flag) {  // the last pass (one block)
+        __threadfence_system();
+        __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
 }
 
@@ -78,7 +90,7 @@ uint64_t pairwise_scratch_size(uint64_t count) {
 }
 
 hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scratch, double* out,
-                                  hipStream_t s, unsigned int* reset_counter) {
+                                  hipStream_t s, unsigned int* reset_counter, unsigned int* flag, unsigned seq) {
   if (count == 0) return hipMemsetAsync(out, 0, sizeof(double), s);
   if (count == 1) return hipMemcpyAsync(out, in, sizeof(double), hipMemcpyDeviceToDevice, s);
   const double* src = in;
@@ -90,7 +102,7 @@ hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scra
       const uint64_t groups2 = (groups + 63) / 64;
       double* target = (groups2 == 1) ? out : dst;
       hipLaunchKernelGGL(pairwise4096_pass, dim3((unsigned)groups2), dim3(kBlock), 0, s, src, count, target, groups,
-                         reset);
+                         reset, groups2 == 1 ? flag : nullptr, seq);
       reset = nullptr;
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
@@ -101,7 +113,8 @@ hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scra
     }
     const uint64_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
     double* target = (groups == 1) ? out : dst;
-    hipLaunchKernelGGL(pairwise64_pass, dim3((unsigned)blocks), dim3(kBlock), 0, s, src, count, target, groups, reset);
+    hipLaunchKernelGGL(pairwise64_pass, dim3((unsigned)blocks), dim3(kBlock), 0, s, src, count, target, groups, reset,
+                       groups == 1 ? flag : nullptr, seq);
     reset = nullptr;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

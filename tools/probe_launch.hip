@@ -6,6 +6,7 @@
 //   hipcc --offload-arch=gfx950 -O2 -o tools/probe_launch tools/probe_launch.hip
 //   tools/probe_launch [spin]      (spin: hipDeviceScheduleSpin before the context exists)
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <chrono>
 #include <cstdio>
@@ -33,6 +34,14 @@ __global__ void tiny_flag(double* out, volatile unsigned* flag, unsigned seq, do
     __threadfence_system();
     flag[0] = seq;
   }
+}
+
+// a walk-sized kernel: every wave busy for `ticks` of the 100 MHz constant clock
+__global__ void busy(double* out, long long ticks) {
+  const long long t0 = wall_clock64();
+  double a = threadIdx.x;
+  while (wall_clock64() - t0 < ticks) a = a * 1.0000001 + 1e-9;
+  if (a == 12345.0) out[1] = a;
 }
 
 static double now_us() {
@@ -68,6 +77,77 @@ int main(int argc, char** argv) {
     std::printf("%-58s %7.2f us per call%s\n", name, t, spin ? " (spin)" : "");
   };
 
+  // the engine's sequence around a 500 us kernel on the whole chip: wall - event time
+  // is what a call costs beyond its walk
+  for (int poll = 0; poll < 2; ++poll) {
+    double wall = 0, kern = 0;
+    const int RB = 400;
+    for (int i = 0; i < RB + 20; ++i) {
+      const double t0 = now_us();
+      CK(hipEventRecord(e0, s));
+      hipLaunchKernelGGL(busy, dim3(2048), dim3(256), 0, s, d, 50000LL);
+      CK(hipEventRecord(e1, s));
+      hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s, d, 1.0);
+      if (poll) {
+        hipError_t q;
+        while ((q = hipStreamQuery(s)) == hipErrorNotReady) {
+        }
+        CK(q);
+      } else {
+        CK(hipStreamSynchronize(s));
+      }
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double t1 = now_us();
+      if (i >= 20) wall += t1 - t0, kern += ms * 1000.0;
+    }
+    std::printf("500 us kernel + ev pair + 1 launch, %s: wall %.2f us, kernel %.2f us, outside %.2f us%s\n",
+                poll ? "poll hipStreamQuery" : "hipStreamSynchronize", wall / RB, kern / RB, (wall - kern) / RB,
+                spin ? " (spin)" : "");
+  }
+  // the same with the events carried by the launch itself (hipExtLaunchKernel:
+  // the dispatch's own timestamps, no marker packets), waiting by sync or by
+  // polling a flag the last kernel writes to mapped host memory
+  unsigned fseq = 1000000;
+  for (int mode = 0; mode < 3; ++mode) {
+    double wall = 0, kern = 0;
+    const int RB = 400;
+    for (int i = 0; i < RB + 20; ++i) {
+      const double t0 = now_us();
+      if (mode == 2) {
+        CK(hipEventRecord(e0, s));
+        hipLaunchKernelGGL(busy, dim3(2048), dim3(256), 0, s, d, 50000LL);
+        CK(hipEventRecord(e1, s));
+      } else {
+        hipExtLaunchKernelGGL(busy, dim3(2048), dim3(256), 0, s, e0, e1, 0, d, 50000LL);
+      }
+      ++fseq;
+      hipLaunchKernelGGL(tiny_flag, dim3(1), dim3(64), 0, s, m, mf, fseq, 1.0);
+      if (mode >= 1) {
+        while (__atomic_load_n(hf, __ATOMIC_ACQUIRE) != fseq) {
+        }
+        CK(hipEventSynchronize(e1));
+      } else {
+        CK(hipStreamSynchronize(s));
+      }
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double t1 = now_us();
+      if (i >= 20) wall += t1 - t0, kern += ms * 1000.0;
+    }
+    const char* names[] = {"ext launch(events) + flag kernel, hipStreamSynchronize",
+                           "ext launch(events) + flag kernel, poll flag",
+                           "ev + launch + ev + flag kernel, poll flag"};
+    std::printf("500 us kernel, %s: wall %.2f us, kernel %.2f us, outside %.2f us%s\n", names[mode], wall / RB,
+                kern / RB, (wall - kern) / RB, spin ? " (spin)" : "");
+  }
+  run("ext launch(events) + 2 launches + sync + elapsed", [&](int) {
+    hipExtLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s, e0, e1, 0, d, 1.0);
+    for (int k = 0; k < 2; ++k) hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s, d, 1.0);
+    CK(hipStreamSynchronize(s));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+  });
   run("launch + sync", [&](int) {
     hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s, d, 1.0);
     CK(hipStreamSynchronize(s));
@@ -98,6 +178,29 @@ int main(int argc, char** argv) {
     CK(hipStreamSynchronize(s));
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
+  });
+  run("ev + launch + ev + 2 launches + poll hipStreamQuery + elapsed", [&](int) {
+    CK(hipEventRecord(e0, s));
+    hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s, d, 1.0);
+    CK(hipEventRecord(e1, s));
+    for (int k = 0; k < 2; ++k) hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s, d, 1.0);
+    hipError_t q;
+    while ((q = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    CK(q);
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+  });
+  run("launch + poll hipStreamQuery", [&](int) {
+    hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s, d, 1.0);
+    hipError_t q;
+    while ((q = hipStreamQuery(s)) == hipErrorNotReady) {
+    }
+    CK(q);
+  });
+  run("hipEventRecord alone [host cost]", [&](int i) {
+    CK(hipEventRecord(e0, s));
+    if (i % 64 == 63) CK(hipStreamSynchronize(s));
   });
   unsigned seq = 0;
   run("ev + launch + ev + launch + flag launch, poll flag + ev sync", [&](int) {
