@@ -446,9 +446,12 @@ def main():
 
     plan_keys = []  # every timed walk's per-rank plan fingerprints (all equal, or check_plans_agree raised)
 
-    def timed(a, kernel=None, jit=None):
+    def timed(a, kernel=None, jit=None, min_seconds=0.0):
         """W untimed + K timed steps of one whole permanent of `a`; returns
-        (elapsed max over ranks, permanent, mean walk-kernel ms, stats, compile ms)."""
+        (elapsed max over ranks, permanent, mean walk-kernel ms, stats, compile ms, K).
+        K = --steps, or (min_seconds > 0: the short config lines) enough steps
+        for ~min_seconds, so the barriers around the timed region do not
+        dominate a sub-millisecond step (at most 4000, the same K on every rank)."""
         n = a.shape[0]
         kernel = args.kernel if kernel is None else kernel
         jit = args.jit if jit is None else jit
@@ -469,12 +472,26 @@ def main():
                 part = combine(part, rank, world, tdev)  # one RCCL all-reduce over xGMI
             return (4 * (n & 1) - 2) * part, k_ms
 
+        one = None
         for _ in range(args.warmup):
+            t1 = time.perf_counter()
             step()
+            one = time.perf_counter() - t1
+        steps = args.steps
+        if min_seconds > 0:
+            if one is None:
+                t1 = time.perf_counter()
+                step()
+                one = time.perf_counter() - t1
+            steps = max(args.steps, min(4000, int(min_seconds / max(one, 1e-6)) + 1))
+            if world > 1:
+                t = torch.tensor([steps], dtype=torch.float64, device=tdev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                steps = int(t.item())
         barrier()
         t0 = time.perf_counter()
         kms, perm = [], None
-        for _ in range(args.steps):
+        for _ in range(steps):
             perm, k_ms = step()
             kms.append(k_ms)
         barrier()
@@ -484,7 +501,7 @@ def main():
             t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        return elapsed, perm, sum(kms) / len(kms), st, prep["compile_ms"]
+        return elapsed, perm, sum(kms) / len(kms), st, prep["compile_ms"], steps
 
     walk_names = {0: "dense", 1: "prefix-blocked", 2: "skipper", 3: "segmented (pattern-specialised)",
                   4: "dense, X in LDS"}
@@ -536,14 +553,14 @@ def main():
 
     a = load(args.matrix)
     n = a.shape[0]
-    elapsed, perm, k_ms, st, compile_ms = timed(a)
+    elapsed, perm, k_ms, st, compile_ms, _ = timed(a)
 
     # companion densities (north star: 0.2 and 0.5; 0.9 near-dense), same shards / all-reduce / clock
     also = []
     for path in [p for p in args.also.split(",") if p and os.path.abspath(p) != os.path.abspath(args.matrix)]:
         b = load(path)
         nb = b.shape[0]
-        e2, perm2, kms2, st2, _ = timed(b)
+        e2, perm2, kms2, st2, _, _ = timed(b)
         also.append({"matrix": os.path.basename(path).replace("__", "/"), "n": nb,
                      "density": round(float((b != 0).sum()) / (nb * nb), 4),
                      "value": args.steps * (1 << (nb - 1)) / e2, "unit": "gray-steps/s",
@@ -570,16 +587,16 @@ def main():
                  "synth44_0.15_int", 2, "skip", 0)):
             b = load(os.path.join(fx, fname), prep)
             nb = b.shape[0]
-            e2, perm2, kms2, st2, _ = timed(b, kernel, jit)
-            configs.append({"config": label, "matrix": fname.replace("__", "/"), "n": nb,
-                            "value": args.steps * (1 << (nb - 1)) / e2, "unit": "gray-steps/s (nominal)",
-                            "ms_per_step": e2 / args.steps * 1e3, "kernel_ms_avg": kms2,
+            e2, perm2, kms2, st2, _, k2 = timed(b, kernel, jit, min_seconds=0.25)
+            configs.append({"config": label, "matrix": fname.replace("__", "/"), "n": nb, "steps": k2,
+                            "value": k2 * (1 << (nb - 1)) / e2, "unit": "gray-steps/s (nominal)",
+                            "ms_per_step": e2 / k2 * 1e3, "kernel_ms_avg": kms2,
                             "walk": walk_names[st2["walk_kind"]],
                             # states evaluated / Gray steps (SkipPer's jumps and the segmented
                             # walk's chunk skip make it < 1); SURVEY 8(d): visited steps/s beside
                             # the nominal rate
                             "visited_frac": st2["visited_steps"] * world / float(1 << (nb - 1)),
-                            "visited_steps_per_s": args.steps * st2["visited_steps"] * world / e2,
+                            "visited_steps_per_s": k2 * st2["visited_steps"] * world / e2,
                             "permanent": perm2})
 
     # every rank's walk-kernel time (strong-scaling diagnosis: the slowest rank sets the step)
