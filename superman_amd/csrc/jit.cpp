@@ -1217,7 +1217,7 @@ struct Gen {
         // a class reading another class's stream loads each piece through a
         // fresh opaque base: otherwise LLVM merges the two steps' loads of the
         // same piece and keeps them live across the block (SGPR spills)
-        static const bool fresh = std::getenv("SUP_JIT_FRESHBASE") && std::atoi(std::getenv("SUP_JIT_FRESHBASE"));
+        const bool fresh = std::getenv("SUP_JIT_FRESHBASE") && std::atoi(std::getenv("SUP_JIT_FRESHBASE"));
         const std::string jb = own_stream[c] && !fresh ? "jt" : "(const char*)opaque_c(p.jtab, 0u)";
         const int pc = piece("((cjdbl8*)(" + jb + " + " + std::to_string((cbase + pos - pos % 8) * 8) + "u))[0]");
         it.text += pref(pc, pos % 8);
@@ -1230,7 +1230,7 @@ struct Gen {
 
   void emit_items(const std::vector<Item>& items, const char* ind) {
     const int kp = P.seg_kp;
-    static const bool pf = std::getenv("SUP_JIT_PF") ? std::atoi(std::getenv("SUP_JIT_PF")) != 0 : true;
+    const bool pf = std::getenv("SUP_JIT_PF") ? std::atoi(std::getenv("SUP_JIT_PF")) != 0 : true;
     if (items.empty()) return;
     std::vector<std::pair<size_t, size_t>> reg;
     std::vector<std::vector<int>> rp;
@@ -1243,7 +1243,7 @@ struct Gen {
           if (std::find(need.begin(), need.end(), pc) == need.end()) need.push_back(pc);
       return need;
     };
-    static const bool xstep = std::getenv("SUP_JIT_XSTEP") ? std::atoi(std::getenv("SUP_JIT_XSTEP")) != 0 : true;
+    const bool xstep = std::getenv("SUP_JIT_XSTEP") ? std::atoi(std::getenv("SUP_JIT_XSTEP")) != 0 : true;
     for (size_t i = 0; i < items.size();) {
       std::vector<int> pcs;
       size_t j = i;
