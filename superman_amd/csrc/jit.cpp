@@ -2054,7 +2054,9 @@ void write_file_atomic(const std::string& dir, const std::string& name, const st
       cur = dir.substr(0, i);
       ::mkdir(cur.c_str(), 0755);
     }
-  const std::string tmp = dir + "/." + name + "." + std::to_string(::getpid());
+  // one temporary per process and thread (threads of one process may write the same entry at once)
+  const std::string tmp = dir + "/." + name + "." + std::to_string(::getpid()) + "." +
+                          std::to_string(std::hash<std::thread::id>()(std::this_thread::get_id()));
   FILE* f = std::fopen(tmp.c_str(), "wb");
   if (!f) return;  // cache is best effort
   const bool ok = std::fwrite(data.data(), 1, data.size(), f) == data.size();
