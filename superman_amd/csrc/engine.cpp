@@ -315,8 +315,11 @@ static constexpr double kLaneOpsPerSec = 3.7e13;
 static constexpr double kJitMinSavingSec = 3.0;
 // Once this host has made a cold segmented plan (make_seg_plan records its
 // cost next to the code objects: ~0.4 s at n = 40 on a GPU box's 16 threads,
-// 2.4-3.4 s on an 8-CPU container), auto mode's cold bar is twice that cost,
-// within [kJitColdBarMin, kJitMinSavingSec].
+// 2.4-3.4 s on an 8-CPU container), auto mode's cold bar is that cost, within
+// [kJitColdBarMin, kJitMinSavingSec]: break-even, because auto mode records its
+// first decision for a matrix and every later run follows it (AutoRecord) — a
+// walk that repays its plan on the first run repays it on every run after
+// (round 3 asked for twice the cost, when a warm run could still switch).
 static constexpr double kJitColdBarMin = 0.25;
 // When an earlier process recorded this matrix's segmented-walk choices (disk
 // cache, make_seg_plan), the plan is rebuilt in ~5-50 ms and its code object
@@ -572,7 +575,7 @@ static double auto_min_saving(const double* A, int n, const Layout& lay, int jit
   if (jit != 0 || n < kJitWarmMinN) return kJitMinSavingSec;  // below: no walk lasts even the lowest bar
   if (seg_choice_exists(seg_disk_key(A, n, lay))) return kJitWarmSavingSec;
   const double c = seg_cost_load();
-  return c > 0.0 ? std::min(kJitMinSavingSec, std::max(kJitColdBarMin, 2.0 * c)) : kJitMinSavingSec;
+  return c > 0.0 ? std::min(kJitMinSavingSec, std::max(kJitColdBarMin, c)) : kJitMinSavingSec;
 }
 
 // Auto mode's first decision per matrix and request, on disk (round 4).  The

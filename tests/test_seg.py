@@ -88,7 +88,7 @@ def test_planner_choice(sup, tmp_path, monkeypatch):
 
 def test_auto_cold_bar_follows_recorded_plan_cost(sup, tmp_path, monkeypatch):
     # make_seg_plan records what a cold plan cost on this host (cost_<toolchain>.txt);
-    # auto mode's cold bar is then twice that, within [0.25 s, 3 s]
+    # auto mode's cold bar is then that cost (break-even: its first decision is recorded), within [0.25 s, 3 s]
     monkeypatch.setenv("SUP_JIT_CACHE_DIR", str(tmp_path))
     a, _, _ = sup.read_matrix(fixture_path("double__40_0.50_0"))
     b = np.ascontiguousarray(a.T)  # another zero pattern: its choices are not on disk
