@@ -1061,10 +1061,12 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
                                  c->d_counter, flagged ? c->m_flag : nullptr, seq));
   if (slot) SUP_HIP(hipMemcpyAsync(slot, c->d_result, sizeof(double), hipMemcpyDeviceToDevice, s));
   if (!direct) SUP_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
-  std::vector<unsigned> vis;
+  // visited states: summed on the device, 8 bytes back (beside the result in
+  // the mapped slot: h_result[2])
+  unsigned long long* vsum = reinterpret_cast<unsigned long long*>(c->h_result + 2);
   if (visited) {
-    vis.resize(count);
-    SUP_HIP(hipMemcpyAsync(vis.data(), c->d_visited, count * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    SUP_HIP(launch_sum_visited(c->d_visited, count, reinterpret_cast<unsigned long long*>(c->d_result + 2), s));
+    SUP_HIP(hipMemcpyAsync(vsum, c->d_result + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   }
   if (!flagged || !wait_flag(c->h_flag, seq)) SUP_HIP(hipStreamSynchronize(s));
   c->counter_zero = count > 1;  // the reduction's first pass zeroed it (one chunk: a copy, no pass)
@@ -1082,9 +1084,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   r.kernel_ms = ms;
   r.grid = (int)grid;
   if (visited) {
-    uint64_t tot = 0;
-    for (unsigned v : vis) tot += v;
-    r.visited = tot * (uint64_t)(1ull << P.lay.L);
+    r.visited = (uint64_t)*vsum * (uint64_t)(1ull << P.lay.L);
   } else {
     r.visited = count << (P.lay.L + P.lay.m);
   }
@@ -1665,7 +1665,12 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   if (o.chunk_log2 > 0) {
     item = 1ull << o.chunk_log2;
   } else {
-    const uint64_t target_items = (uint64_t)G * 16;
+    // 16 items per taker; one device with nothing to balance against (no CPU
+    // worker) and no checkpoint to resume from walks its range as one item —
+    // the same subtree sums, without 15 more launches and launch tails
+    // (config 5 -p8: 0.39 ms of a 48.9 ms step)
+    const bool alone = G == 1 && !o.cpu_worker && !(o.checkpoint && *o.checkpoint);
+    const uint64_t target_items = alone ? 1 : (uint64_t)G * 16;
     while (item * 2 <= total && total / (item * 2) >= target_items) item <<= 1;
   }
   const uint64_t nitems = (total + item - 1) / item;

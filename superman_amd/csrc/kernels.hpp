@@ -101,6 +101,8 @@ hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scra
                                   hipStream_t s, unsigned int* reset_counter = nullptr, unsigned int* flag = nullptr,
                                   unsigned seq = 0);
 uint64_t pairwise_scratch_size(uint64_t count);
+// *out = sum of `count` unsigned values (zeroed first, on stream s).
+hipError_t launch_sum_visited(const unsigned* in, uint64_t count, unsigned long long* out, hipStream_t s);
 // The same tree over each of `nseg` consecutive segments of `count` doubles
 // (a leaf batch's chunk partials): out[i] is bit-identical to
 // launch_pairwise_reduce over segment i alone.  `scratch` holds nseg times
