@@ -81,30 +81,33 @@ def _dense_mat(n, d):
     return a
 
 
-@pytest.mark.parametrize("d", [0.5, 0.9])
-def test_seg_large_dense_n56(sup, orc, d):
-    """Large dense n: the segmented walk plans and compiles at n = 56 (before
+@pytest.mark.parametrize("n,d", [(56, 0.5), (56, 0.9), (64, 0.5), (64, 0.9)])
+def test_seg_large_dense(sup, orc, n, d):
+    """Large dense n: the segmented walk plans and compiles at n = 56 and at
+    the maximum order 64 (before
     round 4 hiprtc refused d = 0.9 patterns from n = 46 on: a region's pinned
     SGPR pieces exceeded the wave's SGPRs) and its walk loop has no scratch
     (the plan's compiler check).  (1) The planned kernel (searched walk order,
     budget ladder) on one wave-chunk of 2^25 Gray steps through the bench's
-    entry point, bit-exact against the oracle's mirror of that plan; (2) the
+    entry point, bit-exact against the oracle's mirror of that plan (n = 56:
+    a shard index is a C int, and n = 64 has 2^38 wave-chunks); (2) the
     reference-order range [k 2^25, (k+1) 2^25) through sup_partial, bit-exact
     against the mirror and within 1e-9 of the reference chunk helper
     cpu_perman64 restated (gpu_exact_dense.cu:6-69)."""
-    n, wl = 56, 19
+    wl = 19
     a = _dense_mat(n, d)
     info = sup.plan_info(a, "dense", jit=1, walk_log2=wl)
     assert info["kind"] == "seg" and info["m"] == wl
     assert info["est_ops_per_step"] < 0.95 * sup.plan_info(a, "dense", jit=-1)["est_ops_per_step"]
-    nshards = 1 << (n - 1 - info["L"] - wl)
     r = 0x2A5A5A5
-    part, st = sup.perman_shard(a, r, nshards, kernel="dense", jit=1, walk_log2=wl, return_stats=True)
-    assert st["walk_kind"] == 3 and st["gray_steps"] == 1 << (info["L"] + wl)
-    assert (st["seg_cached_bits"], st["seg_pair_bits"]) == (info["cached"], info["pair_bits"])
-    mir, _ = orc.engine_range(a, "seg", r, r + 1, info["L"], wl, info["colmap"], 16, info["cached"],
-                              info["pair_bits"])
-    assert part == mir
+    if n - 1 - info["L"] - wl <= 30:  # one wave-chunk per shard (shard counts are C ints: n = 64 has 2^38 chunks)
+        nshards = 1 << (n - 1 - info["L"] - wl)
+        part, st = sup.perman_shard(a, r, nshards, kernel="dense", jit=1, walk_log2=wl, return_stats=True)
+        assert st["walk_kind"] == 3 and st["gray_steps"] == 1 << (info["L"] + wl)
+        assert (st["seg_cached_bits"], st["seg_pair_bits"]) == (info["cached"], info["pair_bits"])
+        mir, _ = orc.engine_range(a, "seg", r, r + 1, info["L"], wl, info["colmap"], 16, info["cached"],
+                                  info["pair_bits"])
+        assert part == mir
     s = r << (info["L"] + wl)
     e = s + (1 << (info["L"] + wl))
     got, st2 = sup.partial(a, s, e, kernel="seg", return_stats=True)
