@@ -279,34 +279,46 @@ def cpu_baseline(a, n: int, budget_s: float, gpu_sup, kernel: str):
 
 def cold_start(matrix: str) -> dict:
     """End-to-end wall time of the drop-in CLI (`perman -f <matrix> -g -p4`,
-    a fresh process: HIP init, read, plan, compile, walk, print) with an
-    empty code/plan cache and again with the cache the first runs filled:
-      cold_default  jit = 0 (auto; cold it keeps the ahead-of-time walk: the
-                    segmented plan's search + compile would cost more than it
-                    saves on one run),
-      cold_jit1     --jit 1 (search + compile + segmented walk),
-      warm_default  jit = 0 again: the plan choices and kernel are on disk, so
-                    auto mode takes the segmented walk."""
+    a fresh process: HIP init, read, plan, compile, walk, print).  "Cold" is
+    an empty plan cache AND an empty comgr cache (hiprtc's compiles are cached
+    by comgr under ~/.cache/comgr, so a plan after another process compiled
+    the same kernels would not be cold):
+      cold_default  jit = 0 (auto: on a host of the modelled speed the n = 40
+                    matrix specialises — its ~0.5 s saving per run repays the
+                    ~1.6 s plan within 4 runs, and the decision is recorded),
+      cold_jit1     --jit 1, its own empty caches (search + compile + walk),
+      cold_aot      --jit -1, its own empty caches (the ahead-of-time walk:
+                    what a one-shot run would cost without specialising),
+      warm_default  jit = 0 again in cold_default's caches: the recorded
+                    decision, plan choices and kernel are on disk."""
     import shutil
     import subprocess
     import tempfile
     exe = os.path.join(ROOT, "superman_amd", "bin", "perman")
-    cache = tempfile.mkdtemp(prefix="sup_cold_")
-    env = dict(os.environ, SUP_JIT_CACHE_DIR=cache)
-    out = {"command": f"superman_amd/bin/perman -f {os.path.relpath(matrix, ROOT)} -g -p4 [--jit 1]",
-           "cache": "empty SUP_JIT_CACHE_DIR for the cold runs; the same directory for the warm run"}
+    out = {"command": f"superman_amd/bin/perman -f {os.path.relpath(matrix, ROOT)} -g -p4 [--jit 1|-1]",
+           "cache": "empty SUP_JIT_CACHE_DIR and AMD_COMGR_CACHE_DIR per cold run; warm_default reuses "
+                    "cold_default's"}
+    dirs = {k: tempfile.mkdtemp(prefix=f"sup_{k}_") for k in ("default", "jit1", "aot")}
     try:
-        for label, extra in (("cold_default", []), ("cold_jit1", ["--jit", "1"]), ("warm_default", [])):
+        for label, extra, d in (("cold_default", [], "default"), ("cold_jit1", ["--jit", "1"], "jit1"),
+                                ("cold_aot", ["--jit", "-1"], "aot"), ("warm_default", [], "default")):
+            env = dict(os.environ, SUP_JIT_CACHE_DIR=os.path.join(dirs[d], "plans"),
+                       AMD_COMGR_CACHE_DIR=os.path.join(dirs[d], "comgr"))
             t = time.perf_counter()
-            r = subprocess.run([exe, "-f", matrix, "-g", "-p4", *extra], capture_output=True, text=True, env=env,
-                               timeout=300)
+            r = subprocess.run([exe, "-f", matrix, "-g", "-p4", "-v", *extra], capture_output=True, text=True,
+                               env=env, timeout=300)
             wall = time.perf_counter() - t
             perm = [ln.split()[1] for ln in r.stdout.splitlines() if ln.startswith("Permanent:")]
-            out[label] = {"wall_s": wall, "rc": r.returncode, "permanent": float(perm[0]) if perm else None}
+            kinds = {"0": "dense", "1": "prefix-blocked", "2": "skipper", "3": "segmented"}
+            walk = [kinds.get(ln.split("walk_kind")[1].split()[0]) for ln in r.stdout.splitlines()
+                    if ln.startswith("Stats:") and "walk_kind" in ln]
+            out[label] = {"wall_s": wall, "rc": r.returncode, "permanent": float(perm[0]) if perm else None,
+                          "walk": walk[0] if walk else None}
     except (subprocess.SubprocessError, OSError, ValueError) as e:
         out["error"] = repr(e)
     finally:
-        shutil.rmtree(cache, ignore_errors=True)
+        for d in dirs.values():
+            shutil.rmtree(d, ignore_errors=True)
     return out
 
 

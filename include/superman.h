@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SUP_ABI_VERSION 7  /* 7: sup_rccl_devices, sup_stats.seg_cached_bits / seg_pair_bits (round 4) */
+#define SUP_ABI_VERSION 8  /* 8: sup_device_checks (round 5); 7: sup_rccl_devices, sup_stats.seg_cached_bits / seg_pair_bits */
 
 /* ---- error codes ------------------------------------------------------ */
 #define SUP_OK            0
@@ -151,6 +151,13 @@ int         sup_device_count(int* count);
  * permute or repeat physical ids, and SUP_ERCCL is returned when two logical
  * devices share one GPU (RCCL needs distinct devices).  No HIP call. */
 int         sup_rccl_devices(int ndev, int* phys);
+/* Device-placement assertions passed so far in this process.  With
+ * SUP_CHECK_DEVICE=1 in the environment, every allocation, module load and
+ * launch of a device thread first checks that the thread's HIP device is the
+ * physical device behind the logical device whose context it uses, and that
+ * this logical device is the one the thread last selected (a mismatch fails
+ * the call with SUP_EHIP); 0 when the mode is off.  Tests and diagnostics. */
+uint64_t    sup_device_checks(void);
 
 /* ------------------------------------------------------------------------ *
  * Generic entry point.  `mat` is n x n row-major of type `t` (already

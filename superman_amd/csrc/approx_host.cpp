@@ -159,7 +159,7 @@ struct DevWorker {
 
   int init(int device, const Job& J, uint64_t item) {
     dev = device;
-    AHIP(hipSetDevice(phys_device(dev)));
+    AHIP(select_device(dev));
     hipDeviceProp_t prop;
     AHIP(hipGetDeviceProperties(&prop, phys_device(dev)));
     cus = prop.multiProcessorCount;
@@ -175,6 +175,7 @@ struct DevWorker {
     else AHIP(approx_occupancy(J.P->W, J.method, &occ));
     grid = std::max(1, cus * std::max(1, occ));
     grid = (int)std::min<uint64_t>((uint64_t)grid, (item + 3) / 4);
+    SUP_ON_DEVICE(dev, "estimator buffers");
     AHIP(hipStreamCreate(&st));
     AHIP(hipEventCreate(&e0));
     AHIP(hipEventCreate(&e1));
@@ -191,7 +192,7 @@ struct DevWorker {
     return SUP_OK;
   }
   int run(const Job& J, uint64_t b0, uint64_t nb, double out[3]) {
-    AHIP(hipSetDevice(phys_device(dev)));
+    AHIP(select_device(dev));
     ApproxParams p{};
     p.rowpat = d_row;
     p.colpat = d_col;
@@ -207,6 +208,7 @@ struct DevWorker {
     p.times = J.times;
     p.lanes_total = (uint32_t)grid * kBlock;
     AHIP(hipMemsetAsync(d_cnt, 0, sizeof(unsigned), st));
+    SUP_ON_DEVICE(dev, "estimator launch");
     AHIP(hipEventRecord(e0, st));
     if (coop) AHIP(launch_approx_coop(J.P->W, p, grid, st));
     else AHIP(launch_approx(J.P->W, p, grid, st));

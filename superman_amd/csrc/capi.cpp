@@ -91,6 +91,7 @@ int sup_device_count(int* count) {
   if (!count) return SUP_EINVAL;
   return device_count(count);
 }
+uint64_t sup_device_checks(void) { return device_checks_passed(); }
 int sup_rccl_devices(int ndev, int* phys) {
   if (ndev < 1 || ndev > 1024 || !phys) return SUP_EINVAL;
   std::vector<int> devs(ndev), p;

@@ -308,19 +308,19 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
 // fp64 VALU lane-ops per second of one MI355X on the walk kernels (measured:
 // 46.6 ops/step at 7.98e11 steps/s on the n=40 bench), for jit's auto mode.
 static constexpr double kLaneOpsPerSec = 3.7e13;
-// The segmented walk's plan (walk-order searches, 0.1-2.5 s at n = 30-44)
-// and compile + load (0.4-0.7 s with hiprtc; 0 when the disk cache holds it)
-// are paid once per matrix; auto mode specialises when the predicted walk time
-// saved is clearly larger than both.
+// Auto mode's bar where nothing bounds the saving (orders below
+// kJitWarmMinN; jit != 0 never asks): no walk that short repays a plan.
 static constexpr double kJitMinSavingSec = 3.0;
-// Once this host has made a cold segmented plan (make_seg_plan records its
-// cost next to the code objects: ~0.4 s at n = 40 on a GPU box's 16 threads,
-// 2.4-3.4 s on an 8-CPU container), auto mode's cold bar is that cost, within
-// [kJitColdBarMin, kJitMinSavingSec]: break-even, because auto mode records its
-// first decision for a matrix and every later run follows it (AutoRecord) — a
-// walk that repays its plan on the first run repays it on every run after
-// (round 3 asked for twice the cost, when a warm run could still switch).
-static constexpr double kJitColdBarMin = 0.25;
+// Auto mode (jit = 0) decides once per matrix and request, and every later
+// run follows that decision (AutoRecord): the plan (walk-order search +
+// compiles, seg_cold_predict: ~1.6 s at n = 40 on a GPU box, cold) is paid
+// once, the walk time it saves on every run.  So a plan is started when the
+// walk time it can save over kAutoRuns runs would repay it — the bench
+// matrix, a 0.5 s saving per run on one MI355X, specialises on a fresh host;
+// a matrix walked once loses at most the plan's cost.  Once the search and
+// the compiler check have run their cost is spent, and the segmented walk is
+// taken when it saves kJitWarmSavingSec per run.
+static constexpr double kAutoRuns = 4.0;
 // When an earlier process recorded this matrix's segmented-walk choices (disk
 // cache, make_seg_plan), the plan is rebuilt in ~5-50 ms and its code object
 // loads from disk: auto mode specialises whenever the walk saves more than this.
@@ -433,7 +433,11 @@ static int make_seg_plan(const double* A, int n, const Layout& lay, Plan& P) {
   seg_choice_store(dkey, P.lay.m, c);
   // what this cold plan cost (search + the compiler check's compiles): auto
   // mode's cold bar on this host (plan_for)
-  seg_cost_store(std::chrono::duration<double>(std::chrono::steady_clock::now() - t_cold).count());
+  const double cold_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_cold).count();
+  seg_cost_store(n, cold_s);
+  if (std::getenv("SUP_JIT_VERBOSE"))
+    std::fprintf(stderr, "cold segmented plan n=%d: %.3f s (compiles %.3f s wall on this thread)\n", n, cold_s,
+                 jit_compile_ms_thread() * 1e-3);
   return SUP_OK;
 }
 
@@ -472,7 +476,8 @@ uint64_t knob_hash() {
   for (char** e = environ; e && *e; ++e) {
     const char* v = *e;
     if (std::strncmp(v, "SUP_JIT_", 8) != 0 || !std::strncmp(v, "SUP_JIT_CACHE_DIR=", 18) ||
-        !std::strncmp(v, "SUP_JIT_DUMP=", 13) || !std::strncmp(v, "SUP_JIT_VERBOSE=", 16))
+        !std::strncmp(v, "SUP_JIT_DUMP=", 13) || !std::strncmp(v, "SUP_JIT_VERBOSE=", 16) ||
+        !std::strncmp(v, "SUP_JIT_COLD_RATIO=", 19))
       continue;
     for (const char* c = v; *c; ++c) h = (h ^ (unsigned char)*c) * 1099511628211ull;
     h = (h ^ 0xffu) * 1099511628211ull;
@@ -567,15 +572,15 @@ static double skip_visited_fraction(const Plan& P, int dev) {
   return tot ? (double)vis / (double)tot : 1.0;
 }
 
-// Auto mode's bar for specialising: the predicted walk time saved must exceed
-// the planning + compile it costs — seconds cold (or twice what this host's
-// last cold plan measured), ~0 when an earlier process left this matrix's plan
-// choices and kernel in the disk cache.
+// Auto mode's bar for starting a segmented plan: the walk time it can save
+// per run must exceed the predicted cold plan cost (seg_cold_predict: n, this
+// host's plan threads and its recorded speed) over kAutoRuns runs; ~0 (the
+// warm bar) when an earlier process left this matrix's plan choices and
+// kernel in the disk cache.
 static double auto_min_saving(const double* A, int n, const Layout& lay, int jit) {
   if (jit != 0 || n < kJitWarmMinN) return kJitMinSavingSec;  // below: no walk lasts even the lowest bar
   if (seg_choice_exists(seg_disk_key(A, n, lay))) return kJitWarmSavingSec;
-  const double c = seg_cost_load();
-  return c > 0.0 ? std::min(kJitMinSavingSec, std::max(kJitColdBarMin, c)) : kJitMinSavingSec;
+  return std::max(kJitWarmSavingSec, seg_cold_predict(n) / kAutoRuns);
 }
 
 // Auto mode's first decision per matrix and request, on disk (round 4).  The
@@ -599,8 +604,11 @@ struct AutoRecord {
           ((uint64_t)std::max(ndev, 1) << 48);
     recorded = auto_decision_load(key);
   }
-  void store(bool seg) const {
-    if (active && recorded < 0) auto_decision_store(key, seg ? 1 : 0);
+  // records seg unless a decision is on disk; returns the decision to follow
+  // (another process that decided first wins)
+  bool store(bool seg) const {
+    if (active && recorded < 0) return auto_decision_store(key, seg ? 1 : 0) == 1;
+    return seg;
   }
 };
 
@@ -636,18 +644,22 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
         if (jit < 1 && steps * skip_cost / kLaneOpsPerSec < min_saving) return false;
         if (make_seg(s) != SUP_OK) return false;
         if (walk_cost_eff(s) >= skip_cost) return false;
-        if (jit < 1 && steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec < min_saving) return false;
+        // the plan is paid for now: the segmented walk when it saves the warm bar
+        const double bar = std::min(min_saving, kJitWarmSavingSec);
+        if (jit < 1 && steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec < bar) return false;
         if (integral) {
           const double f = skip_visited_fraction(P, dev);
           if (f < 0.0) return false;
           skip_cost *= f;
         }
         const double saved = steps * (skip_cost - walk_cost_eff(s)) / kLaneOpsPerSec;
-        return walk_cost_eff(s) < skip_cost && (jit >= 1 || saved >= min_saving);
+        return walk_cost_eff(s) < skip_cost && (jit >= 1 || saved >= bar);
       };
       const bool seg = decide();
-      if (seg) P = std::move(s);
-      rec.store(seg);
+      if (rec.store(seg)) {
+        if (seg) P = std::move(s);
+        else if (make_seg(s) == SUP_OK) P = std::move(s);  // another process decided first
+      }
       return SUP_OK;
     }
     case SUP_KERNEL_DENSE_PLAIN: return make_plan(A, n, kWalkDense, false, lay, P);
@@ -682,15 +694,17 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
       if (make_seg(s) == SUP_OK) best = std::move(s);
     } else if (rec.recorded < 0 && (jit >= 1 || may_save)) {
       bool seg = false;
-      if (make_seg(s) == SUP_OK && walk_cost_eff(s) < walk_cost(best)) {
+      const bool planned = make_seg(s) == SUP_OK;
+      if (planned && walk_cost_eff(s) < walk_cost(best)) {
+        // the search and the compiler check are paid now: the segmented walk
+        // when it saves the warm bar per run
         const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
         const double saved = steps * (walk_cost(best) - walk_cost_eff(s)) / kLaneOpsPerSec;
-        seg = jit >= 1 || saved >= min_saving;
-        if (seg) best = std::move(s);
+        seg = jit >= 1 || saved >= std::min(min_saving, kJitWarmSavingSec);
       }
-      rec.store(seg);
+      if (rec.store(seg) && planned) best = std::move(s);
     } else if (rec.recorded < 0) {
-      rec.store(false);
+      if (rec.store(false) && make_seg(s) == SUP_OK) best = std::move(s);  // another process decided first
     }
   }
   P = std::move(best);
@@ -814,6 +828,39 @@ int phys_device(int dev) {
   return (m.empty() || dev < 0 || dev >= (int)m.size()) ? dev : m[dev];
 }
 
+static thread_local int t_logical = -1;  // the logical device this thread last selected
+
+hipError_t select_device(int dev) {
+  const hipError_t e = hipSetDevice(phys_device(dev));
+  t_logical = e == hipSuccess ? dev : -1;
+  return e;
+}
+
+static bool check_device_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("SUP_CHECK_DEVICE");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
+static std::atomic<uint64_t> g_device_checks{0};
+
+int check_device(int dev, const char* what) {
+  if (!check_device_on()) return SUP_OK;
+  int cur = -1;
+  const int want = phys_device(dev);
+  if (hipGetDevice(&cur) != hipSuccess || cur != want || t_logical != dev) {
+    set_error(std::string("SUP_CHECK_DEVICE: ") + what + " for logical device " + std::to_string(dev) +
+              " (physical " + std::to_string(want) + ") on a thread whose HIP device is " + std::to_string(cur) +
+              " and whose last selected logical device is " + std::to_string(t_logical));
+    return SUP_EHIP;
+  }
+  g_device_checks.fetch_add(1, std::memory_order_relaxed);
+  return SUP_OK;
+}
+
+uint64_t device_checks_passed() { return g_device_checks.load(); }
+
 int device_count(int* n) {
   int c = 0;
   hipError_t e = hipGetDeviceCount(&c);
@@ -862,7 +909,8 @@ static int get_ctx(int dev, DeviceCtx** out) {
     auto c = std::make_unique<DeviceCtx>();
     c->dev = dev;
     c->phys = pd;
-    SUP_HIP(hipSetDevice(pd));
+    SUP_HIP(select_device(dev));
+    SUP_ON_DEVICE(dev, "context allocations");
     hipDeviceProp_t prop;
     SUP_HIP(hipGetDeviceProperties(&prop, pd));
     c->cus = prop.multiProcessorCount;
@@ -941,7 +989,8 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   int rc = get_ctx(dev, &c);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(c->mu);
-  SUP_HIP(hipSetDevice(c->phys));
+  SUP_HIP(select_device(c->dev));
+  SUP_ON_DEVICE(c->dev, "device buffers");
   const uint64_t count = c1 - c0;
   const double* cols_before = c->d_cols;
   const double* jtab_before = c->d_jtab;
@@ -976,6 +1025,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   c->counter_zero = false;
 
   int occ_seg = 0, occ_lds = 0;
+  if (seg) SUP_ON_DEVICE(c->dev, "segmented-walk module load");
   if (seg && (rc = jit_occupancy(c->phys, P, &occ_seg, &r.compile_ms))) return rc;
   if (P.lds) {  // LDS-staged dense walk: one wave per block, LDS-limited residency
     SUP_HIP(lds_occupancy(P.n, P.lay.m, &occ_lds));
@@ -1043,6 +1093,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     else p.nb_hi |= v << (4 * (k - 16));
   }
 
+  SUP_ON_DEVICE(c->dev, "walk launch");
   SUP_HIP(hipEventRecord(c->ev0, s));
   if (seg) {
     if ((rc = jit_launch(c->phys, P, p, (int)grid, s))) return rc;
@@ -1057,6 +1108,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   // a direct result also carries a sequence number the host can wait on
   const bool flagged = direct && !visited && result_flag_wait();
   const unsigned seq = ++c->flag_seq;
+  SUP_ON_DEVICE(c->dev, "reduction launch");
   SUP_HIP(launch_pairwise_reduce(c->d_chunk, count, c->d_scratch, direct ? c->m_result : c->d_result, s,
                                  c->d_counter, flagged ? c->m_flag : nullptr, seq));
   if (slot) SUP_HIP(hipMemcpyAsync(slot, c->d_result, sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -1123,7 +1175,8 @@ int run_range_batch(int dev, const std::vector<const Plan*>& plans, std::vector<
   int rc = get_ctx(dev, &c);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(c->mu);
-  SUP_HIP(hipSetDevice(c->phys));
+  SUP_HIP(select_device(c->dev));
+  SUP_ON_DEVICE(c->dev, "device buffers");
   const uint64_t C = P0.lay.chunks(), count = C * K;
   const size_t colsz = P0.cols.size(), stride = colsz + P0.x0.size();
   if ((rc = ensure(c->d_batch, c->batch_cap, K * stride))) return rc;
@@ -1179,6 +1232,7 @@ int run_range_batch(int dev, const std::vector<const Plan*>& plans, std::vector<
   p.tail_ticket = 0xffffffffu;
   LeafBatch lb{c->d_desc, (unsigned)P0.lay.h, 0};
   SUP_HIP(hipEventRecord(c->ev0, s));
+  SUP_ON_DEVICE(c->dev, "batch walk launch");
   SUP_HIP(launch_walk_batch(P0.kind, P0.n, p, lb, (int)grid, s));
   SUP_HIP(hipEventRecord(c->ev1, s));
   SUP_HIP(launch_pairwise_reduce_seg(c->d_chunk, C, K, c->d_scratch, c->d_bres, s));
@@ -1209,7 +1263,8 @@ int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1,
   int rc = get_ctx(dev, &c);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(c->mu);
-  SUP_HIP(hipSetDevice(c->phys));
+  SUP_HIP(select_device(c->dev));
+  SUP_ON_DEVICE(c->dev, "device buffers");
   int occ = 0;
   SUP_HIP(exact_occupancy(P.n, group, &occ));
   if (occ < 1) occ = 1;
@@ -1242,6 +1297,7 @@ int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1,
   e.nprimes = np;
   e.wave_out = c->d_wave;
   SUP_HIP(hipEventRecord(c->ev0, s));
+  SUP_ON_DEVICE(c->dev, "exact walk launch");
   SUP_HIP(launch_exact(P.n, group, p, e, (int)grid, s));
   SUP_HIP(hipEventRecord(c->ev1, s));
   std::vector<double> w(waves * kMaxPrimes);
@@ -1271,7 +1327,8 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
   int rc = get_ctx(dev, &c);
   if (rc) return rc;
   std::lock_guard<std::mutex> g(c->mu);
-  SUP_HIP(hipSetDevice(c->phys));
+  SUP_HIP(select_device(c->dev));
+  SUP_ON_DEVICE(c->dev, "device buffers");
   int occ = 0;
   SUP_HIP(dd_occupancy(P.n, &occ));
   if (occ < 1) occ = 1;
@@ -1301,6 +1358,7 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
   p.counter = c->d_counter;
   p.group = 1;
   SUP_HIP(hipEventRecord(c->ev0, s));
+  SUP_ON_DEVICE(c->dev, "double-double walk launch");
   SUP_HIP(launch_dd(P.n, p, (int)grid, s));
   SUP_HIP(hipEventRecord(c->ev1, s));
   SUP_HIP(hipMemcpyAsync(parts, c->d_chunk, 2 * count * sizeof(double), hipMemcpyDeviceToHost, s));

@@ -162,13 +162,23 @@ int build_seg(Plan& P, int fixed_budget = 0);
 // were priced with (generated-code headers, compile options, hiprtc).
 bool seg_choice_load(uint64_t key, int* m, SegChoice* c);
 bool seg_choice_exists(uint64_t key);
-double seg_cost_load();             // seconds of the last cold segmented plan on this host, -1 if none
-void seg_cost_store(double seconds);
+// Cold segmented-plan cost (walk-order search + the compiler check's
+// compiles) predicted for order n on this host: seg_cold_model (a GPU box's
+// 16 threads, scaled to this host's plan threads) times this host's recorded
+// speed (the last cold plan's measured / modelled cost; 1 when none).
+double seg_cold_model(int n);
+double seg_cold_predict(int n);
+// Record a cold plan of order n that took `seconds` (the host's speed ratio).
+void seg_cost_store(int n, double seconds);
+double seg_cost_ratio_load();  // recorded measured / modelled ratio, -1 if none
 void seg_choice_store(uint64_t key, int m, const SegChoice& c);
 // Auto mode's (jit = 0) first decision for a matrix and request, recorded next
 // to the plan choices: 1 segmented walk, 0 ahead-of-time walk, -1 none yet.
 int auto_decision_load(uint64_t key);
-void auto_decision_store(uint64_t key, int seg);
+// Records `seg` only if no decision is on disk yet (created exclusively: two
+// processes deciding at once cannot both win) and returns the decision on
+// disk afterwards, which the caller follows; `seg` when there is no cache.
+int auto_decision_store(uint64_t key, int seg);
 uint64_t jit_toolchain_hash();
 // Default specialised pair bits, min(m - 1, 5) (the walk loop is unrolled by
 // 2^b pair steps; walk bits > b share one straight-line step).  Plans choose
@@ -264,6 +274,23 @@ constexpr int kCtxLanes = 8;
 void set_ctx_lane(int lane);
 int ctx_lane();
 int phys_device(int dev);  // logical -> physical (SUP_DEVICE_MAP; identity when unset)
+// Select logical device `dev` (physical phys_device(dev)) on this thread:
+// hipSetDevice plus a thread-local note of the logical id, which
+// check_device compares.
+hipError_t select_device(int dev);
+// SUP_CHECK_DEVICE=1 (tests): before every allocation,
+// module load and launch of a device thread, the thread's HIP device must be
+// the physical device behind the logical device whose context it uses, and
+// the logical device it last selected must be that one (on a one-GPU box with
+// SUP_DEVICE_MAP=0,0,... the physical ids agree, the logical ones do not).  A
+// mismatch returns SUP_EHIP.  Off: one branch.
+int check_device(int dev, const char* what);
+uint64_t device_checks_passed();
+#define SUP_ON_DEVICE(dev, what)                 \
+  do {                                           \
+    const int rc_ = check_device((dev), (what)); \
+    if (rc_) return rc_;                         \
+  } while (0)
 // physical devices of the RCCL combine over logical `devs`; SUP_ERCCL if two share a GPU
 int rccl_physical_devices(const std::vector<int>& devs, std::vector<int>& phys);
 

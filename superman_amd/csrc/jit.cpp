@@ -1892,9 +1892,9 @@ int build_seg(Plan& P, int fixed_budget) {
   // estimate is rough: on the n = 40 bench matrix budgets up to 192 compile
   // without a spill, 194-216 spill 5-13 VGPRs, 218+ 17-27; denser or larger
   // matrices spill inside the walk loop at the default.  So a ladder of
-  // budgets is planned (host threads), the distinct kernels are compiled in
-  // ascending op count, kMaxParallelCompiles at a time (hiprtc on host
-  // threads), and each code object is disassembled (codescan.cpp): the one
+  // budgets is planned (host threads), the distinct kernels are compiled as
+  // a bisection for the largest budget whose loop stays clean (below), and
+  // each code object is disassembled (codescan.cpp): the one
   // with the fewest ops whose walk loop touches no scratch wins, a kernel with
   // no scratch at all preferred unless the other saves more than
   // kScratchTolerance of the ops (spills in the chunk start cost HBM writes
@@ -1937,28 +1937,64 @@ int build_seg(Plan& P, int fixed_budget) {
     std::vector<CodeScan> scans(cand.size());
     std::vector<int> src(cand.size(), SUP_EHIP);
     std::vector<char> done(cand.size(), 0);
-    auto run_batch = [&](const std::vector<size_t>& which) {
+    // One compile at a time: hiprtc compiles in one process do not overlap
+    // (measured on this image: 8 threads compiling 8 different kernels take
+    // 0.8 of the time of 8 sequential compiles, the comgr action behind
+    // hiprtcCompileProgram is serialised), so the ladder is bisected instead
+    // of walked in concurrent batches: 5 compiles instead of 8 on the n = 40
+    // bench matrix, the same choice wherever "clean" and "no scratch at all"
+    // are monotone in the budget (they are on every matrix measured).
+    auto compile_one = [&](size_t i) {
+      if (done[i]) return;
       const auto t0 = std::chrono::steady_clock::now();
-      const double own = t_compile_ms;  // the batch's wall time counts for this call
-      parallel_tasks(which.size(), [&](size_t k) { src[which[k]] = jit_code_scan(cand[which[k]], &scans[which[k]]); },
-                     g_jit_failed.load() ? 1 : (int)kMaxParallelCompiles);
+      const double own = t_compile_ms;  // wall time (the compile's own count stays out)
+      src[i] = jit_code_scan(cand[i], &scans[i]);
       t_compile_ms = own + std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-      for (size_t i : which) done[i] = 1;
+      done[i] = 1;
     };
     auto clean = [&](size_t i) { return done[i] && src[i] == SUP_OK && scans[i].loop_scratch == 0; };
-    // Probe: the default budget's kernel alone.  hiprtc's register allocator
+    // Probe: the default budget's kernel, first.  hiprtc's register allocator
     // gives up on some dense n >= 46 patterns ("maximum depth for
-    // recoloring"), and such a failure next to concurrent compiles has crashed
-    // the process (LLVM's error path is not thread-safe): a failing pattern
-    // stops here, before any concurrent compile.
-    size_t probe = idx[0];
-    for (size_t i : idx)
-      if (budgets[i] <= kRegsMax) probe = i;
-    run_batch({probe});
+    // recoloring"): a pattern that fails here has no segmented plan.
+    size_t pp = 0;
+    for (size_t k = 0; k < idx.size(); ++k)
+      if (budgets[idx[k]] <= kRegsMax) pp = k;
+    const size_t probe = idx[pp];
+    compile_one(probe);
     if (src[probe] != SUP_OK) return SUP_EHIP;
-    // Then batches of up to kMaxParallelCompiles budgets, concurrently: upwards
-    // from the probe while its walk loop is clean (fewer ops, until a kernel
-    // scratches in the loop), downwards while it is not (until one is clean).
+    // The largest clean budget: above the probe when the probe is clean, else
+    // below it (bisection over idx positions; lo clean, hi not).
+    size_t c_pos;
+    if (clean(probe)) {
+      size_t lo = pp, hi = idx.size();
+      while (hi - lo > 1) {
+        const size_t mid = lo + (hi - lo) / 2;
+        compile_one(idx[mid]);
+        (clean(idx[mid]) ? lo : hi) = mid;
+      }
+      c_pos = lo;
+    } else {
+      long lo = -1, hi = (long)pp;
+      while (hi - lo > 1) {
+        const long mid = lo + (hi - lo) / 2;
+        compile_one(idx[mid]);
+        if (clean(idx[mid])) lo = mid;
+        else hi = mid;
+      }
+      if (lo < 0) {
+        set_error("segmented walk: every budget's kernel touches scratch inside its walk loop (or fails to compile)");
+        return SUP_EHIP;
+      }
+      c_pos = (size_t)lo;
+    }
+    // A kernel with no scratch at all is preferred within kScratchTolerance of
+    // the ops: the largest such budget below the chosen one.
+    if (scans[idx[c_pos]].scratch_bytes != 0)
+      for (size_t k = c_pos; k-- > 0;) {
+        if (cand[idx[k]].seg_ops > cand[idx[c_pos]].seg_ops * (1.0 + kScratchTolerance)) break;
+        compile_one(idx[k]);
+        if (clean(idx[k]) && scans[idx[k]].scratch_bytes == 0) break;
+      }
     auto pick = [&]() {
       int c = -1, bare = -1;
       for (size_t i : idx) {
@@ -1968,22 +2004,6 @@ int build_seg(Plan& P, int fixed_budget) {
       }
       return (bare >= 0 && c >= 0 && cand[bare].seg_ops <= cand[c].seg_ops * (1.0 + kScratchTolerance)) ? bare : c;
     };
-    const bool up = clean(probe);
-    for (;;) {
-      std::vector<size_t> batch;
-      if (up) {
-        for (size_t i : idx)
-          if (!done[i] && budgets[i] > budgets[probe] && batch.size() < kMaxParallelCompiles) batch.push_back(i);
-      } else {
-        for (auto it = idx.rbegin(); it != idx.rend(); ++it)
-          if (!done[*it] && budgets[*it] < budgets[probe] && batch.size() < kMaxParallelCompiles) batch.push_back(*it);
-      }
-      if (batch.empty()) break;
-      run_batch(batch);
-      bool stop = false;
-      for (size_t i : batch) stop = stop || (up ? !clean(i) : clean(i));
-      if (stop) break;
-    }
     const int best = pick();
     if (std::getenv("SUP_JIT_VERBOSE"))
       for (size_t i : idx)
@@ -2309,20 +2329,40 @@ int auto_decision_load(uint64_t key) {
   return v;
 }
 
-void auto_decision_store(uint64_t key, int seg) {
+int auto_decision_store(uint64_t key, int seg) {
   const std::string dir = cache_dir();
-  if (dir.empty()) return;
+  if (dir.empty()) return seg;
+  const std::string name = "auto_" + key_hex(key) + ".txt";
   const std::string str = std::string("supauto 1 ") + (seg ? "1" : "0") + "\n";
-  write_file_atomic(dir, "auto_" + key_hex(key) + ".txt", std::vector<char>(str.begin(), str.end()));
+  // write a private temporary, then link() it to the final name: link fails
+  // when the name exists, so the first process to decide wins and every other
+  // follows what it recorded (write_file_atomic's rename would overwrite)
+  const std::string mine = "." + name + ".new" + std::to_string(::getpid()) + "." +
+                           std::to_string(std::hash<std::thread::id>()(std::this_thread::get_id()));
+  write_file_atomic(dir, mine, std::vector<char>(str.begin(), str.end()));
+  (void)::link((dir + "/" + mine).c_str(), (dir + "/" + name).c_str());
+  std::remove((dir + "/" + mine).c_str());
+  const int on_disk = auto_decision_load(key);
+  return on_disk >= 0 ? on_disk : seg;
 }
 
 // What a cold segmented plan (walk-order search + the compiler check's
-// compiles) cost on this host with this compiler, as make_seg_plan last
-// measured it: "supcost 1 <seconds>", one file per toolchain next to the code
-// objects.  Auto mode's cold bar follows it (plan_for).  -1 when none.
+// compiles) costs.  Measured on a GPU box with an empty plan cache and an
+// empty comgr cache (tools/probe_cold.sh, profiles/r5/probe_cold.log), 16
+// threads: the search 0.13 s at n = 32, 0.16 s at 36, 0.39 s at 40, 0.64 s at
+// 44 (8 threads: 0.67 s at 40, 1.17 s at 44); the compiler check's kernels
+// ~0.25 s each, one after another (hiprtc compiles in one process do not
+// overlap), 5 of them for the bisected budget ladder at n = 40 (1.25 s).
+double seg_cold_model(int n) {
+  const double search = 0.39 * std::exp2((n - 40) / 6.5) * std::pow(16.0 / plan_threads(), 0.8);
+  return search + 1.25;
+}
+
+// This host's recorded speed: "supcost 2 <measured / modelled>", one file per
+// toolchain next to the code objects, written by every cold plan.
 static std::string seg_cost_name() { return "cost_" + key_hex(jit_toolchain_hash()) + ".txt"; }
 
-double seg_cost_load() {
+double seg_cost_ratio_load() {
   const std::string dir = cache_dir();
   if (dir.empty()) return -1.0;
   std::vector<char> buf;
@@ -2331,16 +2371,24 @@ double seg_cost_load() {
   std::istringstream in(buf.data());
   std::string tag;
   int ver = 0;
-  double sec = -1.0;
-  if (!(in >> tag >> ver >> sec) || tag != "supcost" || ver != 1 || !(sec > 0.0) || sec > 3600.0) return -1.0;
-  return sec;
+  double r = -1.0;
+  if (!(in >> tag >> ver >> r) || tag != "supcost" || ver != 2 || !(r > 0.0) || r > 1000.0) return -1.0;
+  return r;
 }
 
-void seg_cost_store(double seconds) {
+double seg_cold_predict(int n) {
+  // SUP_JIT_COLD_RATIO (tests, experiments): this host's speed ratio, in place
+  // of the recorded one (not a plan knob: knob_hash leaves it out)
+  const char* e = std::getenv("SUP_JIT_COLD_RATIO");
+  const double r = e ? std::atof(e) : seg_cost_ratio_load();
+  return seg_cold_model(n) * (r > 0.0 ? std::min(8.0, std::max(0.25, r)) : 1.0);
+}
+
+void seg_cost_store(int n, double seconds) {
   const std::string dir = cache_dir();
   if (dir.empty() || !(seconds > 0.0)) return;
   char b[64];
-  std::snprintf(b, sizeof b, "supcost 1 %.4f\n", seconds);
+  std::snprintf(b, sizeof b, "supcost 2 %.4f\n", seconds / seg_cold_model(n));
   const std::string str = b;
   write_file_atomic(dir, seg_cost_name(), std::vector<char>(str.begin(), str.end()));
 }

@@ -388,10 +388,10 @@ int main(int argc, char** argv) {
     report(name, perm, sec);
     if (c.verbose)
       std::printf("Stats: kernel_ms %.3f gray_steps %llu visited %llu devices %d lanes %d walk %d grid %d leaves %d "
-                  "walk_kind %d ops_per_step %.1f jit_ms %.1f\n",
+                  "walk_kind %d ops_per_step %.1f jit_ms %.1f cpu_items %d device_checks %llu\n",
                   st.kernel_ms, (unsigned long long)st.gray_steps, (unsigned long long)st.visited_steps,
                   st.devices_used, st.lane_bits, st.walk_bits, st.grid, st.leaves, st.walk_kind, st.est_ops_per_step,
-                  st.jit_ms);
+                  st.jit_ms, st.chunks_done_cpu, (unsigned long long)sup_device_checks());
   }
   sup_free(mat);
   return 0;
