@@ -718,6 +718,10 @@ static double pair64(double* v) {
   return v[0];
 }
 
+/* walk_skip.hip / superman_amd/csrc/kernels.hpp kSkipSegBits */
+#define SKIP_SEG_BITS 4
+#define SKIP_SEG_MASK ((1u << SKIP_SEG_BITS) - 1u)
+
 static unsigned next_toggle(unsigned t, unsigned k) {
   unsigned c = ((t >> (k + 1)) << (k + 1)) + (1u << k);
   if (c <= t) c += 2u << k;
@@ -788,58 +792,78 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
     if (visited) *visited += (unsigned long long)T << L;
     return pair64(lv);
   }
-  /* skipper: 64 lanes in lock-step with wave-uniform jumps */
+  /* skipper: 64 lanes in lock-step with wave-uniform jumps at the starts of
+   * aligned segments of 2^SKIP_SEG_BITS Gray steps (walk_skip.hip, round 5):
+   * at a segment start t with every lane's term zero, the lane-uniform rows
+   * that are exactly zero and that no walk bit below SKIP_SEG_BITS touches
+   * stay zero until one of their walk columns toggles; the wave moves to the
+   * last such toggle.  Every other segment is walked state by state. */
   static __thread double X[64][ORC_MAXN], UU[64][ORC_MAXN / 8 + 2];
   double acc[64];
   (void)NB;
   for (unsigned l = 0; l < 64; ++l) {
     e_start(P, ga, l, X[l]);
     e_suffix(X[l], n, UU[l]);
-    acc[l] = 0.0;
+    acc[l] = UU[l][0]; /* state 0 */
   }
-  unsigned t = 0;
-  unsigned long long vis = 0;
-  for (;;) {
+  unsigned long long vis = 1;
+  unsigned u = 1;
+  int check = 1;
+  for (; T > 1;) { /* T = 1: state 0 is the chunk */
     int all_zero = 1;
-    vis++;
-    for (unsigned l = 0; l < 64; ++l) {
-      double term = UU[l][0];
-      acc[l] = (t & 1u) ? acc[l] - term : acc[l] + term;
-      if (term != 0.0) all_zero = 0;
-    }
-    unsigned next = t + 1;
-    if (all_zero) {
+    for (unsigned l = 0; l < 64 && all_zero; ++l)
+      if (UU[l][0] != 0.0) all_zero = 0;
+    if (check && all_zero) {
+      unsigned t = u - 1, nx = t;
       unsigned long long zm = 0;
       for (int r = 0; r < n; ++r)
         if (X[0][r] == 0.0) zm |= 1ULL << r;
       zm &= P->umask;
-      if (zm) {
-        unsigned target = t + 1;
-        while (zm) {
-          int r = __builtin_ctzll(zm);
-          zm &= zm - 1;
-          unsigned long long mm = P->rowmask[r];
-          unsigned tr = T;
-          while (mm) {
-            unsigned k = __builtin_ctzll(mm);
-            mm &= mm - 1;
-            unsigned c = next_toggle(t, k);
-            if (c < tr) tr = c;
-          }
-          if (tr > target) target = tr;
+      while (zm) {
+        int r = __builtin_ctzll(zm);
+        zm &= zm - 1;
+        unsigned long long mm = P->rowmask[r];
+        if (mm & SKIP_SEG_MASK) continue;
+        unsigned tr = T;
+        while (mm) {
+          unsigned k = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          unsigned c = next_toggle(t, k);
+          if (c < tr) tr = c;
         }
-        next = target;
+        if (tr > nx) nx = tr;
+      }
+      if (nx >= T) break;
+      if (nx > t) {
+        unsigned gn = nx ^ (nx >> 1), diff = (t ^ (t >> 1)) ^ gn;
+        do {
+          unsigned k = __builtin_ctz(diff);
+          diff &= diff - 1;
+          unsigned neg = ((gn >> k) & 1u) ^ 1u;
+          for (unsigned l = 0; l < 64; ++l) e_sparse_step(X[l], UU[l], n, P->col[2 * (L + k) + neg], P->nblk[L + k]);
+        } while (diff);
+        for (unsigned l = 0; l < 64; ++l) acc[l] += UU[l][0]; /* nx: a segment start, even */
+        vis++;
+        u = nx + 1;
+        continue;
       }
     }
-    if (next >= T) break;
-    unsigned gn = next ^ (next >> 1), diff = (t ^ (t >> 1)) ^ gn;
-    do {
-      unsigned k = __builtin_ctz(diff);
-      diff &= diff - 1;
-      unsigned neg = ((gn >> k) & 1u) ^ 1u;
-      for (unsigned l = 0; l < 64; ++l) e_sparse_step(X[l], UU[l], n, P->col[2 * (L + k) + neg], P->nblk[L + k]);
-    } while (diff);
-    t = next;
+    for (unsigned l = 0; l < 64; ++l) {
+      e_sparse_step(X[l], UU[l], n, P->col[2 * L + ((u >> 1) & 1u)], P->nblk[L]);
+      acc[l] -= UU[l][0];
+    }
+    vis++;
+    if (u + 1 >= T) break;
+    {
+      unsigned v = u + 1, k = __builtin_ctz(v), neg = (v >> (k + 1)) & 1u;
+      for (unsigned l = 0; l < 64; ++l) {
+        e_sparse_step(X[l], UU[l], n, P->col[2 * (L + k) + neg], P->nblk[L + k]);
+        acc[l] += UU[l][0];
+      }
+      vis++;
+      check = (v & SKIP_SEG_MASK) == 0;
+    }
+    u += 2;
   }
   if (visited) *visited += vis << L;
   for (unsigned l = 0; l < 64; ++l) {

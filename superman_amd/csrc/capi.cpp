@@ -569,7 +569,7 @@ int leaf_workers();
 int leaf_batch_max();
 bool leaf_batching(const LeafCtx& c) {
   if (leaf_batch_max() <= 1) return false;
-  return !c.on_cpu && c.sched == SUP_SCHED_SINGLE && c.o.use_rccl == 0 &&
+  return !c.on_cpu && c.sched == SUP_SCHED_SINGLE && c.o.use_rccl == 0 && !(c.o.checkpoint && *c.o.checkpoint) &&
          (c.kernel == SUP_KERNEL_DENSE || c.kernel == SUP_KERNEL_SPARYSER || c.kernel == SUP_KERNEL_DENSE_PLAIN);
 }
 // Default: batches of 16 when the leaves run one worker at a time, none with
@@ -605,7 +605,9 @@ int leaf_compute_batch(const LeafCtx& c, const std::vector<const double*>& mats,
     if (c.preprocessing == 1) rc = sup_sort_order(ms[i].data(), SUP_FLOAT64, n, cp.data());
     else if (c.preprocessing == 2) rc = sup_skip_order(ms[i].data(), SUP_FLOAT64, n, rp.data(), cp.data());
     if (rc) return rc;
-    if ((rc = plan_for_shared(ms[i].data(), n, c.kernel, lay, plans[i], c.o.jit, 1, c.o.device_id))) return rc;
+    // batch leaves stay out of the process plan cache (32 entries): two batches of 16 would evict the
+    // caller's plans; a repeated leaf is served by the reduction's leaf memo
+    if ((rc = plan_for_shared(ms[i].data(), n, c.kernel, lay, plans[i], c.o.jit, 1, c.o.device_id, false))) return rc;
   }
   const double sign = (double)(4 * (n & 1) - 2);  // gpu_exact_dense.cu:698
   std::vector<const Plan*> group;

@@ -489,7 +489,7 @@ uint64_t knob_hash() {
 static uint64_t knob_hash_env() { return knob_hash(); }
 
 int plan_for_shared(const double* A, int n, sup_kernel kernel, const Layout& lay, std::shared_ptr<const Plan>& out,
-                    int jit, int ndev, int dev) {
+                    int jit, int ndev, int dev, bool keep) {
   const size_t nn = (size_t)n * n;
   // in-process cache key only (the entry also keeps the matrix and compares
   // it): four independent FNV-style lanes, so the multiply chain is a quarter
@@ -522,6 +522,10 @@ int plan_for_shared(const double* A, int n, sup_kernel kernel, const Layout& lay
   auto P = std::make_shared<Plan>();
   const int rc = plan_for_uncached(A, n, kernel, lay, *P, jit, ndev, dev, auto_min_saving(A, n, lay, jit));
   if (rc) return rc;
+  if (!keep) {  // a plan walked once (a batch's leaf): the cache keeps the caller's plans
+    out = P;
+    return SUP_OK;
+  }
   std::lock_guard<std::mutex> g(g_plan_mu);
   {
     auto it = g_plans.find(key);  // another thread planned the same request meanwhile: its plan stands
@@ -545,11 +549,13 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
   return rc;
 }
 
-// SkipPer evaluates only the states without an exactly-zero row; its jumps
-// and divergence cost it efficiency per evaluated state: measured on config 5
-// int, 25.5 modelled ops per visited state at 1.38e13 ops/s against the plain
-// walks' 3.7e13 (profiles/r1/probe_seg.log).
-static constexpr double kSkipEfficiency = 0.37;
+// SkipPer evaluates only the states its zero checks cannot rule out; its
+// checks and jumps cost it efficiency per evaluated state.  Round 5's kernel
+// (segment-start checks, walk_sparse's paired steps elsewhere) on config 5
+// int: 25.5 modelled ops per visited state, 25.7 % visited, 2.245 s — 2.57e13
+// ops/s against the plain walks' 3.7e13 (profiles/r5/probe_skip.log; round 4's
+// per-state kernel: 0.37, profiles/r1/probe_seg.log).
+static constexpr double kSkipEfficiency = 0.69;
 
 // Fraction of the states the SkipPer plan P evaluates, measured on a fixed
 // sample of its wave-chunks (8 evenly spaced ranges, ~1/64 of the walk) on
@@ -954,12 +960,15 @@ static bool result_flag_wait() {
 // Spin on the flag for up to 2 ms (a short walk's wait); false: not seen yet
 // (a long walk, or a fault that stopped the stream) — the caller then blocks
 // in hipStreamSynchronize, which also reports the stream's error.
+static constexpr double kFlagSpinMs = 2.0;
 static bool wait_flag(const unsigned* flag, unsigned seq) {
   const auto t0 = std::chrono::steady_clock::now();
   for (unsigned i = 1;; ++i) {
     if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) return true;
     __builtin_ia32_pause();
-    if ((i & 255u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(2000)) return false;
+    if ((i & 255u) == 0 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::microseconds((long)(kFlagSpinMs * 1000.0)))
+      return false;
   }
 }
 
@@ -1120,7 +1129,12 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     SUP_HIP(launch_sum_visited(c->d_visited, count, reinterpret_cast<unsigned long long*>(c->d_result + 2), s));
     SUP_HIP(hipMemcpyAsync(vsum, c->d_result + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   }
-  if (!flagged || !wait_flag(c->h_flag, seq)) SUP_HIP(hipStreamSynchronize(s));
+  // spin on the flag only where the walk is predicted to end within the spin
+  // window (cost model on this device's CUs; a longer walk blocks in the
+  // stream sync at once instead of holding a host core for 2 ms)
+  const double predicted_ms = std::ldexp((double)count, P.lay.L + P.lay.m) * walk_cost_eff(P) / kLaneOpsPerSec *
+                              1e3 * (256.0 / std::max(1, c->cus));
+  if (!flagged || predicted_ms > kFlagSpinMs || !wait_flag(c->h_flag, seq)) SUP_HIP(hipStreamSynchronize(s));
   c->counter_zero = count > 1;  // the reduction's first pass zeroed it (one chunk: a copy, no pass)
   float ms = 0.f;
   hipError_t ee = hipEventElapsedTime(&ms, c->ev0, c->ev1);
@@ -1153,7 +1167,8 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
 bool batchable(const Plan& a, const Plan& b) {
   return (a.kind == kWalkDense || a.kind == kWalkSparse) && a.kind == b.kind && !a.lds && !b.lds && a.n == b.n &&
          a.lay.L == b.lay.L && a.lay.m == b.lay.m && a.lay.h == b.lay.h && a.cols.size() == b.cols.size() &&
-         a.x0.size() == b.x0.size() && a.lay.chunks() >= 1 && a.lay.chunks() <= (1ull << 26);  // 32-bit chunk ids
+         a.x0.size() == b.x0.size() && a.lay.chunks() >= 1 &&
+         a.lay.chunks() <= (1ull << kMaxBatchLeafChunkBits);  // 32-bit chunk ids (engine.hpp)
 }
 
 int run_range_batch(int dev, const std::vector<const Plan*>& plans, std::vector<double>& partial, double* kernel_ms) {

@@ -232,7 +232,7 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
 // The same, sharing the cached plan instead of copying it (the per-call path
 // of sup_perman / sup_perman_shard).
 int plan_for_shared(const double* A, int n, sup_kernel kernel, const Layout& lay, std::shared_ptr<const Plan>& P,
-                    int jit = -1, int ndev = 1, int dev = 0);
+                    int jit = -1, int ndev = 1, int dev = 0, bool keep = true);
 
 struct RangeResult {
   double partial = 0.0;     // pairwise sum over the range's wave-chunks
@@ -260,6 +260,11 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
 // device `dev`; partial[i] is bit-identical to run_range over plan i's whole
 // range.  batchable(): whether two plans can share a launch.
 constexpr int kMaxBatchLeaves = 32;
+// The batch kernels index chunks with 32 bits (walk_sparse_batch): batchable()
+// caps a leaf at 2^kMaxBatchLeafChunkBits chunks, so a batch stays below 2^32.
+constexpr int kMaxBatchLeafChunkBits = 26;
+static_assert((uint64_t)kMaxBatchLeaves << kMaxBatchLeafChunkBits <= (1ull << 32),
+              "leaf batches must fit 32-bit chunk indices");
 bool batchable(const Plan& a, const Plan& b);
 int run_range_batch(int dev, const std::vector<const Plan*>& plans, std::vector<double>& partial, double* kernel_ms);
 

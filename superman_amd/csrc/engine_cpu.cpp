@@ -308,56 +308,69 @@ double chunk_partial(const Plan& P, uint64_t ga) {
     }
     return pairwise64(lane_val);
   }
-  // SkipPer: all 64 lanes in lock-step, wave-uniform jumps (walk_skip.hip).
+  // SkipPer: all 64 lanes in lock-step, wave-uniform jumps at segment
+  // starts (walk_skip.hip: segments of 2^kSkipSegBits Gray steps).
   static thread_local Lane S[64];
   double acc[64];
   for (unsigned l = 0; l < 64; ++l) {
     chunk_start(P, ga, l, S[l]);
     suffix_all(S[l], n);
-    acc[l] = 0.0;
+    acc[l] = S[l].U[0];  // state 0
   }
-  uint32_t t = 0;
-  for (;;) {
-    bool all_zero = true;
-    for (unsigned l = 0; l < 64; ++l) {
-      const double term = S[l].U[0];
-      acc[l] = (t & 1u) ? acc[l] - term : acc[l] + term;
-      if (term != 0.0) all_zero = false;
-    }
-    uint32_t next = t + 1;
-    if (all_zero) {
+  auto all_zero = [&]() {
+    for (unsigned l = 0; l < 64; ++l)
+      if (S[l].U[0] != 0.0) return false;
+    return true;
+  };
+  auto step = [&](uint32_t k, int neg) {
+    for (unsigned l = 0; l < 64; ++l) sparse_step(S[l], n, col_of(P, L + k, neg), P.nblk[L + k]);
+  };
+  uint32_t u = 1;
+  bool check = true;
+  for (; T > 1;) {  // T = 1: state 0 is the chunk
+    if (check && all_zero()) {
+      const uint32_t t = u - 1;
       uint64_t zm = 0;
       for (int r = 0; r < n; ++r)
         if (S[0].x[r] == 0.0) zm |= 1ull << r;
       zm &= P.umask;
-      if (zm) {
-        uint32_t target = t + 1;
-        while (zm) {
-          const int r = __builtin_ctzll(zm);
-          zm &= zm - 1;
-          uint64_t mm = P.rowmask[r];
-          uint32_t tr = T;
-          while (mm) {
-            const uint32_t k = __builtin_ctzll(mm);
-            mm &= mm - 1;
-            const uint32_t c = next_toggle(t, k);
-            tr = c < tr ? c : tr;
-          }
-          target = tr > target ? tr : target;
+      uint32_t nx = t;
+      while (zm) {
+        const int r = __builtin_ctzll(zm);
+        zm &= zm - 1;
+        uint64_t mm = P.rowmask[r];
+        if (mm & kSkipSegMask) continue;
+        uint32_t tr = T;
+        while (mm) {
+          const uint32_t k = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          const uint32_t c = next_toggle(t, k);
+          tr = c < tr ? c : tr;
         }
-        next = target;
+        nx = tr > nx ? tr : nx;
+      }
+      if (nx >= T) break;
+      if (nx > t) {
+        const uint32_t gn = nx ^ (nx >> 1);
+        uint32_t diff = (t ^ (t >> 1)) ^ gn;
+        do {
+          const uint32_t k = __builtin_ctz(diff);
+          diff &= diff - 1;
+          step(k, ((gn >> k) & 1u) ^ 1u);
+        } while (diff);
+        for (unsigned l = 0; l < 64; ++l) acc[l] += S[l].U[0];  // nx: a segment start, even
+        u = nx + 1;
+        continue;
       }
     }
-    if (next >= T) break;
-    const uint32_t gn = next ^ (next >> 1);
-    uint32_t diff = (t ^ (t >> 1)) ^ gn;
-    do {
-      const uint32_t k = __builtin_ctz(diff);
-      diff &= diff - 1;
-      const int neg = ((gn >> k) & 1u) ^ 1u;
-      for (unsigned l = 0; l < 64; ++l) sparse_step(S[l], n, col_of(P, L + k, neg), P.nblk[L + k]);
-    } while (diff);
-    t = next;
+    step(0, (u >> 1) & 1u);
+    for (unsigned l = 0; l < 64; ++l) acc[l] -= S[l].U[0];
+    if (u + 1 >= T) break;
+    const uint32_t v = u + 1, k = __builtin_ctz(v);
+    step(k, (v >> (k + 1)) & 1u);
+    for (unsigned l = 0; l < 64; ++l) acc[l] += S[l].U[0];
+    u += 2;
+    check = (v & kSkipSegMask) == 0;
   }
   for (unsigned l = 0; l < 64; ++l) {
     const unsigned par = (unsigned)__builtin_popcount(l) & 1u;

@@ -7,6 +7,15 @@
 
 namespace sup {
 
+// SkipPer (walk_skip.hip, its host twin engine_cpu.cpp; oracle/oracle.c
+// restates it): zero checks and jumps at the starts of aligned segments of
+// 2^kSkipSegBits Gray steps.
+#ifndef SUP_SKIP_SEG_BITS
+#define SUP_SKIP_SEG_BITS 4  // (other values: experiments; oracle/oracle.c must agree)
+#endif
+constexpr int kSkipSegBits = SUP_SKIP_SEG_BITS;
+constexpr uint32_t kSkipSegMask = (1u << kSkipSegBits) - 1u;
+
 // Per-N-range launchers (one translation unit per range, see Makefile).
 #define SUP_DECL_RANGE(KIND, LO)                                                      \
   hipError_t launch_##KIND##_##LO(int n, const WalkParams& p, int grid, hipStream_t s); \

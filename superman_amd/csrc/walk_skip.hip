@@ -29,7 +29,7 @@ __device__ __forceinline__ uint32_t next_toggle(uint32_t t, uint32_t k) {
   return c;
 }
 
-// x[rows of blocks < nb] += col (jump path: adds only, products refreshed once)
+// x[rows of blocks < nb] += col (jump path: adds only, products re-formed once)
 template <int N, int B>
 __device__ __forceinline__ void add_nest(double (&x)[N], cdbl* col, int nb) {
   if constexpr (B < Blocks<N>::NB) {
@@ -41,16 +41,69 @@ __device__ __forceinline__ void add_nest(double (&x)[N], cdbl* col, int nb) {
   }
 }
 
+// A kernel argument read where it is used: a scalar load from the kernarg
+// segment through an opaque base, so the value is not held in SGPRs across the
+// walk (the register allocator spilled such values to VGPR lanes and reloaded
+// them with v_readlane on every visited state).
+template <class T>
+__device__ __forceinline__ T karg_at(uint32_t offset) {
+  uint64_t a = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(a));
+  return *(const __attribute__((address_space(4))) T*)(a + offset);
+}
+#define SUP_KARG(field) karg_at<decltype(WalkParams::field)>((uint32_t)__builtin_offsetof(WalkParams, field))
+
+// Zero test of every row, one bit per row: a lane-uniform row holds the same
+// value on every lane, so its ballot is 0 or all ones and bit r of it stands
+// for lane 0 (rows outside umask are dropped by the caller).  Two scalar ops
+// per row (and, or) beside the compare; round 4's form took three.
+template <int N>
+__device__ __forceinline__ uint64_t zero_rows(const double (&x)[N]) {
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    const uint64_t b = __builtin_amdgcn_ballot_w64(x[r] == 0.0);
+    if (r < 32) lo |= (uint32_t)b & (1u << (r & 31));
+    else hi |= (uint32_t)(b >> 32) & (1u << (r & 31));
+  }
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Round 5.  Round 4's kernel checked every visited
+// state for an all-zero product and jumped from there: 56 scalar against 37
+// vector instructions per visited wave-state (counters,
+// profiles/r4/pmc_skip44_*.csv) — the scalar unit the four SIMDs of a CU
+// share was the bound, and per-state bookkeeping was its load (the check, the
+// sign, the loop's exits, the move).  A leaner per-state form of the same
+// policy still measured 59 scalar instructions (profiles/r5).  This kernel
+// changes the policy instead: it skips whole segments of 2^kSkipSegBits Gray
+// steps (aligned), and walks the others with walk_sparse's paired loop, whose
+// scalar work per step is a fraction of a checked step's:
+//   * at a segment start t (and only there) with every lane's term zero, the
+//     lane-uniform rows that are exactly zero and that no walk bit below
+//     kSkipSegBits touches are zero for the whole segment, and until one of
+//     their walk columns toggles: the wave moves to the last of those toggles
+//     (a segment start).  Skipped terms are exactly zero, so the sum is the
+//     per-state walk's (the skips are fewer: the simulation on config 5
+//     visits 27.6 % of the states instead of 21.8 %, tools/skip_sim);
+//   * elsewhere the pair (walk bit 0 with its block count in an SGPR, then
+//     walk bit ctz) steps and accumulates as walk_sparse does;
+//   * the move adds the differing walk columns block-wise and re-forms the
+//     suffix products once (bit-identical to one step per bit, see there);
+//   * the arguments only the zero scan and the chunk end read are loaded
+//     where they are used; U is kept out of LLVM's alloca-to-vector
+//     promotion (Makefile: promoted, the jump and step paths disagreed on its
+//     register layout, 8 v_mov_b64 per visited state).
+// The host twin (engine_cpu.cpp) and the oracle's mirror follow the same
+// segments, so results and visited counts agree bit for bit.
 template <int N>
 __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
   constexpr int NP = pad8(N);
-  constexpr int NB = Blocks<N>::NB;
   const uint32_t lane = threadIdx.x & 63u;
   const bool lane_valid = lane < (1u << p.L);
   const uint32_t lane_par = __builtin_popcount(lane) & 1u;
   const uint32_t T = 1u << p.m;
-  const uint32_t offL = 2u * (uint32_t)p.L * NP * 8u;
-  const uint64_t umask = p.umask;  // lane-uniform rows
+  const int nb0 = nb_of(p, 0);
 
   for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {
     double keep = 0.0;
@@ -61,76 +114,80 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
       const uint64_t ga = p.chunk_begin + a;
       double x[N];
       chunk_start<N>(x, p, ga, lane);
-      double U[NB + 1];
+      double U[Blocks<N>::NB + 1];
       suffix_all<N>(x, U);
-      double acc = 0.0;
-      uint32_t visited = 0;
-      uint32_t t = 0;
-      // Zero check after visiting state t (X valid for t, term added): if
-      // every lane's term is zero and some lane-uniform row is exactly zero,
-      // returns the index to continue from (X moved there), else t + 1 with
-      // X untouched (the caller takes the ordinary single-bit step).
-      auto jump = [&](uint32_t t) -> uint32_t {
-        // v_cmp straight into an SGPR mask per row (no VGPR temporaries);
-        // lane-uniform rows hold the same value on every lane, so lane 0 decides
-        uint64_t zm = 0;
-#pragma unroll
-        for (int r = 0; r < N; ++r) zm |= (__builtin_amdgcn_ballot_w64(x[r] == 0.0) & 1ull) << r;
-        zm &= umask;
-        if (!zm) return t + 1;
-        // each zero row r stays zero until one of its walk columns toggles (or
-        // for the rest of the chunk if it has none); the product is zero until
-        // the last of those toggles
-        uint32_t target = t + 1;
-        while (zm) {
-          const uint32_t r = (uint32_t)__builtin_ctzll(zm);
-          zm &= zm - 1;
-          uint64_t mm = ((const __attribute__((address_space(4))) uint64_t*)p.rowmask)[r];
-          uint32_t tr = T;
-          while (mm) {
-            const uint32_t k = (uint32_t)__builtin_ctzll(mm);
-            mm &= mm - 1;
-            const uint32_t c = next_toggle(t, k);
-            tr = c < tr ? c : tr;
-          }
-          target = tr > target ? tr : target;
-        }
-        if (target == t + 1 || target >= T) return target;
-        // Gray move t -> target: add the differing walk columns in ascending
-        // bit order (each to its nblk leading blocks), then refresh all suffix
-        // products once.  Bit-identical to one sparse_step per bit: block b's
-        // x is final after the last bit with nblk > b, and that step formed
-        // U[b] from it and the final U[b+1] — the same expression suffix_all
-        // evaluates on the final x.
-        const uint32_t gn = target ^ (target >> 1);
-        uint32_t diff = (t ^ (t >> 1)) ^ gn;
-        do {
-          const uint32_t k = (uint32_t)__builtin_ctz(diff);
-          diff &= diff - 1;
-          const uint32_t neg = ((gn >> k) & 1u) ^ 1u;
-          add_nest<N, 0>(x, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nb_of(p, k));
-        } while (diff);
-        suffix_all<N>(x, U);
-        return target | 0x80000000u;  // flag: X already moved
-      };
-      for (;;) {
-        // visit state t.  acc +/- term as one fma with an exact +-1 factor
-        // (bit-identical to the add/sub, no per-lane select)
-        ++visited;
-        acc = __builtin_fma((t & 1u) ? -1.0 : 1.0, U[0], acc);
-        if (__builtin_amdgcn_ballot_w64(U[0] != 0.0) == 0) {
-          const uint32_t nx = jump(t);
-          if (nx & 0x80000000u) {
-            t = nx & 0x7fffffffu;
-            continue;
+      const double* colw = p.cols + 2 * p.L * NP;  // walk bit k, sign s: colw + (2k + s) NP
+      double acc = U[0];  // state 0
+      uint32_t visited = 1;
+      uint32_t u = 1;
+      // state 0 opens a segment: the zero check before its walk (T = 1: state 0 is the chunk)
+      bool check = true;
+      for (; T > 1;) {
+        if (check && __builtin_amdgcn_ballot_w64(U[0] != 0.0) == 0) {
+          // Every lane's term at the segment start t = u - 1 is zero.  A
+          // lane-uniform row that is exactly zero and that no walk bit below
+          // kSkipSegBits touches stays zero for the whole segment and until one of its
+          // walk columns toggles (for the rest of the chunk if it has none):
+          // the product is zero until the last of those toggles over all such
+          // rows, a segment start.  Skipped terms are exactly zero.
+          const uint32_t t = u - 1;
+          uint64_t zm = zero_rows<N>(x) & SUP_KARG(umask);
+          const __attribute__((address_space(4))) uint64_t* rmask =
+              (const __attribute__((address_space(4))) uint64_t*)SUP_KARG(rowmask);
+          uint32_t nx = t;
+          while (zm) {
+            const uint32_t r = (uint32_t)__builtin_ctzll(zm);
+            zm &= zm - 1;
+            uint64_t mm = rmask[r];
+            if (mm & kSkipSegMask) continue;
+            uint32_t tr = T;
+            while (mm) {
+              const uint32_t k = (uint32_t)__builtin_ctzll(mm);
+              mm &= mm - 1;
+              const uint32_t c = next_toggle(t, k);
+              tr = c < tr ? c : tr;
+            }
+            nx = tr > nx ? tr : nx;
           }
           if (nx >= T) break;
+          if (nx > t) {
+            // Gray move t -> nx: add the differing walk columns in ascending
+            // bit order (each to its nblk leading blocks), then re-form every
+            // suffix product once.  Bit-identical to one step per bit: block
+            // b's x is final after the last bit with nblk > b, and that step
+            // formed U[b] from it and the final U[b + 1] — the expression
+            // suffix_all evaluates on the final x (oracle: e_sparse_step per bit).
+            const uint32_t gn = nx ^ (nx >> 1);
+            uint32_t diff = (t ^ (t >> 1)) ^ gn;
+            do {
+              const uint32_t k = (uint32_t)__builtin_ctz(diff);
+              diff &= diff - 1;
+              const uint32_t neg = ((gn >> k) & 1u) ^ 1u;
+              add_nest<N, 0>(x, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_of(p, k));
+            } while (diff);
+            suffix_all<N>(x, U);
+            u = nx + 1;
+            ++visited;
+            acc += U[0];  // nx is a segment start: even
+            continue;  // check the new segment start
+          }
         }
-        if (++t >= T) break;
-        // ordinary single-bit Gray step to t
-        const uint32_t k = (uint32_t)__builtin_ctz(t);
-        const uint32_t neg = (t >> (k + 1)) & 1u;
-        sparse_step<N>(x, U, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nb_of(p, k));
+        // the pair u (walk bit 0), u + 1 (walk bit ctz(u + 1)), as walk_sparse
+        {
+          int nbo = nb0;
+          asm volatile("" : "+s"(nbo));
+          sparse_step<N>(x, U, opaque_c(colw, ((u >> 1) & 1u) * NP * 8u), nbo);
+        }
+        acc -= U[0];
+        visited += (u + 1 < T) ? 2u : 1u;  // this state, and the next if there is one
+        if (u + 1 >= T) break;
+        const uint32_t v = u + 1;
+        const uint32_t k = (uint32_t)__builtin_ctz(v);
+        const uint32_t neg = (v >> (k + 1)) & 1u;
+        sparse_step<N>(x, U, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_of(p, k));
+        acc += U[0];
+        u += 2;
+        check = (v & kSkipSegMask) == 0;  // v opens a segment
       }
       if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;
       const double part = wave_sum(lane_valid ? acc : 0.0);
@@ -139,8 +196,9 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
     }
     const uint64_t a = (uint64_t)g * p.group + lane;
     if (lane < (uint32_t)p.group && a < p.chunk_count) {
-      p.chunk_out[a] = keep;
-      if (p.visited) p.visited[a] = vkeep;
+      SUP_KARG(chunk_out)[a] = keep;
+      unsigned int* vis = SUP_KARG(visited);
+      if (vis) vis[a] = vkeep;
     }
   }
 }

@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round-5 GPU sessions: each step under its own time limit, stop at the first
+# crash / timeout (exit >= 124), keep going after ordinary test failures.
+# usage: tools/session_r5.sh <tag> <step>...
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=$1; shift
+O=gpurun_out/$TAG
+mkdir -p "$O"
+export TMPDIR=/tmp
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "   rc=$rc"; tail -3 "$O/$name.log"
+  if [ $rc -eq 124 ] || [ $rc -ge 128 ]; then echo "STOP: $name exit $rc"; exit $rc; fi
+}
+PYT="python3 -u -m pytest -x -v --timeout 400 --timeout-method thread -p no:cacheprovider"
+for step in "$@"; do
+  case $step in
+    seg_cli) run pytest_seg_cli 500 $PYT tests/test_gpu_seg.py -k "cli or schedule";;
+    multidev) SUP_CHECK_DEVICE=1 run pytest_multidev 800 $PYT tests/test_gpu_multidev.py;;
+    skip_parity) run pytest_skip 600 $PYT tests/test_gpu_parity.py -k "config5 or skip or schedulers";;
+    skip_time) run probe_skip 300 python3 -u tools/probe_skip.py 3;;
+    skip_pmc) run pmc_skip 180 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_WAVES SQ_INSTS_SMEM GRBM_GUI_ACTIVE -d $O/pmc_skip -o run --output-format csv -- python3 tools/probe_skip.py 1;;
+    bench_cold) run bench_cold 400 python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 --also= --configs 0 --pmc 0;;
+    gpu_all) run pytest_gpu 1200 $PYT tests -m gpu;;
+    smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()";;
+    bench) run bench 900 python3 bench.py;;
+    *) echo "unknown step $step"; exit 2;;
+  esac
+done
+echo "== done"
