@@ -585,12 +585,14 @@ def main():
         b = load(path)
         nb = b.shape[0]
         e2, perm2, kms2, st2, _, _ = timed(b)
+        roof_b = roofline(path, b, args.prep, args.kernel, args.jit, kms2, st2)
+        roof_b["traffic"] = hbm_traffic(pmc_record(nb, roof_b["kernel"], roof_b["plan_key"]))
         also.append({"matrix": os.path.basename(path).replace("__", "/"), "n": nb,
                      "density": round(float((b != 0).sum()) / (nb * nb), 4),
                      "value": args.steps * (1 << (nb - 1)) / e2, "unit": "gray-steps/s",
                      "ms_per_step": e2 / args.steps * 1e3, "kernel_ms_avg": kms2,
                      "walk": walk_names[st2["walk_kind"]],
-                     "roofline": roofline(path, b, args.prep, args.kernel, args.jit, kms2, st2),
+                     "roofline": roof_b,
                      "permanent": perm2})
 
     # the other BASELINE configs (2, 3, 5), same shards / all-reduce / clock.

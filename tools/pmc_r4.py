@@ -2,7 +2,8 @@
 file under profiles/r4/, keyed by the plan it measured (sup_plan_key for the
 same request, computed here with torch's hiprtc as bench.py plans it).
 
-    python tools/pmc_r4.py <out.json> <matrix> <pmc dir> [<pmc dir> ...]   (request: dense, jit 1, no prep)
+    python tools/pmc_r4.py <out.json> <matrix> <pmc dir> [<pmc dir> ...] [--kernel K --jit J --prep P --walk NAME]
+    (default request: dense, jit 1, no prep, kernel sup_walk_seg)
 
 Every counter of the walk kernel's dispatch is kept (summed over the
 dispatches of the pass, which is one launch: bench.py --pmc-child), with
@@ -44,19 +45,33 @@ def counters(d, walk=WALK):
 
 
 def main():
-    dst, matrix = sys.argv[1:3]
-    dirs = sys.argv[3:]
-    kernel, jit, prep = "dense", 1, 0
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dst")
+    ap.add_argument("matrix")
+    ap.add_argument("dirs", nargs="+")
+    ap.add_argument("--kernel", default="dense")
+    ap.add_argument("--jit", type=int, default=1)
+    ap.add_argument("--prep", type=int, default=0)
+    ap.add_argument("--walk", default=WALK, help="kernel name filter (sup_walk_seg, sup::walk_skip<44>, ...)")
+    ap.add_argument("--visited", action="store_true", help="the walk also stores a visited count per wave-chunk")
+    args = ap.parse_args()
+    dst, matrix, dirs = args.dst, args.matrix, args.dirs
+    kernel, jit, prep, walk = args.kernel, args.jit, args.prep, args.walk
     a = S.read_matrix(matrix)[0]
+    if prep == 1:
+        a = S.sort_order(a)[0]
+    elif prep == 2:
+        a = S.skip_order(a)[0]
     info = S.plan_info(a, kernel, jit=jit)
     vals, ns = {}, []
     for d in dirs:  # one pass per directory (counters that cannot share a pass)
-        v, t = counters(d)
+        v, t = counters(d, walk)
         vals.update(v)
         ns += t
     if not vals:
-        sys.exit(f"no counters of {WALK} under {dirs}")
-    out = {"n": int(a.shape[0]), "matrix": os.path.basename(matrix), "kernel": WALK, "request": kernel, "jit": jit,
+        sys.exit(f"no counters of {walk} under {dirs}")
+    out = {"n": int(a.shape[0]), "matrix": os.path.basename(matrix), "kernel": walk, "request": kernel, "jit": jit,
            "prep": prep, "plan_key": hex(S.plan_key(a, kernel, jit=jit)), "walk": info["kind"],
            "cached": info["cached"], "pair_bits": info["pair_bits"], "model_ops_per_gray_step": info["est_ops_per_step"],
            "kernel_ns_per_pass": ns, "counters": vals,
@@ -76,6 +91,8 @@ def main():
         chunks = 1 << (a.shape[0] - 1 - info["L"] - info["m"])
         np_ = (a.shape[0] + 7) // 8 * 8
         alg = chunks * 8 + 2 * (a.shape[0] - 1) * np_ * 8 + np_ * 8
+        if args.visited:  # SkipPer / the chunk skip: one 4-byte visited count per wave-chunk
+            alg += chunks * 4
         # gfx950's FETCH_SIZE counts half the bytes of a wide coalesced read
         # (MI355X_MICROARCH.md, HBM / rocprofv3): doubled here (round 5 on)
         hbm = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0

@@ -28,6 +28,24 @@ for step in "$@"; do
     gpu_all) run pytest_gpu 1200 $PYT tests -m gpu;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()";;
     bench) run bench 900 python3 bench.py;;
+    hbm)  # FETCH_SIZE / WRITE_SIZE passes (separate: TCC counter limits) of every bench walk
+      P="rocprofv3 --kernel-trace -o run --output-format csv"
+      while read -r tag m k j pr w vis; do
+        C="python3 bench.py --pmc-child --matrix tests/fixtures/$m --kernel $k --jit $j --prep $pr"
+        run fetch_$tag 240 $P --pmc FETCH_SIZE -d $O/fetch_$tag -- $C
+        run write_$tag 240 $P --pmc WRITE_SIZE -d $O/write_$tag -- $C
+        run sum_$tag 300 python3 tools/pmc_r4.py $O/pmc_hbm_$tag.json tests/fixtures/$m $O/fetch_$tag $O/write_$tag \
+          --kernel $k --jit $j --prep $pr --walk "$w" $vis
+      done <<'LIST'
+d050 double__40_0.50_0 dense 1 0 sup_walk_seg
+d020 double__40_0.20_0 dense 1 0 sup_walk_seg
+d090 double__40_0.90_0 dense 1 0 sup_walk_seg
+cfg2 double__32_0.50_0 dense 1 0 sup_walk_seg
+cfg3 double__36_0.20_0 sparse 1 1 sup_walk_seg
+cfg5skip synth44_0.15_int skip -1 2 walk_skip<44> --visited
+cfg5 synth44_0.15_int skip 0 2 sup_walk_seg --visited
+LIST
+      ;;
     *) echo "unknown step $step"; exit 2;;
   esac
 done
