@@ -589,26 +589,53 @@ int leaf_batch_max() {
 // Several leaves of order n: each planned as sup_perman plans it (the same
 // plan, so the same bits), the batchable ones walked in one launch, the rest
 // one at a time through sup_perman.
-int leaf_compute_batch(const LeafCtx& c, const std::vector<const double*>& mats, int n,
-                       const std::vector<double*>& outs, sup_stats* st) {
-  auto t0 = std::chrono::steady_clock::now();
+// A batch of leaves planned on the host (leaf_plan_batch), walked later
+// (leaf_walk_batch), so a worker can plan the next batch while this one walks
+// (decompose_batched_staged).  Each leaf is planned as sup_perman plans it
+// (the same plan, so the same bits); the batchable ones walk in one launch,
+// the rest one at a time through sup_perman.
+struct LeafBatchState {
+  int n = 0;
+  std::vector<std::vector<double>> ms;
+  std::vector<std::shared_ptr<const Plan>> plans;
+  std::vector<double*> outs;
+  std::chrono::steady_clock::time_point t0;
+};
+
+int leaf_plan_batch(const LeafCtx& c, const std::vector<const double*>& mats, int n, const std::vector<double*>& outs,
+                    LeafBatchState& b) {
+  b.t0 = std::chrono::steady_clock::now();
   const size_t K = mats.size();
-  std::memset(st, 0, sizeof(*st));
-  std::vector<std::vector<double>> ms(K);
-  std::vector<std::shared_ptr<const Plan>> plans(K);
+  b.n = n;
+  b.outs = outs;
+  b.ms.assign(K, {});
+  b.plans.assign(K, nullptr);
   const Layout lay = layout_for(n, c.o);
   int rc = check_walk_opts(c.o);
   if (rc) return rc;
   for (size_t i = 0; i < K; ++i) {
-    ms[i].assign(mats[i], mats[i] + (size_t)n * n);
+    b.ms[i].assign(mats[i], mats[i] + (size_t)n * n);
     std::vector<int> rp(n), cp(n);
-    if (c.preprocessing == 1) rc = sup_sort_order(ms[i].data(), SUP_FLOAT64, n, cp.data());
-    else if (c.preprocessing == 2) rc = sup_skip_order(ms[i].data(), SUP_FLOAT64, n, rp.data(), cp.data());
+    if (c.preprocessing == 1) rc = sup_sort_order(b.ms[i].data(), SUP_FLOAT64, n, cp.data());
+    else if (c.preprocessing == 2) rc = sup_skip_order(b.ms[i].data(), SUP_FLOAT64, n, rp.data(), cp.data());
     if (rc) return rc;
     // batch leaves stay out of the process plan cache (32 entries): two batches of 16 would evict the
     // caller's plans; a repeated leaf is served by the reduction's leaf memo
-    if ((rc = plan_for_shared(ms[i].data(), n, c.kernel, lay, plans[i], c.o.jit, 1, c.o.device_id, false))) return rc;
+    if ((rc = plan_for_shared(b.ms[i].data(), n, c.kernel, lay, b.plans[i], c.o.jit, 1, c.o.device_id, false)))
+      return rc;
   }
+  return SUP_OK;
+}
+
+int leaf_walk_batch(const LeafCtx& c, const LeafBatchState& b, sup_stats* st) {
+  const size_t K = b.ms.size();
+  const int n = b.n;
+  const auto& ms = b.ms;
+  const auto& plans = b.plans;
+  const auto& outs = b.outs;
+  const auto t0 = b.t0;
+  int rc = SUP_OK;
+  std::memset(st, 0, sizeof(*st));
   const double sign = (double)(4 * (n & 1) - 2);  // gpu_exact_dense.cu:698
   std::vector<const Plan*> group;
   std::vector<size_t> gi;
@@ -648,6 +675,7 @@ int leaf_compute_batch(const LeafCtx& c, const std::vector<const double*>& mats,
   st->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return SUP_OK;
 }
+
 
 void leaf_accumulate(LeafCtx& c, const sup_stats& st) {
   if (c.first) {
@@ -759,18 +787,25 @@ int sup_perman_reduced(const void* mat, sup_dtype t, int n, sup_kernel kernel, s
   // else one at a time; either way the same bits
   const int rc =
       leaf_batching(c)
-          ? decompose_batched_multi(A.data(), n, r, leaf_workers(), leaf_batch_max(),
-                                    [&c, &smu](int w, const std::vector<const double*>& as, int k,
-                                               const std::vector<double*>& vs) {
-                                      set_ctx_lane(w);
-                                      sup_stats st;
-                                      const int e = leaf_compute_batch(c, as, k, vs, &st);
-                                      if (e) return e;
-                                      std::lock_guard<std::mutex> g(smu);
-                                      leaf_accumulate(c, st);
-                                      return SUP_OK;
-                                    },
-                                    out, &leaves)
+          // two stages: a worker plans its next batch while its walker thread walks this one
+          ? decompose_batched_staged(
+                A.data(), n, r, leaf_workers(), leaf_batch_max(),
+                [&c, &smu](int w, const std::vector<const double*>& as, int k, const std::vector<double*>& vs,
+                           std::function<int()>& walk) {
+                  set_ctx_lane(w);
+                  auto b = std::make_shared<LeafBatchState>();
+                  if (const int e = leaf_plan_batch(c, as, k, vs, *b)) return e;
+                  walk = [&c, &smu, b, w]() {
+                    set_ctx_lane(w);
+                    sup_stats st;
+                    if (const int e = leaf_walk_batch(c, *b, &st)) return e;
+                    std::lock_guard<std::mutex> g(smu);
+                    leaf_accumulate(c, st);
+                    return SUP_OK;
+                  };
+                  return SUP_OK;
+                },
+                out, &leaves)
           : decompose_batched(A.data(), n, r, c.on_cpu ? 1 : leaf_workers(),
                               [&c, &smu](int w, const double* a, int k, double* v) {
                                 set_ctx_lane(w);

@@ -27,6 +27,7 @@
 #include <cstring>
 #include <condition_variable>
 #include <deque>
+#include <type_traits>
 #include <functional>
 #include <mutex>
 #include <string>
@@ -402,7 +403,8 @@ int batched(const double* A, int n, const sup_reduce_opts& r, int workers,
             const std::function<int(int, const double*, int, typename Ops::V*)>& leaf, typename Ops::V* out,
             int* n_leaves, const char* who, bool memo, int batch_max = 1,
             const std::function<int(int, const std::vector<const double*>&, int,
-                                    const std::vector<typename Ops::V*>&)>* leaves = nullptr) {
+                                    const std::vector<typename Ops::V*>&)>* leaves = nullptr,
+            const LeafBatchStagedFn* staged = nullptr) {
   typedef typename Ops::V V;
   set_error("");
   if (int rc = check_reduce_opts(r, who)) return rc;
@@ -419,8 +421,51 @@ int batched(const double* A, int n, const sup_reduce_opts& r, int workers,
   bool closed = false, failed = false;
   int frc = SUP_OK;
   std::string ferr;
-  batch_max = leaves ? std::max(1, batch_max) : 1;
+  batch_max = leaves || staged ? std::max(1, batch_max) : 1;
   const size_t cap = (size_t)workers * 4 * (size_t)batch_max;
+  // Two-stage batches (staged): each worker plans its batch on the host and
+  // hands the device part to its own walker thread through a channel of
+  // depth 2, so the next batch is planned while this one walks (one worker:
+  // the GPU no longer idles while the host plans).  Batches of one worker walk
+  // in the order it planned them; values land in their slots either way.
+  struct Chan {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<int()>> q;
+    bool closed = false;
+  };
+  std::vector<std::unique_ptr<Chan>> chans;
+  std::vector<std::thread> walkers;
+  auto fail = [&](int e) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!failed) failed = true, frc = e, ferr = sup_last_error();
+    cv_put.notify_all();
+  };
+  if (staged) {
+    for (int w = 0; w < workers; ++w) chans.emplace_back(new Chan);
+    for (int w = 0; w < workers; ++w)
+      walkers.emplace_back([&, w]() {
+        Chan& ch = *chans[w];
+        for (;;) {
+          std::function<int()> job;
+          {
+            std::unique_lock<std::mutex> lk(ch.mu);
+            ch.cv.wait(lk, [&] { return !ch.q.empty() || ch.closed; });
+            if (ch.q.empty()) return;
+            job = std::move(ch.q.front());
+            ch.q.pop_front();
+          }
+          ch.cv.notify_all();
+          bool skip;
+          {
+            std::lock_guard<std::mutex> lk(mu);
+            skip = failed;
+          }
+          if (!skip)
+            if (const int e = job()) fail(e);
+        }
+      });
+  }
   auto work = [&](int w) {
     for (;;) {
       std::vector<Job> js;
@@ -442,7 +487,21 @@ int batched(const double* A, int n, const sup_reduce_opts& r, int workers,
         if (failed) continue;  // drain without computing
       }
       int e = SUP_OK;
-      if (leaves) {
+      if (staged) {
+        std::vector<const double*> mats;
+        std::vector<V*> slots;
+        for (const Job& j : js) mats.push_back(j.a.data()), slots.push_back(j.slot);
+        std::function<int()> walk;
+        if constexpr (std::is_same<V, double>::value) e = (*staged)(w, mats, js[0].n, slots, walk);
+        if (!e) {
+          Chan& ch = *chans[w];
+          std::unique_lock<std::mutex> lk(ch.mu);
+          ch.cv.wait(lk, [&] { return ch.q.size() < 2; });
+          ch.q.push_back(std::move(walk));
+          lk.unlock();
+          ch.cv.notify_all();
+        }
+      } else if (leaves) {
         std::vector<const double*> mats;
         std::vector<V*> slots;
         for (const Job& j : js) mats.push_back(j.a.data()), slots.push_back(j.slot);
@@ -450,11 +509,7 @@ int batched(const double* A, int n, const sup_reduce_opts& r, int workers,
       } else {
         e = leaf(w, js[0].a.data(), js[0].n, js[0].slot);
       }
-      if (e) {
-        std::lock_guard<std::mutex> lk(mu);
-        if (!failed) failed = true, frc = e, ferr = sup_last_error();
-        cv_put.notify_all();
-      }
+      if (e) fail(e);
     }
   };
   std::vector<std::thread> th;
@@ -500,6 +555,14 @@ int batched(const double* A, int n, const sup_reduce_opts& r, int workers,
   }
   cv_get.notify_all();
   for (auto& t : th) t.join();
+  for (auto& ch : chans) {  // the planners are done: let the walkers drain their channels
+    {
+      std::lock_guard<std::mutex> lk(ch->mu);
+      ch->closed = true;
+    }
+    ch->cv.notify_all();
+  }
+  for (auto& t : walkers) t.join();
   if (failed) {
     set_error(ferr);
     return frc;
@@ -523,12 +586,15 @@ int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int work
   return batched<DblOps>(A, n, r, workers, leaf, out, n_leaves, "sup_perman_reduced", memo);
 }
 
-int decompose_batched_multi(const double* A, int n, const sup_reduce_opts& r, int workers, int batch_max,
-                            const LeafBatchFn& leaves, double* out, int* n_leaves) {
+int decompose_batched_staged(const double* A, int n, const sup_reduce_opts& r, int workers, int batch_max,
+                             const LeafBatchStagedFn& staged, double* out, int* n_leaves) {
   const std::function<int(int, const double*, int, double*)> one = [&](int w, const double* a, int k, double* v) {
-    return leaves(w, std::vector<const double*>{a}, k, std::vector<double*>{v});
+    std::function<int()> walk;
+    const int e = staged(w, std::vector<const double*>{a}, k, std::vector<double*>{v}, walk);
+    return e ? e : walk();
   };
-  return batched<DblOps>(A, n, r, workers, one, out, n_leaves, "sup_perman_reduced", true, batch_max, &leaves);
+  return batched<DblOps>(A, n, r, workers, one, out, n_leaves, "sup_perman_reduced", true, batch_max, nullptr,
+                         &staged);
 }
 
 int decompose_dd_batched(const double* A, int n, const sup_reduce_opts& r, int workers,

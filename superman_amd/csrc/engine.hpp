@@ -379,12 +379,16 @@ struct dd;
 int decompose_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
                       const std::function<int(int, const double*, int, double*)>& leaf, double* out, int* n_leaves,
                       bool memo = true);
-// The same with leaves handed out in batches: a worker takes up to
-// `batch_max` queued leaves of one order at once and calls
-// leaves(worker, mats, n, values) (sup_perman_reduced: one launch per batch).
-typedef std::function<int(int, const std::vector<const double*>&, int, const std::vector<double*>&)> LeafBatchFn;
-int decompose_batched_multi(const double* A, int n, const sup_reduce_opts& r, int workers, int batch_max,
-                            const LeafBatchFn& leaves, double* out, int* n_leaves);
+// The same with leaves handed out in batches (a worker takes up to
+// `batch_max` queued leaves of one order at once), in two stages:
+// staged(worker, mats, n, values, walk) plans a batch
+// on the host and returns its device part in `walk`, which the worker's own
+// walker thread runs while the worker plans the next batch (channel depth 2).
+typedef std::function<int(int, const std::vector<const double*>&, int, const std::vector<double*>&,
+                          std::function<int()>&)>
+    LeafBatchStagedFn;
+int decompose_batched_staged(const double* A, int n, const sup_reduce_opts& r, int workers, int batch_max,
+                             const LeafBatchStagedFn& staged, double* out, int* n_leaves);
 int decompose_dd_batched(const double* A, int n, const sup_reduce_opts& r, int workers,
                          const std::function<int(int, const double*, int, dd*)>& leaf, dd* out, int* n_leaves);
 // Permanent in double-double (sup_perman_quad): *hi + *lo.

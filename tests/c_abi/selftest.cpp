@@ -14,6 +14,8 @@
 //   - the readers, CSR/CSC, SortOrder/SkipOrder, the -o/-u reductions.
 // Usage: selftest <repo root>
 #include <atomic>
+#include <functional>
+#include <memory>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -246,6 +248,44 @@ static void test_io_and_reductions(const std::string& root) {
     CHECK(sup::decompose_batched(R.data(), m, r, 6, [&](int, const double* a, int k, double* v) { return leaf(a, k, v); },
                                  &par, &lp) == SUP_OK);
     CHECK(ls == lp && ls > 4 && std::memcmp(&seq, &par, sizeof seq) == 0);
+    // two-stage batches (sup_perman_reduced's batched GPU form): planners hand
+    // each batch's walk to their walker threads; 1 and 3 workers, batches of
+    // up to 4 leaves, the walk on host threads here: the same bits
+    for (int workers : {1, 3}) {
+      double stg = 0.0;
+      int lst = 0;
+      const sup::LeafBatchStagedFn staged = [&](int, const std::vector<const double*>& as, int k,
+                                                const std::vector<double*>& vs, std::function<int()>& walk) {
+        auto mats = std::make_shared<std::vector<std::vector<double>>>();
+        for (const double* a : as) mats->emplace_back(a, a + (size_t)k * k);
+        walk = [mats, vs, k, &leaf]() {
+          for (size_t i = 0; i < mats->size(); ++i)
+            if (const int e = leaf((*mats)[i].data(), k, vs[i])) return e;
+          return SUP_OK;
+        };
+        return SUP_OK;
+      };
+      CHECK(sup::decompose_batched_staged(R.data(), m, r, workers, 4, staged, &stg, &lst) == SUP_OK);
+      CHECK(lst == ls && std::memcmp(&seq, &stg, sizeof seq) == 0);
+    }
+    // a failing walk stops the staged decomposition and its message survives the walker thread
+    {
+      std::atomic<int> walks{0};
+      double stg = 0.0;
+      const sup::LeafBatchStagedFn staged = [&](int, const std::vector<const double*>&, int,
+                                                const std::vector<double*>&, std::function<int()>& walk) {
+        walk = [&walks]() {
+          if (walks.fetch_add(1) == 1) {
+            sup::set_error("walk 1 failed on purpose");
+            return SUP_EHIP;
+          }
+          return SUP_OK;
+        };
+        return SUP_OK;
+      };
+      CHECK(sup::decompose_batched_staged(R.data(), m, r, 2, 2, staged, &stg, &lp) == SUP_EHIP);
+      CHECK(std::strcmp(sup_last_error(), "walk 1 failed on purpose") == 0);
+    }
     // a failing leaf stops the decomposition and its message survives the worker thread
     std::atomic<int> calls{0};
     CHECK(sup::decompose_batched(R.data(), m, r, 4,
