@@ -245,7 +245,7 @@ def pmc_record(n: int, kernel: str, key: str):
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if (d.get("n") == n and "hbm_bytes_per_launch" in d and kernel in d.get("kernel", "")
+        if (d.get("n") == n and "hbm_bytes_per_launch" in d and kernel.split("::")[-1] in d.get("kernel", "")
                 and d.get("plan_key") == key):
             d["_path"] = os.path.relpath(p, ROOT)
             return d
@@ -617,6 +617,11 @@ def main():
             roof2 = roofline(os.path.join(fx, fname), b, prep, kernel, jit, kms2, st2)
             pmc2 = pmc_record(nb, roof2["kernel"], roof2["plan_key"])
             roof2["traffic"] = hbm_traffic(pmc2)
+            visited = float(st2["visited_steps"])
+            if world > 1:  # the shards' visited counts differ (SkipPer's jumps): sum them
+                t = torch.tensor([visited], dtype=torch.float64, device=tdev)
+                dist.all_reduce(t)
+                visited = float(t.item())
             configs.append({"config": label, "matrix": fname.replace("__", "/"), "n": nb, "steps": k2,
                             "roofline": roof2,
                             "value": k2 * (1 << (nb - 1)) / e2, "unit": "gray-steps/s (nominal)",
@@ -625,8 +630,8 @@ def main():
                             # states evaluated / Gray steps (SkipPer's jumps and the segmented
                             # walk's chunk skip make it < 1); SURVEY 8(d): visited steps/s beside
                             # the nominal rate
-                            "visited_frac": st2["visited_steps"] * world / float(1 << (nb - 1)),
-                            "visited_steps_per_s": k2 * st2["visited_steps"] * world / e2,
+                            "visited_frac": visited / float(1 << (nb - 1)),
+                            "visited_steps_per_s": k2 * visited / e2,
                             "permanent": perm2})
 
     # every rank's walk-kernel time (strong-scaling diagnosis: the slowest rank sets the step)

@@ -28,6 +28,12 @@ for step in "$@"; do
     gpu_all) run pytest_gpu 1200 $PYT tests -m gpu;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()";;
     bench) run bench 900 python3 bench.py;;
+    stats) run stats 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
+             python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --configs 0 --also= --pmc 0 --cold 0;;
+    rehearse)
+      for g in 2 4 8; do
+        run rehearse_$g 400 python3 bench.py --gpus $g --rehearse --steps 3 --warmup 1 --cpu-seconds 0 --pmc 0 --cold 0
+      done;;
     hbm)  # FETCH_SIZE / WRITE_SIZE passes (separate: TCC counter limits) of every bench walk
       P="rocprofv3 --kernel-trace -o run --output-format csv"
       while read -r tag m k j pr w vis; do
