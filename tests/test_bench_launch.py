@@ -39,3 +39,24 @@ def test_gpus_without_devices_fails_loudly():
 def test_gpus_zero_refused():
     r = _run(["--gpus", "0"])
     assert r.returncode == 2
+
+
+def test_hbm_profiles_found_for_every_bench_walk():
+    """Every committed FETCH_SIZE / WRITE_SIZE profile of round 5 is found by
+    the lookup the bench line uses, under the kernel name the bench reports
+    (`sup::walk_skip<44>` for the ahead-of-time SkipPer kernel, whose profile
+    records `walk_skip<44>`)."""
+    import glob
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r5", "pmc_hbm_*.json")))
+    assert paths
+    for p in paths:
+        d = json.load(open(p))
+        kernel = d["kernel"] if d["kernel"].startswith("sup_") else "sup::" + d["kernel"]
+        rec = b.pmc_record(d["n"], kernel, d["plan_key"])
+        assert rec is not None, p
+        assert b.hbm_traffic(rec) > d["algorithmic_bytes_per_launch"], p
