@@ -692,6 +692,12 @@ def main():
         key = os.path.basename(args.matrix)
         if key in ex and args.prep == 0:
             rec["rel_err_vs_exact"] = abs(perm - ex[key]) / abs(ex[key])
+            rec["exact_source"] = (
+                "tests/golden/exact_corpus.json: this engine's exact integer path (sup_perman_exact: residue walks "
+                "+ CRT with a divisibility self-check) on the file's 6-digit decimals; that path matches the "
+                "reference's __float128 goldens wherever they exist (n <= 30, tests/test_gpu_exact.py), and at "
+                "n = 40 the double-double walk, a different arithmetic, lands within 1 ulp of it "
+                "(tests/test_gpu_quad.py::test_gpu_quad_bench_matrix)")
         for d in also:
             k2 = d["matrix"].replace("/", "__")
             if k2 in ex:
