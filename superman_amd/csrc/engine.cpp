@@ -151,6 +151,186 @@ std::vector<int> greedy_walk_order(const double* A, int n, int count) {
   return best;
 }
 
+// ---- SkipPer column order (round 5) ----------------------------------------
+// The SkipPer kernel's zero check at a wave-chunk's first state ends the chunk
+// when a row that no walk and no lane column touches ("uniform tail" row) is
+// exactly zero: its value is fixed for the whole chunk (x0 plus the chunk
+// bits' columns).  Which rows those are is decided by the set of walk + lane
+// columns, so the column map decides how many chunks SkipPer walks at all.
+// SkipOrder's own map (identity) walks 25.7 % of config 5's states
+// (profiles/r5); a map chosen for these chunk ends walks ~17 % at a lower
+// prefix cost (tools/skip_sim.c).
+namespace {
+struct SkipOrderEval {
+  const double* A;
+  int n, m, L;
+  std::vector<uint64_t> cm;  // column -> rows (bit set)
+  std::vector<double> x0;
+  // prefix-block cost of the first m columns (walk_cost's terms)
+  double prefix_cost(const std::vector<int>& o) const {
+    uint64_t placed = 0;
+    double cost = 0.0, w = 0.5;
+    for (int k = 0; k < m; ++k) {
+      placed |= cm[o[k]];
+      cost += w * (16.0 * ((__builtin_popcountll(placed) + 7) / 8) + 1.0);
+      w *= 0.5;
+    }
+    return cost + w * 16.0 * ((n + 7) / 8);
+  }
+  // sampled fraction of wave-chunks whose first state has an exactly zero
+  // uniform tail row (integer matrices: every sum here is exact); chunk
+  // indices drawn as in seg_skip_estimate (jit.cpp)
+  double kill(const std::vector<int>& o, int samples) const {
+    const int nb = n - 1;
+    uint64_t wl = 0;  // rows touched by a walk or lane column
+    std::vector<char> used(nb, 0);
+    for (int k = 0; k < m + L; ++k) wl |= cm[o[k]], used[o[k]] = 1;
+    std::vector<int> high;
+    for (int c = 0; c < nb; ++c)
+      if (!used[c]) high.push_back(c);
+    struct Row {
+      double x0;
+      std::vector<std::pair<int, double>> hi;
+    };
+    std::vector<Row> rows;
+    for (int r = 0; r < n; ++r) {
+      if ((wl >> r) & 1u) continue;
+      Row q{x0[r], {}};
+      for (int k = 0; k < (int)high.size(); ++k)
+        if (A[(size_t)r * n + high[k]] != 0.0) q.hi.push_back({k, A[(size_t)r * n + high[k]]});
+      rows.push_back(std::move(q));
+    }
+    if (rows.empty()) return 0.0;
+    const int h = (int)high.size();
+    int killed = 0;
+    for (int s = 0; s < samples; ++s) {
+      const uint64_t a = h ? ((uint64_t)s * 0x9E3779B97F4A7C15ull) >> (64 - std::min(h, 63)) : 0;
+      const uint64_t g = a ^ (a >> 1);
+      for (const Row& q : rows) {
+        double v = q.x0;
+        for (const auto& e : q.hi)
+          if ((g >> e.first) & 1u) v += e.second;
+        if (v == 0.0) {
+          ++killed;
+          break;
+        }
+      }
+    }
+    return (double)killed / samples;
+  }
+  double eff(const std::vector<int>& o, int samples) const { return prefix_cost(o) * (1.0 - kill(o, samples)); }
+};
+}  // namespace
+
+// Walk + lane columns (m + L of them, walk first) for the SkipPer walk of an
+// integer matrix, chosen on ops per nominal step x the fraction of chunks not
+// ended at their first state; false when SkipOrder's own map (columns
+// L..L+m-1 walk, 0..L-1 lanes) is not clearly worse (the estimate does not see
+// the jumps inside a chunk, which favour SkipOrder's map: it must be beaten
+// by 2x).  Deterministic (fixed seeds, results gathered in start order), so
+// every process and host plans the same walk.  Random-restart local search:
+// starts = the greedy prefix order, SkipOrder's map and random column sets;
+// each start takes kRounds random moves (swap a walk or lane column with an
+// unused one, or a walk with a lane column), keeping improvements on a
+// 512-sample estimate; the best end on 8192 samples wins.
+bool skip_walk_order(const double* A, int n, const Layout& lay, std::vector<int>& out) {
+  const int nb = n - 1, m = lay.m, L = lay.L;
+  if (m < 3 || m + L >= nb) return false;
+  SkipOrderEval E{A, n, m, L, std::vector<uint64_t>(nb, 0), std::vector<double>(n)};
+  for (int c = 0; c < nb; ++c)
+    for (int i = 0; i < n; ++i)
+      if (A[(size_t)i * n + c] != 0.0) E.cm[c] |= 1ull << i;
+  double p0;
+  nw_start(A, n, E.x0.data(), &p0);
+  std::vector<int> ident;
+  for (int k = 0; k < m; ++k) ident.push_back(L + k);
+  for (int e = 0; e < L; ++e) ident.push_back(e);
+  constexpr int kStarts = 12, kRounds = 400, kScreen = 512, kFinal = 8192;
+  std::vector<std::vector<int>> starts;
+  {
+    std::vector<int> g = greedy_walk_order(A, n, m + L);
+    starts.push_back(g);
+    starts.push_back(ident);
+    uint64_t z = 0x5EED5C1Bull;
+    auto rnd = [&z]() {  // splitmix64
+      uint64_t x = (z += 0x9E3779B97F4A7C15ull);
+      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+      x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+      return x ^ (x >> 31);
+    };
+    while ((int)starts.size() < kStarts) {
+      std::vector<int> cols(nb);
+      for (int c = 0; c < nb; ++c) cols[c] = c;
+      for (int i = nb - 1; i > 0; --i) std::swap(cols[i], cols[rnd() % (uint64_t)(i + 1)]);
+      cols.resize(m + L);
+      starts.push_back(cols);
+    }
+  }
+  std::vector<std::vector<int>> ends(starts.size());
+  std::vector<double> effs(starts.size());
+  auto search = [&](size_t si) {
+    uint64_t z = 0xC0FFEEull + 7919ull * si;
+    auto rnd = [&z]() {
+      uint64_t x = (z += 0x9E3779B97F4A7C15ull);
+      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+      x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+      return x ^ (x >> 31);
+    };
+    std::vector<int> cur = starts[si];
+    double cv = E.eff(cur, kScreen);
+    std::vector<char> in(nb, 0);
+    for (int c : cur) in[c] = 1;
+    for (int it = 0; it < kRounds; ++it) {
+      std::vector<int> t = cur;
+      const int a = (int)(rnd() % (uint64_t)(m + L));
+      // the other side of the move: an unused column, or (walk <-> lane) a
+      // position on the other side
+      const int n_out = nb - (m + L), n_other = a < m ? L : m;
+      const int pick = (int)(rnd() % (uint64_t)(n_out + n_other));
+      int incoming = -1;
+      if (pick < n_out) {
+        int k = pick;
+        for (int c = 0; c < nb; ++c)
+          if (!in[c] && k-- == 0) {
+            incoming = c;
+            break;
+          }
+        t[a] = incoming;
+      } else {
+        const int b = a < m ? m + (pick - n_out) : pick - n_out;
+        std::swap(t[a], t[b]);
+      }
+      const double v = E.eff(t, kScreen);
+      if (v < cv) {
+        if (incoming >= 0) in[cur[a]] = 0, in[incoming] = 1;
+        cur = std::move(t), cv = v;
+      }
+    }
+    ends[si] = cur;
+    effs[si] = E.eff(cur, kFinal);
+  };
+  {
+    std::atomic<size_t> next{0};
+    auto worker = [&]() {
+      for (size_t i = next++; i < starts.size(); i = next++) search(i);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < std::min<int>(plan_threads(), (int)starts.size()); ++t) th.emplace_back(worker);
+    worker();
+    for (auto& t : th) t.join();
+  }
+  size_t bi = 0;
+  for (size_t i = 1; i < ends.size(); ++i)
+    if (effs[i] < effs[bi] - 1e-12) bi = i;
+  const double e_ident = E.eff(ident, kFinal);
+  if (std::getenv("SUP_JIT_VERBOSE"))
+    std::fprintf(stderr, "skip column search n=%d: best eff %.4f (cost %.3f, kill %.3f) vs SkipOrder's %.4f\n", n,
+                 effs[bi], E.prefix_cost(ends[bi]), E.kill(ends[bi], kFinal), e_ident);
+  if (!(effs[bi] < 0.5 * e_ident)) return false;
+  out = ends[bi];
+  return true;
+}
+
 double walk_cost(const Plan& P) {
   if (P.kind == kWalkDense) return 2.0 * P.n + 1.0;
   if (P.kind == kWalkSeg) return seg_walk_cost(P);
@@ -184,7 +364,8 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
   // ---- engine bit -> matrix column
   P.colmap.resize(nb);
   for (int e = 0; e < nb; ++e) P.colmap[e] = e;
-  if (!identity_map && (kind == kWalkSparse || kind == kWalkSeg) && m > 0) {
+  const bool skip_order = kind == kWalkSkip && choice && m > 0;  // a searched SkipPer map (skip_walk_order)
+  if (!identity_map && (kind == kWalkSparse || kind == kWalkSeg || skip_order) && m > 0) {
     // walk bits get the greedy prefix order (greedy_walk_order; the segmented
     // walk: seg_walk_order), lane bits the next L columns of that order, high
     // bits the rest in matrix order.
@@ -202,7 +383,13 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
       }
       return true;
     };
-    if (kind == kWalkSeg && choice && valid_order(choice->order) && choice->b >= 0 && choice->b <= m) {
+    if (skip_order) {
+      if (!valid_order(choice->order)) {
+        set_error("SkipPer column order: not m + L distinct flippable columns");
+        return SUP_EINVAL;
+      }
+      order = choice->order;
+    } else if (kind == kWalkSeg && choice && valid_order(choice->order) && choice->b >= 0 && choice->b <= m) {
       order = choice->order;
       segb = choice->b;
     } else {
@@ -222,11 +409,12 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
     // 5 before: the top chunk bit alone decided skipping, half the shards had
     // nothing to walk at 2, 4 and 8 GPUs.)  Otherwise matrix order.
     std::vector<char> top(n, 0);
-    if (kind == kWalkSeg) {
+    if (kind == kWalkSeg || skip_order) {
       bool integral = true;
       for (size_t i = 0; i < (size_t)n * n && integral; ++i) integral = A[i] == std::floor(A[i]);
+      // (SkipPer ends a chunk on a row no walk and no lane column touches)
       std::vector<char> wrow(n, 0);
-      for (int k = 0; k < m; ++k)
+      for (int k = 0; k < (skip_order ? m + L : m); ++k)
         for (int i = 0; i < n; ++i) wrow[i] |= A[(size_t)i * n + order[k]] != 0.0;
       for (int c = 0; c < nb && integral; ++c) {
         top[c] = 1;
@@ -551,11 +739,15 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
 
 // SkipPer evaluates only the states its zero checks cannot rule out; its
 // checks and jumps cost it efficiency per evaluated state.  Round 5's kernel
-// (segment-start checks, walk_sparse's paired steps elsewhere) on config 5
-// int: 25.5 modelled ops per visited state, 25.7 % visited, 2.245 s — 2.57e13
-// ops/s against the plain walks' 3.7e13 (profiles/r5/probe_skip.log; round 4's
-// per-state kernel: 0.37, profiles/r1/probe_seg.log).
-static constexpr double kSkipEfficiency = 0.69;
+// (segment-start checks, walk_sparse's paired steps elsewhere) with the
+// searched column map (skip_walk_order) on config 5 int: 19.3 modelled ops per
+// visited state, 11.6 % visited, 0.836 s — 2.35e13 ops/s against the plain
+// walks' 3.7e13 (profiles/r5/probe_skip_searched_map.log; SkipOrder's map:
+// 0.69, round 4's per-state kernel: 0.37).
+static constexpr double kSkipEfficiency = 0.64;
+// SkipPer walks predicted (every state, SkipOrder's map) to take at least
+// this long search their column map for chunk ends (~0.1-0.3 s of host time).
+static constexpr double kSkipSearchMinSec = 1.0;
 
 // Fraction of the states the SkipPer plan P evaluates, measured on a fixed
 // sample of its wave-chunks (8 evenly spaced ranges, ~1/64 of the walk) on
@@ -632,9 +824,21 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
       // device the request keeps SkipPer).  The segmented walk (same sum,
       // every state) runs instead when that is cheaper.
       int rc = make_plan(A, n, kWalkSkip, false, lay, P);
-      if (rc || jit < 0 || n < 10 || lay.m < 3) return rc;
+      if (rc) return rc;
       bool integral = true;
       for (size_t i = 0; i < (size_t)n * n && integral; ++i) integral = A[i] == std::floor(A[i]);
+      // an integer matrix whose SkipPer walk is long: the column map chosen
+      // for the chunks SkipPer ends at their first state (skip_walk_order;
+      // decided from the matrix alone, so every device count and host plans
+      // the same walk)
+      if (integral && n >= 10 &&
+          std::ldexp(1.0, n - 1) * walk_cost(P) / (kSkipEfficiency * kLaneOpsPerSec) >= kSkipSearchMinSec) {
+        SegChoice c;
+        Plan Q;
+        if (skip_walk_order(A, n, lay, c.order) && make_plan(A, n, kWalkSkip, false, lay, Q, &c) == SUP_OK)
+          P = std::move(Q);
+      }
+      if (jit < 0 || n < 10 || lay.m < 3) return SUP_OK;
       const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
       double skip_cost = walk_cost(P) / (integral ? kSkipEfficiency : 1.0);  // f <= 1
       const AutoRecord rec(A, n, lay, kernel, ndev, jit, steps * skip_cost / kLaneOpsPerSec);

@@ -136,6 +136,11 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
 
 // Walk-column order minimising the prefix-block cost (first `count` columns).
 std::vector<int> greedy_walk_order(const double* A, int n, int count);
+// SkipPer walk + lane columns (walk first) chosen for the chunks its first-state
+// zero check ends (integer matrices); false: keep SkipOrder's map (engine.cpp).
+bool skip_walk_order(const double* A, int n, const Layout& lay, std::vector<int>& out);
+// Host threads the planners' searches use (jit.cpp).
+int plan_threads();
 
 // ---- segmented walk (jit.cpp) ----
 // Walk-column order for the segmented walk: greedy starts from every column,

@@ -127,3 +127,32 @@ def test_config5_fixtures_reproducible(sup, tmp_path):
         b, t, _ = sup.read_matrix(fixture_path(f"synth44_0.15_{typ}"))
         assert t == typ and np.array_equal(a, b)
         assert (b != 0).any(0).all() and (b != 0).any(1).all()
+
+
+def test_skipper_column_search(sup):
+    """SkipPer's column map for long integer walks (engine.cpp
+    skip_walk_order): config 5 takes a searched map, the same in every process
+    (the plan must not depend on the host or the device count), with a lower
+    prefix cost than SkipOrder's map; a non-integer matrix and a short walk keep
+    SkipOrder's map (engine bit e = column e)."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    a = sup.skip_order(sup.read_matrix(fixture_path("synth44_0.15_int"))[0])[0]
+    info = sup.plan_info(a, "skip", jit=-1)
+    assert info["kind"] == "skip"
+    cm = [int(c) for c in info["colmap"]]
+    assert sorted(cm) == list(range(a.shape[0] - 1))
+    assert cm != list(range(a.shape[0] - 1))
+    assert info["est_ops_per_step"] < 25.5
+    code = ("import sys; sys.path.insert(0, %r); import superman_amd as S; "
+            "a = S.skip_order(S.read_matrix(%r)[0])[0]; "
+            "print(' '.join(map(str, S.plan_info(a, 'skip', jit=-1)['colmap'])))") % (
+        ROOT, fixture_path("synth44_0.15_int"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True,
+                         env=dict(os.environ, OMP_NUM_THREADS="3")).stdout.split()
+    assert [int(c) for c in out] == cm
+    real = sup.skip_order(sup.read_matrix(fixture_path("synth44_0.15_double"))[0])[0]
+    assert [int(c) for c in sup.plan_info(real, "skip", jit=-1)["colmap"]] == list(range(43))
+    short = sup.skip_order(sup.read_matrix(fixture_path("int__30_0.20_0"))[0])[0]
+    assert [int(c) for c in sup.plan_info(short, "skip", jit=-1)["colmap"]] == list(range(29))
