@@ -37,6 +37,7 @@ for step in "$@"; do
     hbm)  # FETCH_SIZE / WRITE_SIZE passes (separate: TCC counter limits) of every bench walk
       P="rocprofv3 --kernel-trace -o run --output-format csv"
       while read -r tag m k j pr w vis; do
+        [ -n "${HBM_ONLY:-}" ] && [ "$tag" != "$HBM_ONLY" ] && continue
         C="python3 bench.py --pmc-child --matrix tests/fixtures/$m --kernel $k --jit $j --prep $pr"
         run fetch_$tag 240 $P --pmc FETCH_SIZE -d $O/fetch_$tag -- $C
         run write_$tag 240 $P --pmc WRITE_SIZE -d $O/write_$tag -- $C
