@@ -158,7 +158,7 @@ std::vector<int> greedy_walk_order(const double* A, int n, int count) {
 // bits' columns).  Which rows those are is decided by the set of walk + lane
 // columns, so the column map decides how many chunks SkipPer walks at all.
 // SkipOrder's own map (identity) walks 25.7 % of config 5's states
-// (profiles/r5); a map chosen for these chunk ends walks ~17 % at a lower
+// (profiles/r5); a map chosen for these chunk ends walks 10.6 % at a lower
 // prefix cost (tools/skip_sim.c).
 namespace {
 struct SkipOrderEval {
@@ -245,7 +245,7 @@ bool skip_walk_order(const double* A, int n, const Layout& lay, std::vector<int>
   std::vector<int> ident;
   for (int k = 0; k < m; ++k) ident.push_back(L + k);
   for (int e = 0; e < L; ++e) ident.push_back(e);
-  constexpr int kStarts = 12, kRounds = 400, kScreen = 512, kFinal = 8192;
+  constexpr int kStarts = 16, kRounds = 1500, kScreen = 512, kFinal = 8192;
   std::vector<std::vector<int>> starts;
   {
     std::vector<int> g = greedy_walk_order(A, n, m + L);
@@ -741,13 +741,14 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
 // checks and jumps cost it efficiency per evaluated state.  Round 5's kernel
 // (segment-start checks, walk_sparse's paired steps elsewhere) with the
 // searched column map (skip_walk_order) on config 5 int: 19.3 modelled ops per
-// visited state, 11.6 % visited, 0.836 s — 2.35e13 ops/s against the plain
+// visited state, 10.6 % visited, 0.779 s — 2.31e13 ops/s against the plain
 // walks' 3.7e13 (profiles/r5/probe_skip_searched_map.log; SkipOrder's map:
 // 0.69, round 4's per-state kernel: 0.37).
-static constexpr double kSkipEfficiency = 0.64;
+static constexpr double kSkipEfficiency = 0.62;
 // SkipPer walks predicted (every state, SkipOrder's map) to take at least
-// this long search their column map for chunk ends (~0.1-0.3 s of host time).
-static constexpr double kSkipSearchMinSec = 1.0;
+// this long search their column map for chunk ends (~0.2-0.6 s of host time;
+// config 5: 9.5 s predicted, 0.74 s walked after the search).
+static constexpr double kSkipSearchMinSec = 4.0;
 
 // Fraction of the states the SkipPer plan P evaluates, measured on a fixed
 // sample of its wave-chunks (8 evenly spaced ranges, ~1/64 of the walk) on
