@@ -732,6 +732,18 @@ static double e_chunk(const eplan* P, unsigned long long ga, unsigned long long*
   int n = P->n, L = P->L, m = P->m, NB = (n + 7) / 8;
   unsigned T = 1u << m;
   double lv[64];
+  if (P->kind == 1) {
+    /* walk_sparse.hip's chunk end (round 5): a lane-uniform row that no walk
+     * column touches is constant over the chunk; exactly zero at its first
+     * state, every term is zero and the chunk's part is +0 */
+    double x[ORC_MAXN];
+    e_start(P, ga, 0, x);
+    for (int r = 0; r < n; ++r)
+      if (((P->umask >> r) & 1ULL) && P->rowmask[r] == 0 && x[r] == 0.0) {
+        if (visited) *visited += (unsigned long long)T << L;
+        return 0.0;
+      }
+  }
   if (P->kind != 2) {
     for (unsigned l = 0; l < 64; ++l) {
       if (l >= (1u << L)) {

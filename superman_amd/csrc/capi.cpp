@@ -572,18 +572,19 @@ bool leaf_batching(const LeafCtx& c) {
   return !c.on_cpu && c.sched == SUP_SCHED_SINGLE && c.o.use_rccl == 0 && !(c.o.checkpoint && *c.o.checkpoint) &&
          (c.kernel == SUP_KERNEL_DENSE || c.kernel == SUP_KERNEL_SPARYSER || c.kernel == SUP_KERNEL_DENSE_PLAIN);
 }
-// Default: batches of 16 when the leaves run one worker at a time, none with
-// several workers.  Measured on dwt_59 (145,798 n = 30 leaves, one MI355X,
-// profiles/r4/probe_reduce_batch.log): one worker 65.2 s -> 46.7 s with
-// batches of 16 (1.12e12 -> 1.56e12 leaf Gray steps/s); with 8 workers the
-// concurrent one-leaf launches already fill the GPU (37.8 s, 1.93e12, ~90 % of
-// the prefix-blocked walk's issue bound) and batches of 16 are slower (39.6 s:
-// the batch kernel holds its leaf's table pointers in SGPRs, 34 SGPR spills
-// against 12 in the one-leaf kernel at n = 30).
+// Default: batches of 16.  Measured on dwt_59 (145,798 n = 30 leaves, one
+// MI355X): round 4, one worker 65.2 s -> 46.7 s with batches of 16, but with 8
+// workers the concurrent one-leaf launches filled the GPU (37.8 s against
+// 39.6 s batched), so batches were for one worker only.  Since round 5 the
+// prefix-blocked walk ends ~64 % of these leaves' chunks at their first state
+// (walk_sparse.hip): the leaves are short, launches and host planning weigh
+// more, and batches win at every worker count — 8 workers 17.9 s one leaf per
+// launch, 12.7 s batched; one worker 48.1 s / 16.8 s
+// (profiles/r5/probe_reduce_chunk_ends.log).
 int leaf_batch_max() {
   const char* e = std::getenv("SUP_LEAF_BATCH");
   if (e) return std::max(1, std::min(kMaxBatchLeaves, std::atoi(e)));
-  return leaf_workers() == 1 ? 16 : 1;
+  return 16;
 }
 
 // Several leaves of order n: each planned as sup_perman plans it (the same

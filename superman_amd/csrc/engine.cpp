@@ -488,6 +488,9 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
     for (int k = 0; k < m; ++k)
       if (A[(size_t)i * n + P.colmap[L + k]] != 0.0) rm |= 1ull << k;
     P.rowmask[j] = rm;
+    // a lane-uniform row no walk column touches is constant over a wave-chunk:
+    // exactly zero at the chunk's first state, the chunk ends there (walk_sparse)
+    if (kind == kWalkSparse && !lane_touched && rm == 0) P.chunk_ends |= 1ull << j;
   }
   if (kind == kWalkSeg) return build_seg(P, choice ? choice->budget : 0);
   return SUP_OK;
@@ -1291,7 +1294,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   p.L = P.lay.L;
   p.m = P.lay.m;
   p.n = P.n;
-  p.umask = P.umask;
+  p.umask = P.kind == kWalkSparse ? P.chunk_ends : P.umask;  // walk_sparse: its chunk-end rows
   p.chunk_out = c->d_chunk;
   p.counter = c->d_counter;
   p.visited = visited ? c->d_visited : nullptr;
@@ -1414,6 +1417,7 @@ int run_range_batch(int dev, const std::vector<const Plan*>& plans, std::vector<
     desc[i].cols = c->d_batch + i * stride;
     desc[i].x0 = c->d_batch + i * stride + colsz;
     desc[i].nb_lo = desc[i].nb_hi = 0;
+    desc[i].ends = P.kind == kWalkSparse ? P.chunk_ends : 0;
     for (int k = 0; k < P.lay.m && k < 32 && P.kind == kWalkSparse; ++k) {
       const uint64_t v = (uint64_t)(P.nblk[P.lay.L + k] & 15);
       if (k < 16) desc[i].nb_lo |= v << (4 * k);

@@ -82,6 +82,7 @@ struct Plan {
   std::vector<int> nblk;           // n-1: prefix row-block count per engine bit
   std::vector<uint64_t> rowmask;   // n: walk-bit mask of each engine row
   uint64_t umask = 0;              // lane-uniform engine rows
+  uint64_t chunk_ends = 0;         // prefix-blocked walk: lane-uniform rows no walk column touches (walk_sparse.hip)
   // ---- segmented walk (kind kWalkSeg, jit.cpp) ----
   // Engine rows [0, R) are the rows some walk column touches, in first-touch
   // order; segment i = rows [seg_start[i], seg_start[i+1]) are the rows walk

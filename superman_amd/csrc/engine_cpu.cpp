@@ -274,6 +274,14 @@ double chunk_partial(const Plan& P, uint64_t ga) {
     return pairwise64(lane_val);
   }
   if (P.kind != kWalkSkip) {
+    if (P.kind == kWalkSparse && P.chunk_ends) {
+      // the kernel's chunk end: a chunk-end row (lane-uniform, no walk column)
+      // exactly zero at the first state -> the chunk's part is +0
+      Lane s;
+      chunk_start(P, ga, 0, s);
+      for (int j = 0; j < n; ++j)
+        if (((P.chunk_ends >> j) & 1u) && s.x[j] == 0.0) return 0.0;
+    }
     for (unsigned l = 0; l < 64; ++l) {
       if (l >= (1u << L)) {
         lane_val[l] = 0.0;

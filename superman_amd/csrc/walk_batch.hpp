@@ -19,6 +19,7 @@ struct LeafDesc {
   const double* x0;         // its start vector (NP)
   unsigned long long nb_lo;  // prefix-blocked walk: packed nblk (WalkParams::nb_lo / nb_hi)
   unsigned long long nb_hi;
+  unsigned long long ends;   // prefix-blocked walk: chunk-end rows (walk_sparse.hip; WalkParams::umask there)
 };
 
 struct LeafBatch {

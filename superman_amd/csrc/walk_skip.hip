@@ -18,6 +18,7 @@
 //     row r flips), so the sum is unchanged.
 // Rows are prefix-blocked exactly as in walk_sparse.hip.
 #include "walk_common.hpp"
+#include "walk_zero.hpp"
 #include "kernels.hpp"
 
 namespace sup {
@@ -39,34 +40,6 @@ __device__ __forceinline__ void add_nest(double (&x)[N], cdbl* col, int nb) {
       add_nest<N, B + 1>(x, col, nb);
     }
   }
-}
-
-// A kernel argument read where it is used: a scalar load from the kernarg
-// segment through an opaque base, so the value is not held in SGPRs across the
-// walk (the register allocator spilled such values to VGPR lanes and reloaded
-// them with v_readlane on every visited state).
-template <class T>
-__device__ __forceinline__ T karg_at(uint32_t offset) {
-  uint64_t a = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(a));
-  return *(const __attribute__((address_space(4))) T*)(a + offset);
-}
-#define SUP_KARG(field) karg_at<decltype(WalkParams::field)>((uint32_t)__builtin_offsetof(WalkParams, field))
-
-// Zero test of every row, one bit per row: a lane-uniform row holds the same
-// value on every lane, so its ballot is 0 or all ones and bit r of it stands
-// for lane 0 (rows outside umask are dropped by the caller).  Two scalar ops
-// per row (and, or) beside the compare; round 4's form took three.
-template <int N>
-__device__ __forceinline__ uint64_t zero_rows(const double (&x)[N]) {
-  uint32_t lo = 0, hi = 0;
-#pragma unroll
-  for (int r = 0; r < N; ++r) {
-    const uint64_t b = __builtin_amdgcn_ballot_w64(x[r] == 0.0);
-    if (r < 32) lo |= (uint32_t)b & (1u << (r & 31));
-    else hi |= (uint32_t)(b >> 32) & (1u << (r & 31));
-  }
-  return ((uint64_t)hi << 32) | lo;
 }
 
 // Round 5.  Round 4's kernel checked every visited

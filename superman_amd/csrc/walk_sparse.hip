@@ -16,7 +16,17 @@
 // step costs a fraction of the dense 2n ops.  Zero rows need no special case:
 // a zero x_j simply makes the product 0 (the reference's zero_num logic
 // computes the same term).
+//
+// Chunk end at the first state (round 5): a lane-uniform row that no walk
+// column touches keeps its value for the whole wave-chunk (x0 plus the chunk
+// bits' columns); when one of those rows (WalkParams::umask, set by the host
+// to exactly them for this kernel) is exactly zero, every term of the chunk is
+// an exact zero and the chunk's part is +0 without walking it — the segmented
+// walk's chunk skip in the ahead-of-time kernel (integer matrices: the -o
+// leaves of dwt_59 end ~64 % of their chunks there).  The oracle's mirror and
+// the host twin end the same chunks.
 #include "walk_common.hpp"
+#include "walk_zero.hpp"
 #include "walk_batch.hpp"
 #include "kernels.hpp"
 
@@ -41,6 +51,10 @@ __global__ __launch_bounds__(kBlock) void walk_sparse(WalkParams p) {
       const uint64_t ga = p.chunk_begin + a;
       double x[N];
       chunk_start<N>(x, p, ga, lane);
+      if (zero_rows<N>(x) & SUP_KARG(umask)) {  // chunk end: every term an exact zero
+        keep = (lane == j) ? 0.0 : keep;
+        continue;
+      }
       double U[NB + 1];
       suffix_all<N>(x, U);
       double acc = U[0];
@@ -77,11 +91,12 @@ __global__ __launch_bounds__(kBlock) void walk_sparse(WalkParams p) {
 // kept apart so the one-leaf kernel's code is untouched).
 template <int N>
 __device__ __forceinline__ double sparse_chunk(const WalkParams& p, uint64_t ga, uint32_t lane, uint32_t lane_par,
-                                               uint32_t T, uint32_t offL, int nb0) {
+                                               uint32_t T, uint32_t offL, int nb0, uint64_t ends) {
   constexpr int NP = pad8(N);
   constexpr int NB = Blocks<N>::NB;
   double x[N];
   chunk_start<N>(x, p, ga, lane);
+  if (zero_rows<N>(x) & ends) return 0.0;  // chunk end (see walk_sparse): every lane's part +0
   double U[NB + 1];
   suffix_all<N>(x, U);
   double acc = U[0];
@@ -132,7 +147,7 @@ __global__ __launch_bounds__(kBlock) void walk_sparse_batch(WalkParams p, LeafBa
     double keep = 0.0;
     for (uint32_t j = 0; j < group; ++j) {
       if (a0 + j >= count) break;
-      const double acc = sparse_chunk<N>(q, c0 + j, lane, lane_par, T, offL, nb0);
+      const double acc = sparse_chunk<N>(q, c0 + j, lane, lane_par, T, offL, nb0, dp->ends);
       const double part = wave_sum(lane_valid ? acc : 0.0);
       keep = (lane == j) ? part : keep;
     }
