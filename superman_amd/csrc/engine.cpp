@@ -345,6 +345,17 @@ static double walk_cost_eff(const Plan& P) {
   return P.kind == kWalkSeg ? walk_cost(P) * (1.0 - P.seg_skip) : walk_cost(P);
 }
 
+// SUP_NO_CHUNK_ENDS=1 (experiments, A/B): no chunk ends in the prefix-blocked
+// and exact walks (walk_sparse.hip); the sums are the same, the ended chunks'
+// terms being exact zeros.
+static bool no_chunk_ends() {
+  static const bool off = [] {
+    const char* e = std::getenv("SUP_NO_CHUNK_ENDS");
+    return e && std::atoi(e) != 0;
+  }();
+  return off;
+}
+
 int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const Layout& lay, Plan& P,
               const SegChoice* choice) {
   if (n < 1 || n > SUP_MAX_N) {
@@ -364,8 +375,10 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
   // ---- engine bit -> matrix column
   P.colmap.resize(nb);
   for (int e = 0; e < nb; ++e) P.colmap[e] = e;
-  const bool skip_order = kind == kWalkSkip && choice && m > 0;  // a searched SkipPer map (skip_walk_order)
-  if (!identity_map && (kind == kWalkSparse || kind == kWalkSeg || skip_order) && m > 0) {
+  // a caller-chosen walk + lane order: SkipPer's searched map (skip_walk_order),
+  // or the exact walk's chunk-end order (exact.cpp)
+  const bool given_order = (kind == kWalkSkip || kind == kWalkDense) && choice && m > 0;
+  if (!identity_map && (kind == kWalkSparse || kind == kWalkSeg || given_order) && m > 0) {
     // walk bits get the greedy prefix order (greedy_walk_order; the segmented
     // walk: seg_walk_order), lane bits the next L columns of that order, high
     // bits the rest in matrix order.
@@ -383,9 +396,9 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
       }
       return true;
     };
-    if (skip_order) {
+    if (given_order) {
       if (!valid_order(choice->order)) {
-        set_error("SkipPer column order: not m + L distinct flippable columns");
+        set_error("walk column order: not m + L distinct flippable columns");
         return SUP_EINVAL;
       }
       order = choice->order;
@@ -409,12 +422,12 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
     // 5 before: the top chunk bit alone decided skipping, half the shards had
     // nothing to walk at 2, 4 and 8 GPUs.)  Otherwise matrix order.
     std::vector<char> top(n, 0);
-    if (kind == kWalkSeg || skip_order) {
+    if (kind == kWalkSeg || given_order) {
       bool integral = true;
       for (size_t i = 0; i < (size_t)n * n && integral; ++i) integral = A[i] == std::floor(A[i]);
       // (SkipPer ends a chunk on a row no walk and no lane column touches)
       std::vector<char> wrow(n, 0);
-      for (int k = 0; k < (skip_order ? m + L : m); ++k)
+      for (int k = 0; k < (given_order ? m + L : m); ++k)
         for (int i = 0; i < n; ++i) wrow[i] |= A[(size_t)i * n + order[k]] != 0.0;
       for (int c = 0; c < nb && integral; ++c) {
         top[c] = 1;
@@ -490,7 +503,8 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
     P.rowmask[j] = rm;
     // a lane-uniform row no walk column touches is constant over a wave-chunk:
     // exactly zero at the chunk's first state, the chunk ends there (walk_sparse)
-    if (kind == kWalkSparse && !lane_touched && rm == 0) P.chunk_ends |= 1ull << j;
+    if ((kind == kWalkSparse || kind == kWalkDense) && !lane_touched && rm == 0 && !no_chunk_ends())
+      P.chunk_ends |= 1ull << j;
   }
   if (kind == kWalkSeg) return build_seg(P, choice ? choice->budget : 0);
   return SUP_OK;
@@ -1516,6 +1530,7 @@ int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1,
   p.n = P.n;
   p.counter = c->d_counter;
   p.group = 1;
+  p.umask = P.chunk_ends;  // walk_exact: its chunk-end rows (walk_sparse.hip's check)
   ExactParams e{};
   for (int q = 0; q < np; ++q) e.prime[q] = primes[q], e.pinv[q] = 1.0 / primes[q];
   e.nprimes = np;
@@ -1573,6 +1588,7 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
   WalkParams p{};
   p.cols = c->d_cols;
   p.x0 = c->d_x0dd;
+  p.umask = P.chunk_ends;  // walk_dd: its chunk-end rows
   p.chunk_begin = c0;
   p.chunk_count = count;
   p.L = P.lay.L;

@@ -448,6 +448,13 @@ void cpu_exact_range(const Plan& P, uint64_t c0, uint64_t c1, const std::vector<
       for (int q = 0; q < np; ++q) pinv[q] = 1.0 / primes[q];
       for (uint64_t a = w; a < count; a += (uint64_t)TH) {
         const uint64_t ga = c0 + a;
+        if (P.chunk_ends) {  // walk_exact's chunk end: a zero chunk-end row, every term zero
+          Lane s;
+          chunk_start(P, ga, 0, s);
+          bool end = false;
+          for (int j = 0; j < n && !end; ++j) end = ((P.chunk_ends >> j) & 1u) && s.x[j] == 0.0;
+          if (end) continue;
+        }
         for (unsigned l = 0; l < (1u << L); ++l) {
           Lane s;
           chunk_start(P, ga, l, s);

@@ -204,7 +204,13 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
   Plan P;
   std::vector<double> A2((size_t)n * n);
   for (size_t i = 0; i < A2.size(); ++i) A2[i] = 2.0 * A[i];
-  int rc = make_plan(A2.data(), n, kWalkDense, true, default_layout(n), P);
+  // walk + lane columns in the greedy prefix order (fewest rows touched): the
+  // rows none of them touches end the chunks where they are exactly zero
+  // (walk_exact.hip); any column order gives the same exact sum
+  const Layout lay = default_layout(n);
+  SegChoice order;
+  order.order = greedy_walk_order(A2.data(), n, lay.m + lay.L);
+  int rc = make_plan(A2.data(), n, kWalkDense, false, lay, P, lay.m > 0 ? &order : nullptr);
   if (rc) return rc;
   const uint64_t C = P.lay.chunks();
 

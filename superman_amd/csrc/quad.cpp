@@ -65,6 +65,11 @@ dd dd_chunk(const Plan& P, const std::vector<double>& x0dd, uint64_t ga) {
   const double* colL = P.cols.data() + (size_t)(2 * L) * NP;  // walk bit 0, + and - columns follow
   dd v[64];
   std::vector<dd> x(n);
+  if (P.chunk_ends) {  // walk_dd's chunk end: a zero chunk-end row, every term zero
+    dd_start(P, x0dd, ga, 0, x.data());
+    for (int r = 0; r < n; ++r)
+      if (((P.chunk_ends >> r) & 1u) && x[r].hi == 0.0) return dd{0.0, 0.0};
+  }
   for (uint32_t lane = 0; lane < 64; ++lane) {
     if (lane >= (1u << L)) {
       v[lane] = dd{0.0, 0.0};
@@ -130,7 +135,12 @@ void cpu_dd_range(const Plan& P, const std::vector<double>& x0dd, uint64_t c0, u
 int quad_perman(const double* A, int n, const sup_opts& o, bool on_cpu, double* hi, double* lo, double* kernel_ms,
                 int* devices_used) {
   Plan P;
-  int rc = make_plan(A, n, kWalkDense, true, default_layout(n), P);
+  // walk + lane columns in the greedy prefix order (fewest rows touched): the
+  // rows none of them touches end the chunks where they are exactly zero
+  const Layout lay = default_layout(n);
+  SegChoice order;
+  order.order = greedy_walk_order(A, n, lay.m + lay.L);
+  int rc = make_plan(A, n, kWalkDense, false, lay, P, lay.m > 0 ? &order : nullptr);
   if (rc) return rc;
   // Nijenhuis-Wilf start vector in double-double (rows in engine order)
   std::vector<double> x0dd(2 * (size_t)P.NP, 0.0);

@@ -15,9 +15,14 @@
 // partials in a fixed pairwise order (quad.cpp), and quad.cpp's host twin runs
 // the same dd.hpp operations in the same order: results are bit-identical on
 // the GPU, on any device count and on host threads.
+// Chunk ends (round 5, walk_sparse.hip's check): a lane-uniform row that no
+// walk column touches (WalkParams::umask; quad.cpp orders the columns to leave
+// many) and is exactly zero at a chunk's first state makes every term of the
+// chunk zero; the chunk's part is (0, 0) without walking it.
 #include "dd.hpp"
 #include "kernels.hpp"
 #include "walk_common.hpp"
+#include "walk_zero.hpp"
 
 namespace sup {
 
@@ -110,6 +115,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N <= 40 
           const bool on = (lane >> e) & 1u;
 #pragma unroll
           for (int r = 0; r < N; ++r) x[r] = dd_add_d(x[r], on ? col[r] : 0.0);
+        }
+      }
+      {
+        double h[N];  // a normalised double-double is zero iff its high part is
+#pragma unroll
+        for (int r = 0; r < N; ++r) h[r] = x[r].hi;
+        if (zero_rows<N>(h) & SUP_KARG(umask)) {  // chunk end: every term exactly zero
+          if (lane == j) keep = dd{0.0, 0.0};
+          continue;
         }
       }
       dd acc = dd_prod4<N>(x);  // t = 0

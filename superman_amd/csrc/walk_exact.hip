@@ -13,8 +13,13 @@
 //   T = sum_i (-1)^i prod_j X_j(gray(i)) = 2^(n-1) perm / (2 - 4(n&1)).
 // The reference computes the same sum in fp64 (its -b / int path); this path
 // is exact, so it equals every exact reference result bit for bit.
+// Chunk ends (round 5): X holds exact integers, so a lane-uniform row that no
+// walk column touches (WalkParams::umask, exact.cpp's column order chosen to
+// leave many) and is exactly zero at a chunk's first state makes every term of
+// the chunk zero; the chunk is not walked (walk_sparse.hip's check).
 #include "kernels.hpp"
 #include "walk_common.hpp"
+#include "walk_zero.hpp"
 
 namespace sup {
 
@@ -72,6 +77,7 @@ __global__ __launch_bounds__(kBlock) void walk_exact(WalkParams p, ExactParams e
     const uint64_t ga = p.chunk_begin + g;
     double x[N];
     chunk_start<N>(x, p, ga, lane);
+    if (zero_rows<N>(x) & SUP_KARG(umask)) continue;  // chunk end: every term exactly zero
     double acc[kMaxPrimes], y[K];
     group_products<N, G>(x, y);
 #pragma unroll
