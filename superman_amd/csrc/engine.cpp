@@ -1493,7 +1493,10 @@ int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1,
   res.assign(np, 0);
   if (kernel_ms) *kernel_ms = 0.0;
   if (c1 <= c0) return SUP_OK;
-  if (np < 1 || np > kMaxPrimes || P.kind != kWalkDense || c1 > P.lay.chunks()) {
+  // group 1, 2, 4: the dense kernel on a dense plan; 8 + g: the prefix-blocked
+  // kernel on a prefix-blocked plan (walk_exact.hip)
+  const bool blocked = (group & 8) != 0;
+  if (np < 1 || np > kMaxPrimes || P.kind != (blocked ? kWalkSparse : kWalkDense) || c1 > P.lay.chunks()) {
     set_error("run_range_exact: bad request");
     return SUP_EINVAL;
   }
@@ -1531,6 +1534,12 @@ int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1,
   p.counter = c->d_counter;
   p.group = 1;
   p.umask = P.chunk_ends;  // walk_exact: its chunk-end rows (walk_sparse.hip's check)
+  p.nb_lo = p.nb_hi = 0;
+  for (int k = 0; blocked && k < P.lay.m && k < 32; ++k) {  // walk_exact_blocked: nblk of walk bit k
+    const uint64_t v = (uint64_t)(P.nblk[P.lay.L + k] & 15);
+    if (k < 16) p.nb_lo |= v << (4 * k);
+    else p.nb_hi |= v << (4 * (k - 16));
+  }
   ExactParams e{};
   for (int q = 0; q < np; ++q) e.prime[q] = primes[q], e.pinv[q] = 1.0 / primes[q];
   e.nprimes = np;

@@ -204,13 +204,23 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
   Plan P;
   std::vector<double> A2((size_t)n * n);
   for (size_t i = 0; i < A2.size(); ++i) A2[i] = 2.0 * A[i];
-  // walk + lane columns in the greedy prefix order (fewest rows touched): the
-  // rows none of them touches end the chunks where they are exactly zero
-  // (walk_exact.hip); any column order gives the same exact sum
+  // The prefix-blocked walk (walk_exact_blocked: rows in first-touch order,
+  // only the flipped column's leading 8-row blocks re-formed) when its cost
+  // model beats the dense walk's, as plan_for decides for the fp64 walks;
+  // else the dense walk with its walk + lane columns in the greedy prefix
+  // order.  Either way the rows no walk or lane column touches end the chunks
+  // where they are exactly zero (walk_exact.hip), and any column order gives
+  // the same exact sum.
   const Layout lay = default_layout(n);
-  SegChoice order;
-  order.order = greedy_walk_order(A2.data(), n, lay.m + lay.L);
-  int rc = make_plan(A2.data(), n, kWalkDense, false, lay, P, lay.m > 0 ? &order : nullptr);
+  int rc = SUP_OK;
+  if (lay.m > 0 && (rc = make_plan(A2.data(), n, kWalkSparse, false, lay, P)) == SUP_OK &&
+      walk_cost(P) < 2.0 * n + 1.0) {
+    group |= 8;  // run_range_exact / walk_exact.hip: the blocked kernel
+  } else {
+    SegChoice order;
+    order.order = greedy_walk_order(A2.data(), n, lay.m + lay.L);
+    rc = make_plan(A2.data(), n, kWalkDense, false, lay, P, lay.m > 0 ? &order : nullptr);
+  }
   if (rc) return rc;
   const uint64_t C = P.lay.chunks();
 

@@ -124,12 +124,116 @@ __global__ __launch_bounds__(kBlock) void walk_exact(WalkParams p, ExactParams e
     }
 }
 
+// Prefix-blocked form (round 5; walk_sparse.hip's structure in residues): rows
+// in first-touch order over the walk columns (make_plan, kind kWalkSparse), so
+// flipping walk column k changes only the nblk[k] leading 8-row blocks.  Per
+// prime, R[b] = prod of the rows of blocks >= b mod p (R[NB] = 1), re-formed
+// for the changed blocks only, top block first: R[b] = chain of block b's
+// exact group products starting from R[b + 1].  Every value is an exact
+// residue, so the sums equal the dense walk's residue for residue.
+template <int N, int G>
+__device__ __forceinline__ double block_chain(const double (&x)[N], int b, double r, double p, double pinv) {
+  // block b's rows in groups of G (exact products), each folded into r
+#pragma unroll
+  for (int j0 = 0; j0 < 8; j0 += G) {
+    const int r0 = 8 * b + j0;
+    if (r0 < N) {
+      double y = x[r0];
+#pragma unroll
+      for (int i = 1; i < G; ++i)
+        if (r0 + i < N && j0 + i < 8) y *= x[(r0 + i < N) ? r0 + i : 0];
+      r = red(r * y, p, pinv);
+    }
+  }
+  return r;
+}
+
+template <int N, int G>
+__global__ __launch_bounds__(kBlock) void walk_exact_blocked(WalkParams p, ExactParams e) {
+  constexpr int NP = pad8(N);
+  constexpr int NB = Blocks<N>::NB;
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool lane_valid = lane < (1u << p.L);
+  const uint32_t lane_par = __builtin_popcount(lane) & 1u;
+  const uint32_t T = 1u << p.m;
+  const uint32_t offL = 2u * (uint32_t)p.L * NP * 8u;
+
+  double tot[kMaxPrimes];
+#pragma unroll
+  for (int q = 0; q < kMaxPrimes; ++q) tot[q] = 0.0;
+
+  for (uint32_t g = next_chunk(p.counter); (uint64_t)g < p.chunk_count; g = next_chunk(p.counter)) {
+    const uint64_t ga = p.chunk_begin + g;
+    double x[N];
+    chunk_start<N>(x, p, ga, lane);
+    if (zero_rows<N>(x) & SUP_KARG(umask)) continue;  // chunk end: every term exactly zero
+    double R[kMaxPrimes][NB + 1], acc[kMaxPrimes];
+#pragma unroll
+    for (int q = 0; q < kMaxPrimes; ++q)
+      if (q < e.nprimes) {
+        R[q][NB] = 1.0;
+#pragma unroll
+        for (int b = NB - 1; b >= 0; --b) R[q][b] = block_chain<N, G>(x, b, R[q][b + 1], e.prime[q], e.pinv[q]);
+        acc[q] = R[q][0];
+      }
+    for (uint32_t t = 1; t < T; ++t) {
+      const uint32_t k = (uint32_t)__builtin_ctz(t);
+      const uint32_t neg = (t >> (k + 1)) & 1u;
+      const int nb = nb_of(p, k);
+      cdbl* col = opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u);
+#pragma unroll
+      for (int b = NB - 1; b >= 0; --b)
+        if (b < nb) {
+#pragma unroll
+          for (int j = 8 * b; j < 8 * b + 8 && j < N; ++j) x[j] += col[j];
+        }
+      const bool odd = t & 1u;
+#pragma unroll
+      for (int q = 0; q < kMaxPrimes; ++q)
+        if (q < e.nprimes) {
+#pragma unroll
+          for (int b = NB - 1; b >= 0; --b)
+            if (b < nb) R[q][b] = block_chain<N, G>(x, b, R[q][b + 1], e.prime[q], e.pinv[q]);
+          acc[q] = odd ? acc[q] - R[q][0] : acc[q] + R[q][0];
+          if ((t & 255u) == 0u) acc[q] = red(acc[q], e.prime[q], e.pinv[q]);
+        }
+    }
+    const bool flip = ((uint32_t)ga ^ lane_par) & 1u;
+#pragma unroll
+    for (int q = 0; q < kMaxPrimes; ++q)
+      if (q < e.nprimes) {
+        const double a = red(acc[q], e.prime[q], e.pinv[q]);
+        tot[q] = red(tot[q] + (lane_valid ? (flip ? -a : a) : 0.0), e.prime[q], e.pinv[q]);
+      }
+  }
+  const uint32_t wave = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+#pragma unroll
+  for (int q = 0; q < kMaxPrimes; ++q)
+    if (q < e.nprimes) {
+      double v = tot[q];
+#pragma unroll
+      for (int off = 1; off <= 32; off <<= 1) v += __shfl_xor(v, off, 64);
+      double r = red(v, e.prime[q], e.pinv[q]);
+      if (r < 0.0) r += e.prime[q];
+      if (r < 0.0) r += e.prime[q];
+      if (r >= e.prime[q]) r -= e.prime[q];
+      if (lane == 0) e.wave_out[(uint64_t)wave * kMaxPrimes + q] = r;
+    }
+}
+
+// g = 1, 2, 4: the dense walk with groups of g; 8 + g: the prefix-blocked walk
 template <int N, int HI>
 static hipError_t launch_rec(int n, int g, const WalkParams& p, const ExactParams& e, int grid, hipStream_t s) {
   if (n == N) {
-    if (g == 4) hipLaunchKernelGGL((walk_exact<N, 4>), dim3(grid), dim3(kBlock), 0, s, p, e);
-    else if (g == 2) hipLaunchKernelGGL((walk_exact<N, 2>), dim3(grid), dim3(kBlock), 0, s, p, e);
-    else hipLaunchKernelGGL((walk_exact<N, 1>), dim3(grid), dim3(kBlock), 0, s, p, e);
+    switch (g) {
+      case 4: hipLaunchKernelGGL((walk_exact<N, 4>), dim3(grid), dim3(kBlock), 0, s, p, e); break;
+      case 2: hipLaunchKernelGGL((walk_exact<N, 2>), dim3(grid), dim3(kBlock), 0, s, p, e); break;
+      case 1: hipLaunchKernelGGL((walk_exact<N, 1>), dim3(grid), dim3(kBlock), 0, s, p, e); break;
+      case 12: hipLaunchKernelGGL((walk_exact_blocked<N, 4>), dim3(grid), dim3(kBlock), 0, s, p, e); break;
+      case 10: hipLaunchKernelGGL((walk_exact_blocked<N, 2>), dim3(grid), dim3(kBlock), 0, s, p, e); break;
+      case 9: hipLaunchKernelGGL((walk_exact_blocked<N, 1>), dim3(grid), dim3(kBlock), 0, s, p, e); break;
+      default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
   }
   if constexpr (N < HI) return launch_rec<N + 1, HI>(n, g, p, e, grid, s);
@@ -139,9 +243,15 @@ static hipError_t launch_rec(int n, int g, const WalkParams& p, const ExactParam
 template <int N, int HI>
 static hipError_t occ_rec(int n, int g, int* blocks_per_cu) {
   if (n == N) {
-    if (g == 4) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact<N, 4>, kBlock, 0);
-    if (g == 2) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact<N, 2>, kBlock, 0);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact<N, 1>, kBlock, 0);
+    switch (g) {
+      case 4: return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact<N, 4>, kBlock, 0);
+      case 2: return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact<N, 2>, kBlock, 0);
+      case 1: return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact<N, 1>, kBlock, 0);
+      case 12: return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact_blocked<N, 4>, kBlock, 0);
+      case 10: return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact_blocked<N, 2>, kBlock, 0);
+      case 9: return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_exact_blocked<N, 1>, kBlock, 0);
+      default: return hipErrorInvalidValue;
+    }
   }
   if constexpr (N < HI) return occ_rec<N + 1, HI>(n, g, blocks_per_cu);
   return hipErrorInvalidValue;
