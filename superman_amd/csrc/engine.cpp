@@ -1567,7 +1567,8 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
                  double* parts, double* kernel_ms) {
   if (kernel_ms) *kernel_ms = 0.0;
   if (c1 <= c0) return SUP_OK;
-  if (P.kind != kWalkDense || c1 > P.lay.chunks() || x0dd.size() != 2 * (size_t)P.NP) {
+  const bool blocked = P.kind == kWalkSparse;  // walk_dd_blocked; else the dense walk_dd
+  if ((P.kind != kWalkDense && !blocked) || c1 > P.lay.chunks() || x0dd.size() != 2 * (size_t)P.NP) {
     set_error("run_range_dd: bad request");
     return SUP_EINVAL;
   }
@@ -1578,7 +1579,7 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
   SUP_HIP(select_device(c->dev));
   SUP_ON_DEVICE(c->dev, "device buffers");
   int occ = 0;
-  SUP_HIP(dd_occupancy(P.n, &occ));
+  SUP_HIP(blocked ? dd_blocked_occupancy(P.n, &occ) : dd_occupancy(P.n, &occ));
   if (occ < 1) occ = 1;
   const uint64_t count = c1 - c0;
   uint64_t grid = (uint64_t)c->cus * (uint64_t)occ;
@@ -1606,9 +1607,15 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
   p.chunk_out = c->d_chunk;
   p.counter = c->d_counter;
   p.group = 1;
+  p.nb_lo = p.nb_hi = 0;
+  for (int k = 0; blocked && k < P.lay.m && k < 32; ++k) {  // walk_dd_blocked: nblk of walk bit k
+    const uint64_t v = (uint64_t)(P.nblk[P.lay.L + k] & 15);
+    if (k < 16) p.nb_lo |= v << (4 * k);
+    else p.nb_hi |= v << (4 * (k - 16));
+  }
   SUP_HIP(hipEventRecord(c->ev0, s));
   SUP_ON_DEVICE(c->dev, "double-double walk launch");
-  SUP_HIP(launch_dd(P.n, p, (int)grid, s));
+  SUP_HIP(blocked ? launch_dd_blocked(P.n, p, (int)grid, s) : launch_dd(P.n, p, (int)grid, s));
   SUP_HIP(hipEventRecord(c->ev1, s));
   SUP_HIP(hipMemcpyAsync(parts, c->d_chunk, 2 * count * sizeof(double), hipMemcpyDeviceToHost, s));
   SUP_HIP(hipStreamSynchronize(s));

@@ -62,6 +62,14 @@ SUP_DECL_DD(17)
 SUP_DECL_DD(33)
 SUP_DECL_DD(49)
 #undef SUP_DECL_DD
+#define SUP_DECL_DDB(LO)                                                                  \
+  hipError_t launch_ddblocked_##LO(int n, const WalkParams& p, int grid, hipStream_t s);  \
+  hipError_t occupancy_ddblocked_##LO(int n, int* blocks_per_cu);
+SUP_DECL_DDB(1)
+SUP_DECL_DDB(17)
+SUP_DECL_DDB(33)
+SUP_DECL_DDB(49)
+#undef SUP_DECL_DDB
 #define SUP_DECL_LDS(LO)                                                                   \
   hipError_t launch_lds_##LO(int n, const WalkParams& p, int grid, hipStream_t s);        \
   hipError_t occupancy_lds_##LO(int n, int m, int* blocks_per_cu);
@@ -98,6 +106,9 @@ hipError_t exact_occupancy(int n, int g, int* blocks_per_cu);
 // p.chunk_out = 2 doubles (hi, lo) per wave-chunk.
 hipError_t launch_dd(int n, const WalkParams& p, int grid, hipStream_t s);
 hipError_t dd_occupancy(int n, int* blocks_per_cu);
+// Its prefix-blocked form (walk_dd_blocked, a kWalkSparse plan: p.nb_lo / nb_hi).
+hipError_t launch_dd_blocked(int n, const WalkParams& p, int grid, hipStream_t s);
+hipError_t dd_blocked_occupancy(int n, int* blocks_per_cu);
 
 // Fixed-order pairwise reduction of `count` doubles into *out (64-way passes,
 // zero padded; mirrored by oracle/oracle.c orc_pairwise_reduce).  `scratch`

@@ -58,6 +58,13 @@ void dd_add_colv(dd* x, const double* col, int n) {
   for (int r = 0; r < n; ++r) x[r] = dd_add_d(x[r], col[r]);
 }
 
+// walk_dd_blocked's block product: ((x0 x1)(x2 x3))((x4 x5)(x6 x7)), rows
+// past n = 1.
+dd dd_bprod8(const dd* x, int n, int b) {
+  auto v = [&](int i) { return 8 * b + i < n ? x[8 * b + i] : dd{1.0, 0.0}; };
+  return dd_mul(dd_mul(dd_mul(v(0), v(1)), dd_mul(v(2), v(3))), dd_mul(dd_mul(v(4), v(5)), dd_mul(v(6), v(7))));
+}
+
 // One wave-chunk, every lane, then the 64-lane xor butterfly (dd_wave_sum).
 dd dd_chunk(const Plan& P, const std::vector<double>& x0dd, uint64_t ga) {
   const int n = P.n, NP = P.NP, L = P.lay.L;
@@ -76,6 +83,28 @@ dd dd_chunk(const Plan& P, const std::vector<double>& x0dd, uint64_t ga) {
       continue;
     }
     dd_start(P, x0dd, ga, lane, x.data());
+    if (P.kind == kWalkSparse) {  // walk_dd_blocked: suffix products of 8-row blocks
+      const int NB = (n + 7) / 8;
+      std::vector<dd> U(NB + 1);
+      U[NB] = dd{1.0, 0.0};
+      for (int b = NB - 1; b >= 0; --b) U[b] = dd_mul(dd_bprod8(x.data(), n, b), U[b + 1]);
+      dd acc = U[0];
+      for (uint32_t t = 1; t < T; ++t) {
+        const uint32_t k = (uint32_t)__builtin_ctz(t);
+        const uint32_t neg = (t >> (k + 1)) & 1u;
+        const double* col = colL + (size_t)(2u * k + neg) * NP;
+        const int nb = P.nblk[L + k];
+        for (int b = nb - 1; b >= 0; --b) {  // top block first (deeper blocks' U current)
+          for (int j = 8 * b; j < 8 * b + 8 && j < n; ++j) x[j] = dd_add_d(x[j], col[j]);
+          U[b] = dd_mul(dd_bprod8(x.data(), n, b), U[b + 1]);
+        }
+        acc = dd_add(acc, (t & 1u) ? dd_neg(U[0]) : U[0]);
+      }
+      const uint32_t lane_par = __builtin_popcount(lane) & 1u;
+      if (((uint32_t)ga ^ lane_par) & 1u) acc = dd_neg(acc);
+      v[lane] = acc;
+      continue;
+    }
     dd acc = dd_prod(x.data(), n);
     uint32_t t = 1;
     for (; t + 1 < T; t += 2) {
@@ -135,12 +164,23 @@ void cpu_dd_range(const Plan& P, const std::vector<double>& x0dd, uint64_t c0, u
 int quad_perman(const double* A, int n, const sup_opts& o, bool on_cpu, double* hi, double* lo, double* kernel_ms,
                 int* devices_used) {
   Plan P;
-  // walk + lane columns in the greedy prefix order (fewest rows touched): the
-  // rows none of them touches end the chunks where they are exactly zero
+  // The prefix-blocked walk (walk_dd_blocked) when its cost model beats the
+  // dense walk's, else the dense walk with its walk + lane columns in the
+  // greedy prefix order; the rows none of them touches end the chunks where
+  // they are exactly zero.  Above n = 28 the blocked kernel's suffix products
+  // do not fit two waves per SIMD (1 wave: 268 VGPRs at n = 30), so it must
+  // save more: measured (profiles/r5/probe_quad_blocked.log) the bench matrix
+  // (n = 40, modelled 45.5 against 81 ops) ran 12.0 s blocked against 9.9 s
+  // dense, d = 0.2 and dwt_59's n = 30 leaves (~0.25-0.3 of the dense ops)
+  // faster blocked.
   const Layout lay = default_layout(n);
-  SegChoice order;
-  order.order = greedy_walk_order(A, n, lay.m + lay.L);
-  int rc = make_plan(A, n, kWalkDense, false, lay, P, lay.m > 0 ? &order : nullptr);
+  const double bar = (n <= 28 ? 1.0 : 0.4) * (2.0 * n + 1.0);
+  int rc = SUP_OK;
+  if (!(lay.m > 0 && (rc = make_plan(A, n, kWalkSparse, false, lay, P)) == SUP_OK && walk_cost(P) < bar)) {
+    SegChoice order;
+    order.order = greedy_walk_order(A, n, lay.m + lay.L);
+    rc = make_plan(A, n, kWalkDense, false, lay, P, lay.m > 0 ? &order : nullptr);
+  }
   if (rc) return rc;
   // Nijenhuis-Wilf start vector in double-double (rows in engine order)
   std::vector<double> x0dd(2 * (size_t)P.NP, 0.0);

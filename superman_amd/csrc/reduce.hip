@@ -247,6 +247,16 @@ hipError_t dd_occupancy(int n, int* blocks_per_cu) {
   SUP_DISPATCH(dd, occupancy, n, blocks_per_cu)
 }
 
+hipError_t launch_dd_blocked(int n, const WalkParams& p, int grid, hipStream_t s) {
+  if (n < 1 || n > 64) return hipErrorInvalidValue;
+  SUP_DISPATCH(ddblocked, launch, n, p, grid, s)
+}
+
+hipError_t dd_blocked_occupancy(int n, int* blocks_per_cu) {
+  if (n < 1 || n > 64) return hipErrorInvalidValue;
+  SUP_DISPATCH(ddblocked, occupancy, n, blocks_per_cu)
+}
+
 hipError_t exact_occupancy(int n, int g, int* blocks_per_cu) {
   if (n < 1 || n > 64) return hipErrorInvalidValue;
   SUP_DISPATCH(exact, occupancy, n, g, blocks_per_cu)

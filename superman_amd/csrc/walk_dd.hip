@@ -154,6 +154,108 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N <= 40 
   }
 }
 
+// Prefix-blocked form (round 5; walk_sparse.hip's structure in
+// double-double): rows in first-touch order over the walk columns (make_plan,
+// kind kWalkSparse), x in 8-row blocks with suffix products U[b] = prod of the
+// rows of blocks >= b (U[NB] = 1); flipping walk column k adds it to the
+// nblk[k] leading blocks and re-forms their U top block first, block b as
+// ((x0 x1)(x2 x3))((x4 x5)(x6 x7)) times U[b + 1].  quad.cpp's host twin runs
+// the same operations in the same order.
+template <int N, int B>
+__device__ __forceinline__ dd dd_bprod8(const dd (&x)[N]) {
+  const dd one{1.0, 0.0};
+  auto v = [&](int i) -> dd { return (8 * B + i < N) ? x[(8 * B + i < N) ? 8 * B + i : 0] : one; };
+  return dd_mul(dd_mul(dd_mul(v(0), v(1)), dd_mul(v(2), v(3))), dd_mul(dd_mul(v(4), v(5)), dd_mul(v(6), v(7))));
+}
+
+template <int N, int B>
+__device__ __forceinline__ void dd_blk_step(dd (&x)[N], dd (&U)[Blocks<N>::NB + 1], cdbl* col, int nb) {
+  constexpr int NB = Blocks<N>::NB;
+  if constexpr (B < NB) {
+    if (nb > B) {
+      dd_blk_step<N, B + 1>(x, U, col, nb);  // deeper blocks first: U[B + 1] is current below
+#pragma unroll
+      for (int j = 8 * B; j < 8 * B + 8 && j < N; ++j) x[j] = dd_add_d(x[j], col[j]);
+      U[B] = dd_mul(dd_bprod8<N, B>(x), U[B + 1]);
+    }
+  }
+}
+
+template <int N, int B>
+__device__ __forceinline__ void dd_suffix_all(const dd (&x)[N], dd (&U)[Blocks<N>::NB + 1]) {
+  if constexpr (B >= 0) {
+    U[B] = dd_mul(dd_bprod8<N, B>(x), U[B + 1]);
+    dd_suffix_all<N, B - 1>(x, U);
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N <= 28 ? 2 : 1))) void walk_dd_blocked(
+    WalkParams p) {
+  constexpr int NP = pad8(N);
+  constexpr int NB = Blocks<N>::NB;
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool lane_valid = lane < (1u << p.L);
+  const uint32_t lane_par = __builtin_popcount(lane) & 1u;
+  const uint32_t T = 1u << p.m;
+  const uint32_t offL = 2u * (uint32_t)p.L * NP * 8u;
+
+  for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {
+    dd keep{0.0, 0.0};
+    for (uint32_t j = 0; j < (uint32_t)p.group; ++j) {
+      const uint64_t a = (uint64_t)g * p.group + j;
+      if (a >= p.chunk_count) break;
+      const uint64_t ga = p.chunk_begin + a;
+      dd x[N];
+      {
+        cdbl* x0 = opaque_c(p.x0, 0);
+#pragma unroll
+        for (int r = 0; r < N; ++r) x[r] = dd{x0[r], x0[NP + r]};
+        uint64_t h = ga ^ (ga >> 1);
+        const uint32_t hb = (uint32_t)(p.L + p.m);
+        while (h) {
+          const uint32_t b = (uint32_t)__builtin_ctzll(h);
+          h &= h - 1;
+          dd_add_col<N>(x, opaque_c(p.cols, (2u * (hb + b)) * NP * 8u));
+        }
+        for (int e = 0; e < p.L; ++e) {
+          cdbl* col = opaque_c(p.cols, (2u * e) * NP * 8u);
+          const bool on = (lane >> e) & 1u;
+#pragma unroll
+          for (int r = 0; r < N; ++r) x[r] = dd_add_d(x[r], on ? col[r] : 0.0);
+        }
+      }
+      {
+        double h[N];
+#pragma unroll
+        for (int r = 0; r < N; ++r) h[r] = x[r].hi;
+        if (zero_rows<N>(h) & SUP_KARG(umask)) {  // chunk end: every term exactly zero
+          if (lane == j) keep = dd{0.0, 0.0};
+          continue;
+        }
+      }
+      dd U[NB + 1];
+      U[NB] = dd{1.0, 0.0};
+      dd_suffix_all<N, NB - 1>(x, U);
+      dd acc = U[0];  // t = 0
+      for (uint32_t t = 1; t < T; ++t) {
+        const uint32_t k = (uint32_t)__builtin_ctz(t);
+        const uint32_t neg = (t >> (k + 1)) & 1u;
+        dd_blk_step<N, 0>(x, U, opaque_c(p.cols, offL + (2u * k + neg) * NP * 8u), nb_of(p, k));
+        acc = dd_add(acc, (t & 1u) ? dd_neg(U[0]) : U[0]);
+      }
+      if (((uint32_t)ga ^ lane_par) & 1u) acc = dd_neg(acc);
+      const dd part = dd_wave_sum(lane_valid ? acc : dd{0.0, 0.0});
+      if (lane == j) keep = part;
+    }
+    const uint64_t a = (uint64_t)g * p.group + lane;
+    if (lane < (uint32_t)p.group && a < p.chunk_count) {
+      p.chunk_out[2 * a] = keep.hi;
+      p.chunk_out[2 * a + 1] = keep.lo;
+    }
+  }
+}
+
 template <int N, int HI>
 static hipError_t launch_rec(int n, const WalkParams& p, int grid, hipStream_t s) {
   if (n == N) {
@@ -171,8 +273,32 @@ static hipError_t occ_rec(int n, int* blocks_per_cu) {
   return hipErrorInvalidValue;
 }
 
+template <int N, int HI>
+static hipError_t launch_blocked_rec(int n, const WalkParams& p, int grid, hipStream_t s) {
+  if (n == N) {
+    hipLaunchKernelGGL(walk_dd_blocked<N>, dim3(grid), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
+  }
+  if constexpr (N < HI) return launch_blocked_rec<N + 1, HI>(n, p, grid, s);
+  return hipErrorInvalidValue;
+}
+
+template <int N, int HI>
+static hipError_t occ_blocked_rec(int n, int* blocks_per_cu) {
+  if (n == N) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_dd_blocked<N>, kBlock, 0);
+  if constexpr (N < HI) return occ_blocked_rec<N + 1, HI>(n, blocks_per_cu);
+  return hipErrorInvalidValue;
+}
+
 #define SUP_CAT2(a, b) a##b
 #define SUP_CAT(a, b) SUP_CAT2(a, b)
+
+hipError_t SUP_CAT(launch_ddblocked_, SUP_N_LO)(int n, const WalkParams& p, int grid, hipStream_t s) {
+  return launch_blocked_rec<SUP_N_LO, SUP_N_HI>(n, p, grid, s);
+}
+hipError_t SUP_CAT(occupancy_ddblocked_, SUP_N_LO)(int n, int* blocks_per_cu) {
+  return occ_blocked_rec<SUP_N_LO, SUP_N_HI>(n, blocks_per_cu);
+}
 
 hipError_t SUP_CAT(launch_dd_, SUP_N_LO)(int n, const WalkParams& p, int grid, hipStream_t s) {
   return launch_rec<SUP_N_LO, SUP_N_HI>(n, p, grid, s);
