@@ -233,7 +233,8 @@ struct SkipOrderEval {
 // each start takes kRounds random moves (swap a walk or lane column with an
 // unused one, or a walk with a lane column), keeping improvements on a
 // 512-sample estimate; the best end on 8192 samples wins.
-bool skip_walk_order(const double* A, int n, const Layout& lay, std::vector<int>& out) {
+bool skip_walk_order(const double* A, int n, const Layout& lay, std::vector<int>& out,
+                     const std::vector<int>* baseline, double factor) {
   const int nb = n - 1, m = lay.m, L = lay.L;
   if (m < 3 || m + L >= nb) return false;
   SkipOrderEval E{A, n, m, L, std::vector<uint64_t>(nb, 0), std::vector<double>(n)};
@@ -322,13 +323,38 @@ bool skip_walk_order(const double* A, int n, const Layout& lay, std::vector<int>
   size_t bi = 0;
   for (size_t i = 1; i < ends.size(); ++i)
     if (effs[i] < effs[bi] - 1e-12) bi = i;
-  const double e_ident = E.eff(ident, kFinal);
+  const std::vector<int>& base = baseline && (int)baseline->size() == m + L ? *baseline : ident;
+  const double e_base = E.eff(base, kFinal);
   if (std::getenv("SUP_JIT_VERBOSE"))
-    std::fprintf(stderr, "skip column search n=%d: best eff %.4f (cost %.3f, kill %.3f) vs SkipOrder's %.4f\n", n,
-                 effs[bi], E.prefix_cost(ends[bi]), E.kill(ends[bi], kFinal), e_ident);
-  if (!(effs[bi] < 0.5 * e_ident)) return false;
+    std::fprintf(stderr, "chunk-end column search n=%d: best eff %.4f (cost %.3f, kill %.3f) vs the baseline's %.4f\n",
+                 n, effs[bi], E.prefix_cost(ends[bi]), E.kill(ends[bi], kFinal), e_base);
+  if (!(effs[bi] < factor * e_base)) return false;
   out = ends[bi];
   return true;
+}
+
+// A prefix-blocked plan of an integer matrix whose walk is predicted to take
+// >= kChunkEndSearchSec (every state, walk_cost's ops): its walk + lane columns
+// searched for chunk ends (skip_walk_order against its greedy order; taken when
+// it cuts ops x chunks walked by 10 %).  Deterministic, from the matrix alone.
+static constexpr double kChunkEndSearchSec = 4.0;
+// fp64 VALU lane-ops per second of one MI355X on the walk kernels (measured:
+// 46.6 ops/step at 7.98e11 steps/s on the n=40 bench), for the planners' time
+// predictions (this search, SkipPer's, jit's auto mode).
+static constexpr double kLaneOpsPerSec = 3.7e13;
+int improve_sparse_plan(const double* A, int n, const Layout& lay, Plan& P) {
+  if (P.kind != kWalkSparse || !P.integral || lay.m < 3 ||
+      std::ldexp(1.0, n - 1) * walk_cost(P) / kLaneOpsPerSec < kChunkEndSearchSec)
+    return SUP_OK;
+  std::vector<int> base;
+  for (int k = 0; k < lay.m; ++k) base.push_back(P.colmap[lay.L + k]);
+  for (int e = 0; e < lay.L; ++e) base.push_back(P.colmap[e]);
+  SegChoice c;
+  if (!skip_walk_order(A, n, lay, c.order, &base, 0.9)) return SUP_OK;
+  Plan Q;
+  const int rc = make_plan(A, n, kWalkSparse, false, lay, Q, &c);
+  if (rc == SUP_OK) P = std::move(Q);
+  return rc;
 }
 
 double walk_cost(const Plan& P) {
@@ -375,9 +401,10 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
   // ---- engine bit -> matrix column
   P.colmap.resize(nb);
   for (int e = 0; e < nb; ++e) P.colmap[e] = e;
-  // a caller-chosen walk + lane order: SkipPer's searched map (skip_walk_order),
-  // or the exact walk's chunk-end order (exact.cpp)
-  const bool given_order = (kind == kWalkSkip || kind == kWalkDense) && choice && m > 0;
+  // a caller-chosen walk + lane order: a map searched for chunk ends
+  // (skip_walk_order: SkipPer, and long prefix-blocked / exact / double-double
+  // walks of integer matrices), or the exact walk's greedy order (exact.cpp)
+  const bool given_order = (kind == kWalkSkip || kind == kWalkDense || kind == kWalkSparse) && choice && m > 0;
   if (!identity_map && (kind == kWalkSparse || kind == kWalkSeg || given_order) && m > 0) {
     // walk bits get the greedy prefix order (greedy_walk_order; the segmented
     // walk: seg_walk_order), lane bits the next L columns of that order, high
@@ -510,9 +537,6 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
   return SUP_OK;
 }
 
-// fp64 VALU lane-ops per second of one MI355X on the walk kernels (measured:
-// 46.6 ops/step at 7.98e11 steps/s on the n=40 bench), for jit's auto mode.
-static constexpr double kLaneOpsPerSec = 3.7e13;
 // Auto mode's bar where nothing bounds the saving (orders below
 // kJitWarmMinN; jit != 0 never asks): no walk that short repays a plan.
 static constexpr double kJitMinSavingSec = 3.0;
@@ -853,7 +877,7 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
           std::ldexp(1.0, n - 1) * walk_cost(P) / (kSkipEfficiency * kLaneOpsPerSec) >= kSkipSearchMinSec) {
         SegChoice c;
         Plan Q;
-        if (skip_walk_order(A, n, lay, c.order) && make_plan(A, n, kWalkSkip, false, lay, Q, &c) == SUP_OK)
+        if (skip_walk_order(A, n, lay, c.order, nullptr, 0.5) && make_plan(A, n, kWalkSkip, false, lay, Q, &c) == SUP_OK)
           P = std::move(Q);
       }
       if (jit < 0 || n < 10 || lay.m < 3) return SUP_OK;
@@ -908,10 +932,13 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
   }
   Plan best;
   int rc = make_plan(A, n, kinds[0], false, lay, best);
+  if (rc == SUP_OK && kinds[0] == kWalkSparse) rc = improve_sparse_plan(A, n, lay, best);
   if (rc) return rc;
   for (size_t i = 1; i < kinds.size(); ++i) {
     Plan c;
-    if (make_plan(A, n, kinds[i], false, lay, c) == SUP_OK && walk_cost(c) < walk_cost(best)) best = std::move(c);
+    if (make_plan(A, n, kinds[i], false, lay, c) == SUP_OK && walk_cost(c) < walk_cost(best) &&
+        (kinds[i] != kWalkSparse || improve_sparse_plan(A, n, lay, c) == SUP_OK))
+      best = std::move(c);
   }
   const double best_s = std::ldexp(1.0, n - 1) / std::max(ndev, 1) * walk_cost(best) / kLaneOpsPerSec;
   const bool may_save = best_s >= min_saving;  // auto mode: skip the segmented plan's search where it cannot pay

@@ -139,7 +139,13 @@ int make_plan(const double* A, int n, WalkKind kind, bool identity_map, const La
 std::vector<int> greedy_walk_order(const double* A, int n, int count);
 // SkipPer walk + lane columns (walk first) chosen for the chunks its first-state
 // zero check ends (integer matrices); false: keep SkipOrder's map (engine.cpp).
-bool skip_walk_order(const double* A, int n, const Layout& lay, std::vector<int>& out);
+// baseline (m + L columns; NULL: SkipOrder's map) is kept unless the search beats
+// its ops x chunks walked by `factor`.
+bool skip_walk_order(const double* A, int n, const Layout& lay, std::vector<int>& out,
+                     const std::vector<int>* baseline, double factor);
+// A long prefix-blocked plan of an integer matrix, its columns searched for
+// chunk ends (engine.cpp; exact.cpp and quad.cpp use it too).
+int improve_sparse_plan(const double* A, int n, const Layout& lay, Plan& P);
 // Host threads the planners' searches use (jit.cpp).
 int plan_threads();
 

@@ -214,7 +214,7 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
   const Layout lay = default_layout(n);
   int rc = SUP_OK;
   if (lay.m > 0 && (rc = make_plan(A2.data(), n, kWalkSparse, false, lay, P)) == SUP_OK &&
-      walk_cost(P) < 2.0 * n + 1.0) {
+      walk_cost(P) < 2.0 * n + 1.0 && (rc = improve_sparse_plan(A2.data(), n, lay, P)) == SUP_OK) {
     group |= 8;  // run_range_exact / walk_exact.hip: the blocked kernel
   } else {
     SegChoice order;

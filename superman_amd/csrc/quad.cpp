@@ -176,7 +176,8 @@ int quad_perman(const double* A, int n, const sup_opts& o, bool on_cpu, double* 
   const Layout lay = default_layout(n);
   const double bar = (n <= 28 ? 1.0 : 0.4) * (2.0 * n + 1.0);
   int rc = SUP_OK;
-  if (!(lay.m > 0 && (rc = make_plan(A, n, kWalkSparse, false, lay, P)) == SUP_OK && walk_cost(P) < bar)) {
+  if (!(lay.m > 0 && (rc = make_plan(A, n, kWalkSparse, false, lay, P)) == SUP_OK && walk_cost(P) < bar &&
+        (rc = improve_sparse_plan(A, n, lay, P)) == SUP_OK)) {
     SegChoice order;
     order.order = greedy_walk_order(A, n, lay.m + lay.L);
     rc = make_plan(A, n, kWalkDense, false, lay, P, lay.m > 0 ? &order : nullptr);
