@@ -205,6 +205,23 @@ static void test_planning(const std::string& root) {
   CHECK(sup_perman_cpu(mat, t, 22 < n ? 22 : n, SUP_KERNEL_SEGMENTED, 8, &s8, nullptr) == SUP_OK);
   CHECK(s1 == s8);
   sup_free(mat);
+  // config 5 (n = 44 integer, SkipOrder): the SkipPer, SpaRyser and exact
+  // plans search their columns for chunk ends on host threads (round 5)
+  CHECK(sup_read_matrix((root + "/tests/fixtures/synth44_0.15_int").c_str(), 0, &mat, &t, &n, &nnz) == SUP_OK);
+  if (!mat) return;
+  std::vector<double> A5(n * n);
+  for (int i = 0; i < n * n; ++i) A5[i] = t == SUP_INT32 ? ((const int*)mat)[i] : ((const double*)mat)[i];
+  std::vector<int> rp(n), cp(n);
+  CHECK(sup_skip_order(A5.data(), SUP_FLOAT64, n, rp.data(), cp.data()) == SUP_OK);
+  o.jit = -1;
+  std::vector<int> cm1(n), cm2(n);
+  CHECK(sup_plan_info(A5.data(), SUP_FLOAT64, n, SUP_KERNEL_SKIPPER, &o, &kind, cm1.data(), &L, &m, &cc, &pb, &ops) ==
+        SUP_OK);
+  CHECK(kind == 2 && ops < 25.5);
+  CHECK(sup_plan_info(A5.data(), SUP_FLOAT64, n, SUP_KERNEL_SPARYSER, &o, &kind, cm2.data(), &L, &m, &cc, &pb, &ops) ==
+        SUP_OK);
+  CHECK(kind == 1 && cm1 == cm2);  // the same search, the same columns
+  sup_free(mat);
 }
 
 static void test_io_and_reductions(const std::string& root) {
