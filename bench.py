@@ -76,6 +76,9 @@ def parse():
                          "(N = 1, rank 0; falls back to the committed profile); 0: committed profile only")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cold", type=int, default=1, help="time the CLI end to end with an empty / warm cache (N = 1)")
+    ap.add_argument("--pg", action="store_true",
+                    help="create the process group (RCCL, device_id = this rank's GPU) and run every collective "
+                         "even at world 1: executes the N-GPU code path on a one-GPU box")
     return ap.parse_args()
 
 
@@ -121,10 +124,10 @@ def check_plans_agree(key: int, rank: int, world: int, device) -> list:
     shards add up to the permanent only if all ranks walk the same plan.
     All-gather each rank's plan fingerprint (sup_plan_key: walk kind, layout,
     column map, tables, kernel source) and abort on any mismatch."""
-    if world == 1:
-        return [key]
     import torch
     import torch.distributed as dist
+    if not dist.is_initialized():
+        return [key]
     t = torch.tensor([key - (1 << 64) if key >= (1 << 63) else key], dtype=torch.int64, device=device)
     got = [torch.zeros_like(t) for _ in range(world)]
     dist.all_gather(got, t)
@@ -446,7 +449,12 @@ def main():
     # one-GPU box); the real N-GPU run uses one device per rank and RCCL.
     dev = 0 if args.rehearse else local
     tdev = "cpu" if args.rehearse else f"cuda:{dev}"
-    if world > 1:
+    # use_pg: the process group exists and every collective below runs (world
+    # > 1, or --pg at world 1, which executes the RCCL branch on one GPU)
+    use_pg = world > 1 or args.pg
+    if use_pg:
+        if env_world is None:  # --pg without a launcher: a one-rank group on this host
+            os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
         torch.cuda.set_device(dev)
         if args.rehearse:
             dist.init_process_group("gloo")
@@ -464,7 +472,7 @@ def main():
         return a
 
     def barrier():
-        if world > 1:
+        if use_pg:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -479,7 +487,7 @@ def main():
         n = a.shape[0]
         kernel = args.kernel if kernel is None else kernel
         jit = args.jit if jit is None else jit
-        if jit == 0 and world > 1:
+        if jit == 0 and use_pg:
             jit = auto_decision(S, a, kernel, rank, world, dev, tdev)
         # plan + (segmented walk) hiprtc compile, once, before the timed region;
         # gpu_num = world so that --jit 0 decides as the N-rank plan would
@@ -492,7 +500,7 @@ def main():
 
         def step():
             part, k_ms = call()
-            if world > 1:
+            if use_pg:
                 part = combine(part, rank, world, tdev)  # one RCCL all-reduce over xGMI
             return (4 * (n & 1) - 2) * part, k_ms
 
@@ -508,7 +516,7 @@ def main():
                 step()
                 one = time.perf_counter() - t1
             steps = max(args.steps, min(4000, int(min_seconds / max(one, 1e-6)) + 1))
-            if world > 1:
+            if use_pg:
                 t = torch.tensor([steps], dtype=torch.float64, device=tdev)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 steps = int(t.item())
@@ -521,7 +529,7 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
         st = call.stats()
-        if world > 1:
+        if use_pg:
             t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
@@ -618,7 +626,7 @@ def main():
             pmc2 = pmc_record(nb, roof2["kernel"], roof2["plan_key"])
             roof2["traffic"] = hbm_traffic(pmc2)
             visited = float(st2["visited_steps"])
-            if world > 1:  # the shards' visited counts differ (SkipPer's jumps): sum them
+            if use_pg:  # the shards' visited counts differ (SkipPer's jumps): sum them
                 t = torch.tensor([visited], dtype=torch.float64, device=tdev)
                 dist.all_reduce(t)
                 visited = float(t.item())
@@ -636,7 +644,7 @@ def main():
 
     # every rank's walk-kernel time (strong-scaling diagnosis: the slowest rank sets the step)
     rank_kms = [k_ms]
-    if world > 1:
+    if use_pg:
         t = torch.tensor([k_ms], dtype=torch.float64, device=tdev)
         lst = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(lst, t)
@@ -674,6 +682,7 @@ def main():
         "permanent": perm,
         "kernel_ms_per_rank": rank_kms,
         "plan_keys_per_rank": plan_keys[0],
+        "process_group": dist.get_backend() if use_pg else None,
         "densities": also,
         "configs": configs,
     }
@@ -732,7 +741,7 @@ def main():
         rec["cold_start"] = cold_start(args.matrix)
     if rank == 0:
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -100,7 +100,9 @@ typedef struct {
                       /*  wave-chunk (sup_perman, sup_perman_shard, sup_plan_info)           */
   int chunk_log2;     /* 0 = auto; for SUP_SCHED_CHUNKS: wave-chunks per queue item = 2^x    */
   int use_rccl;       /* 1: multi-device partials combined by one RCCL all-reduce (bit-     */
-                      /*    identical to the host combine); 2: also with a single device    */
+                      /*    identical to the host combine); 2: also with a single device;   */
+                      /*    -1: RCCL when the devices are distinct physical GPUs, else the  */
+                      /*    host pairwise tree (the perman CLI's default); 0: host tree     */
   int verbose;        /* print per-device / per-chunk timing lines like the reference        */
   int jit;            /* segmented walk specialised for the matrix pattern (hiprtc, gfx950):  */
                       /*  -1 never; 0 auto: when its cost model wins and the predicted walk  */

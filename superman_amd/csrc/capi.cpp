@@ -569,7 +569,7 @@ int leaf_workers();
 int leaf_batch_max();
 bool leaf_batching(const LeafCtx& c) {
   if (leaf_batch_max() <= 1) return false;
-  return !c.on_cpu && c.sched == SUP_SCHED_SINGLE && c.o.use_rccl == 0 && !(c.o.checkpoint && *c.o.checkpoint) &&
+  return !c.on_cpu && c.sched == SUP_SCHED_SINGLE && c.o.use_rccl <= 0 && !(c.o.checkpoint && *c.o.checkpoint) &&
          (c.kernel == SUP_KERNEL_DENSE || c.kernel == SUP_KERNEL_SPARYSER || c.kernel == SUP_KERNEL_DENSE_PLAIN);
 }
 // Default: batches of 16.  Measured on dwt_59 (145,798 n = 30 leaves, one

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -1351,6 +1352,15 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     else p.nb_hi |= v << (4 * (k - 16));
   }
 
+  // SUP_JIT_TRACE=<file>: the segmented walk's per-wave stamps (diagnostics)
+  const char* trace_path = seg ? std::getenv("SUP_JIT_TRACE") : nullptr;
+  unsigned long long* d_trace = nullptr;
+  if (trace_path && *trace_path) {
+    SUP_HIP(hipMalloc(&d_trace, grid * kWavesPerBlock * 8 * sizeof(unsigned long long)));
+    SUP_HIP(hipMemsetAsync(d_trace, 0, grid * kWavesPerBlock * 8 * sizeof(unsigned long long), s));
+    p.trace = d_trace;
+  }
+
   SUP_ON_DEVICE(c->dev, "walk launch");
   SUP_HIP(hipEventRecord(c->ev0, s));
   if (seg) {
@@ -1398,6 +1408,20 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   r.partial = *c->h_result;
   r.kernel_ms = ms;
   r.grid = (int)grid;
+  if (d_trace) {
+    std::vector<unsigned long long> tr(grid * kWavesPerBlock * 8);
+    SUP_HIP(hipMemcpy(tr.data(), d_trace, tr.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    SUP_HIP(hipFree(d_trace));
+    if (FILE* f = std::fopen(trace_path, "a")) {
+      std::fprintf(f, "# launch chunks %llu grid %llu waves_resident %llu group %u tail_group %u kernel_ms %.4f\n",
+                   (unsigned long long)count, (unsigned long long)grid, (unsigned long long)res_waves, group,
+                   tail_group, ms);
+      for (size_t w = 0; w < tr.size() / 8; ++w)
+        std::fprintf(f, "%zu %llu %llu %llu %llu %llu %llu\n", w, tr[8 * w], tr[8 * w + 1], tr[8 * w + 2],
+                     tr[8 * w + 3], tr[8 * w + 4], tr[8 * w + 5]);
+      std::fclose(f);
+    }
+  }
   if (visited) {
     r.visited = (uint64_t)*vsum * (uint64_t)(1ull << P.lay.L);
   } else {
@@ -1716,22 +1740,45 @@ static int rccl_slots_init(const std::vector<int>& devs, size_t len, RcclSlots& 
 static std::mutex g_comm_mu;
 static std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;
 
-static int rccl_allreduce_slots(RcclSlots& r, std::vector<double>& merged) {
-  const int G = (int)r.devs.size();
-  std::lock_guard<std::mutex> lk(g_comm_mu);  // one collective per communicator at a time
-  auto it = g_comms.find(r.devs);
+// Whether the logical devices `devs` sit on distinct physical GPUs (the auto
+// combine's test; no error is set).
+static bool distinct_physical(const std::vector<int>& devs) {
+  std::vector<int> p;
+  for (int d : devs) p.push_back(phys_device(d));
+  std::sort(p.begin(), p.end());
+  return std::adjacent_find(p.begin(), p.end()) == p.end();
+}
+
+// The communicators of the physical device set `phys`, created on first use
+// (ncclCommInitAll) and kept for the process.  Thread-safe; the error message
+// is returned in `err` as well, since g_err is thread-local and the caller may
+// run this on a helper thread to overlap it with the walk.
+static int rccl_comms(const std::vector<int>& phys, std::vector<ncclComm_t>** out, std::string& err) {
+  std::lock_guard<std::mutex> lk(g_comm_mu);
+  auto it = g_comms.find(phys);
   if (it == g_comms.end()) {
-    std::vector<ncclComm_t> comms(G);
-    const ncclResult_t nr = ncclCommInitAll(comms.data(), G, r.devs.data());
+    std::vector<ncclComm_t> comms(phys.size());
+    const ncclResult_t nr = ncclCommInitAll(comms.data(), (int)phys.size(), phys.data());
     if (nr != ncclSuccess) {
-      set_error(std::string("ncclCommInitAll: ") + ncclGetErrorString(nr));
+      err = std::string("ncclCommInitAll: ") + ncclGetErrorString(nr);
+      set_error(err);
       return SUP_ERCCL;
     }
-    it = g_comms.emplace(r.devs, std::move(comms)).first;
+    it = g_comms.emplace(phys, std::move(comms)).first;
   }
+  *out = &it->second;
+  return SUP_OK;
+}
+
+static int rccl_allreduce_slots(RcclSlots& r, std::vector<double>& merged) {
+  const int G = (int)r.devs.size();
+  std::vector<ncclComm_t>* comms = nullptr;
+  std::string err;
+  if (int rc = rccl_comms(r.devs, &comms, err)) return rc;
+  std::lock_guard<std::mutex> lk(g_comm_mu);  // one collective per communicator at a time
   ncclResult_t nr = ncclGroupStart();
   for (int g = 0; g < G && nr == ncclSuccess; ++g)
-    nr = ncclAllReduce(r.buf[g], r.buf[g], r.len, ncclFloat64, ncclSum, it->second[g], r.st[g]);
+    nr = ncclAllReduce(r.buf[g], r.buf[g], r.len, ncclFloat64, ncclSum, (*comms)[g], r.st[g]);
   const ncclResult_t ge = ncclGroupEnd();
   if (nr != ncclSuccess || ge != ncclSuccess) {
     set_error(std::string("ncclAllReduce: ") + ncclGetErrorString(nr != ncclSuccess ? nr : ge));
@@ -1746,6 +1793,30 @@ static int rccl_allreduce_slots(RcclSlots& r, std::vector<double>& merged) {
   SUP_HIP(hipMemcpy(merged.data(), r.buf[0], r.len * sizeof(double), hipMemcpyDeviceToHost));
   return SUP_OK;
 }
+
+// The communicators' creation (ncclCommInitAll: hundreds of ms on a fresh
+// 8-GPU process) started on a helper thread as soon as the schedule knows it
+// will combine over RCCL, so it overlaps the walk instead of following it.
+struct CommWarmup {
+  std::future<std::pair<int, std::string>> f;
+  void start(const std::vector<int>& phys) {
+    f = std::async(std::launch::async, [phys] {
+      std::vector<ncclComm_t>* c = nullptr;
+      std::string err;
+      const int rc = rccl_comms(phys, &c, err);
+      return std::make_pair(rc, err);
+    });
+  }
+  int join() {  // before the all-reduce (and on every exit path, by the destructor)
+    if (!f.valid()) return SUP_OK;
+    auto r = f.get();
+    if (r.first) set_error(r.second);
+    return r.first;
+  }
+  ~CommWarmup() {
+    if (f.valid()) f.wait();
+  }
+};
 
 // ------------------------------------------------------------ checkpoint --
 // sup_opts::checkpoint: a text file, header "supckpt 2 <plan fingerprint>
@@ -1921,7 +1992,18 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   const uint64_t total = c1 - c0;
   const bool want_visited = true;
 
-  const bool rccl = (G > 1 && o.use_rccl) || o.use_rccl == 2;  // 2: also on one device (exercises RCCL)
+  // Combine of the device partials: use_rccl 2 forces RCCL (even on one
+  // device: exercises it), 1 asks for it (SUP_ERCCL when the devices share a
+  // GPU), -1 (the CLI default) takes it whenever the G > 1 devices are
+  // distinct physical GPUs and keeps the host pairwise tree otherwise; 0: host.
+  bool rccl = (G > 1 && o.use_rccl > 0) || o.use_rccl == 2;
+  if (G > 1 && o.use_rccl < 0) rccl = distinct_physical(devs);
+  auto say_combine = [&](bool used, const char* why) {
+    if (o.verbose)
+      std::printf("Combine: %s over %d device%s%s\n", used ? "RCCL all-reduce (slot buffers)" : "host pairwise tree",
+                  G, G == 1 ? "" : "s", why);
+  };
+  CommWarmup warm;
   if (sched != SUP_SCHED_CHUNKS && o.checkpoint && *o.checkpoint) {
     set_error("a checkpoint file needs the chunk queue (-p6 / -p8, SUP_SCHED_CHUNKS)");
     return SUP_EUNSUPPORTED;
@@ -1941,6 +2023,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     for (int q = 0; q < npieces; ++q) owner[q] = manual ? (q < 3 ? 0 : q < 6 ? 1 : q == 6 ? 2 : 3) % G : q;
     RcclSlots slots;
     if (rccl && (rc = rccl_slots_init(devs, npieces, slots))) return rc;
+    if (rccl) warm.start(slots.devs);
     std::vector<RangeResult> rr(npieces);
     std::vector<int> rcs(G, SUP_OK);
     std::vector<std::string> errs(G);  // g_err is thread_local: carry worker messages back
@@ -1990,11 +2073,12 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
     out.devices = G;
     if (rccl) {
       std::vector<double> merged;
-      if ((rc = rccl_allreduce_slots(slots, merged))) return rc;
+      if ((rc = warm.join()) || (rc = rccl_allreduce_slots(slots, merged))) return rc;
       out.total = pairwise_host(merged);
     } else {
       out.total = pairwise_host(piece);
     }
+    say_combine(rccl, rccl || G == 1 ? "" : o.use_rccl < 0 ? " (devices share a GPU)" : "");
     return SUP_OK;
   }
 
@@ -2044,6 +2128,7 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   const bool rccl_items = rccl && !o.cpu_worker && !ckpt;
   RcclSlots slots;
   if (rccl_items && (rc = rccl_slots_init(devs, nitems, slots))) return rc;
+  if (rccl_items) warm.start(slots.devs);
   std::vector<double> dev_ms(G + 1, 0.0), dev_jit(G, 0.0);
   std::vector<uint64_t> dev_vis(G + 1, 0);
   std::vector<int> dev_grid(G + 1, 0);
@@ -2095,11 +2180,15 @@ int schedule(const Plan& P, sup_sched sched, const sup_opts& o, uint64_t c0, uin
   out.dev_partials = dev_sum;
   if (rccl_items) {
     std::vector<double> merged;
-    if ((rc = rccl_allreduce_slots(slots, merged))) return rc;
+    if ((rc = warm.join()) || (rc = rccl_allreduce_slots(slots, merged))) return rc;
     out.total = pairwise_host(merged);
   } else {
     out.total = pairwise_host(ipart);
   }
+  say_combine(rccl_items, rccl_items || G == 1 ? ""
+                          : o.cpu_worker  ? " (the CPU worker's items have no device slot)"
+                          : ckpt          ? " (checkpointed items)"
+                          : o.use_rccl < 0 ? " (devices share a GPU)" : "");
   return SUP_OK;
 }
 

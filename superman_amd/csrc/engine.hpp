@@ -344,11 +344,6 @@ int ckpt_record(Checkpoint& ck, uint64_t it, double part, uint64_t visited);
 // (sup_plan_key; the checkpoint file's header)
 uint64_t plan_fingerprint(const Plan& P);
 
-// All-reduce (sum, fp64) over RCCL, in one process, of per-device vectors with
-// disjoint supports (exact in any order); merged = the slot-wise sum.
-int rccl_allreduce_partials(const std::vector<int>& devs, const std::vector<std::vector<double>>& contrib,
-                            std::vector<double>& merged);
-
 // CPU worker: the same wave-chunk walk on host threads (used for `-c` and for
 // the hybrid `-c -g` chunk queue).  Bit-identical to the dense/sparse kernels.
 double cpu_walk_range(const Plan& P, uint64_t c0, uint64_t c1, int threads);

@@ -1554,6 +1554,14 @@ struct Gen {
     o << "  __shared__ double s_keep[" << kBlock / 64 << "][64];\n";
     o << "  __shared__ uint32_t s_vkeep[" << kBlock / 64 << "][64];\n";
     o << "  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);\n";
+    // SUP_JIT_TRACE (diagnostics; a knob, so a fresh plan and kernel): each
+    // wave stamps its entry / exit and sums the shader cycles of its chunk
+    // starts (the start state, row copies and trees: everything before the walk
+    // loop), for the launch ramp / queue tail / chunk-start split
+    const bool trace = std::getenv("SUP_JIT_TRACE") != nullptr;
+    if (trace)
+      o << "  const uint64_t tr_r0 = __builtin_amdgcn_s_memrealtime(), tr_c0 = __builtin_amdgcn_s_memtime();\n"
+        << "  uint64_t tr_n = 0, tr_sc = 0;\n";
     // ticket t -> chunks [base, base + len): groups of p.group, then (from
     // p.tail_begin) groups of p.tail_group
     // (p.tail_ticket = p.tail_begin / p.group from the host: all of it
@@ -1573,6 +1581,7 @@ struct Gen {
     o << "      if (a >= p.chunk_count) break;\n";
     o << "      const uint64_t ga = p.chunk_begin + a;\n";
     o << "      double x[N], y[" << len0 << "];\n";
+    if (trace) o << "      const uint64_t tr_s = __builtin_amdgcn_s_memtime();\n";
     o << "      chunk_start<N>(x, p, ga, SUP_LANE());\n";
     o << "      {\n";  // y = x + a_0 on segment 0 (the + block of walk bit 0) = y^0
     o << "        cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off_const(0, 0) << ");\n";
@@ -1624,6 +1633,7 @@ struct Gen {
     // two-level lane sum: acc folds into tot after each shared dyn step, so
     // no sequential sum runs longer than 2^b pairs (error growth)
     o << "      double tot = 0.0;\n";
+    if (trace) o << "      asm volatile(\"\" : \"+v\"(acc));\n      tr_sc += __builtin_amdgcn_s_memtime() - tr_s;\n      ++tr_n;\n";
     o << "      for (uint32_t q = 0; q < " << Q << "u; ++q) {\n";
     const char* ind = "        ";
     // pair index j = B*q + s, s = 1 .. B-1: pair bit p = ctz(s) (walk bit p+1);
@@ -1684,6 +1694,12 @@ struct Gen {
     o << "    }\n";
     o << "    __builtin_amdgcn_wave_barrier();\n";
     o << "  }\n";
+    if (trace)
+      o << "  if (p.trace && SUP_LANE() == 0) {\n"
+        << "    unsigned long long* t = p.trace + 8ull * (blockIdx.x * " << kBlock / 64 << "u + wv);\n"
+        << "    t[0] = tr_r0; t[1] = __builtin_amdgcn_s_memrealtime(); t[2] = tr_c0;\n"
+        << "    t[3] = __builtin_amdgcn_s_memtime(); t[4] = tr_n; t[5] = tr_sc;\n"
+        << "  }\n";
     o << "}\n";
     o << "}  // namespace sup\n";
     return o.str();

@@ -7,7 +7,8 @@
 // first device, -k <reps> repetitions, -o compression (d1/d2 singletons, then
 // the d1/d2/d34 expansion while n > 30), -u <t> scaling; MatrixMarket input
 // (detected by its banner, read as main.cpp:1515-1615).  Own additions: -R
-// combine multi-GPU partials with RCCL; -v per-kernel / per-chunk timing;
+// insist on the RCCL combine of multi-GPU partials (by default it runs
+// whenever the -d devices are distinct GPUs, else the host pairwise tree); -v per-kernel / per-chunk timing;
 // --seed (-S) the estimators' Philox seed (-a / -i; the reference seeds with
 // time(0), so its estimates are not reproducible); --jit (-J) <-1|0|1> the
 // pattern-specialised segmented walk (sup_opts.jit: never / auto / whenever
@@ -243,7 +244,9 @@ int main(int argc, char** argv) {
   o.device_id = c.device;
   o.threads = c.threads;
   o.cpu_worker = (c.gpu && c.cpu) ? 1 : 0;
-  o.use_rccl = c.rccl ? 1 : 0;
+  // multi-device partials: RCCL whenever the devices are distinct GPUs (-1),
+  // -R insists on it (an error when SUP_DEVICE_MAP shares a GPU)
+  o.use_rccl = c.rccl ? 1 : -1;
   o.verbose = c.verbose ? 1 : 0;
   o.jit = c.jit;
   o.checkpoint = c.checkpoint.empty() ? nullptr : c.checkpoint.c_str();

@@ -51,6 +51,10 @@ struct WalkParams {
   // segmented walk (jit.cpp): per walk bit, the values of the rows its column
   // touches, packed (+ block, then - block, each padded to 8 doubles)
   const double* jtab;
+  // diagnostics (SUP_JIT_TRACE): per wave 8 u64 — realtime and shader-clock
+  // stamps at entry and exit, chunks walked, shader cycles spent in chunk
+  // starts; nullptr (and never written) otherwise
+  unsigned long long* trace;
 };
 
 // Exact path (walk_exact.hip): residues of the walk's terms modulo up to
