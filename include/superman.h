@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SUP_ABI_VERSION 8  /* 8: sup_device_checks (round 5); 7: sup_rccl_devices, sup_stats.seg_cached_bits / seg_pair_bits */
+#define SUP_ABI_VERSION 9  /* 9: sup_device_warmup, sup_opts.use_rccl = -1 (round 6); 8: sup_device_checks (round 5); 7: sup_rccl_devices, sup_stats.seg_cached_bits / seg_pair_bits */
 
 /* ---- error codes ------------------------------------------------------ */
 #define SUP_OK            0
@@ -160,6 +160,11 @@ int         sup_rccl_devices(int ndev, int* phys);
  * this logical device is the one the thread last selected (a mismatch fails
  * the call with SUP_EHIP); 0 when the mode is off.  Tests and diagnostics. */
 uint64_t    sup_device_checks(void);
+/* Initialise the HIP runtime, the contexts of devices [device_id, device_id +
+ * gpu_num) and the ahead-of-time walk code objects of order n (0: none), so a
+ * caller can run it on a thread beside its planning (the perman CLI does).
+ * Thread-safe; a later call on the same devices returns at once. */
+int         sup_device_warmup(int device_id, int gpu_num, int n);
 
 /* ------------------------------------------------------------------------ *
  * Generic entry point.  `mat` is n x n row-major of type `t` (already

@@ -92,6 +92,10 @@ int sup_device_count(int* count) {
   return device_count(count);
 }
 uint64_t sup_device_checks(void) { return device_checks_passed(); }
+int sup_device_warmup(int device_id, int gpu_num, int n) {
+  if (device_id < 0 || gpu_num < 1) return SUP_EINVAL;
+  return warm_devices(device_id, gpu_num, n);
+}
 int sup_rccl_devices(int ndev, int* phys) {
   if (ndev < 1 || ndev > 1024 || !phys) return SUP_EINVAL;
   std::vector<int> devs(ndev), p;

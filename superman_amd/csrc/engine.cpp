@@ -1192,6 +1192,25 @@ static int get_ctx(int dev, DeviceCtx** out) {
   return SUP_OK;
 }
 
+// Device warm-up (sup_device_warmup): the HIP runtime's initialisation,
+// each device's context (stream, events, buffers) and the ahead-of-time walk
+// code objects of order n, so a caller can overlap them with its host-side
+// planning instead of paying them after it.
+int warm_devices(int first, int count, int n) {
+  for (int d = first; d < first + count; ++d) {
+    DeviceCtx* c = nullptr;
+    if (int rc = get_ctx(d, &c)) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    SUP_HIP(select_device(c->dev));
+    if (n >= 1 && n <= SUP_MAX_N)
+      for (WalkKind k : {kWalkDense, kWalkSparse}) {
+        int b = 0;
+        SUP_HIP(walk_occupancy(k, n, &b));
+      }
+  }
+  return SUP_OK;
+}
+
 // Per-call completion (round 4, tools/probe_launch.hip, profiles/r4/probe_launch_b.log):
 // around a 500 us kernel, marker events + one more launch + hipStreamSynchronize
 // cost 18.9 us beyond the kernel; waiting instead for a sequence number the

@@ -308,6 +308,8 @@ uint64_t device_checks_passed();
     const int rc_ = check_device((dev), (what)); \
     if (rc_) return rc_;                         \
   } while (0)
+// HIP init, contexts of devices [first, first + count) and the AOT walks of order n (sup_device_warmup)
+int warm_devices(int first, int count, int n);
 // physical devices of the RCCL combine over logical `devs`; SUP_ERCCL if two share a GPU
 int rccl_physical_devices(const std::vector<int>& devs, std::vector<int>& phys);
 

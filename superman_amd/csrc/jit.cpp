@@ -69,8 +69,13 @@
 // dynamic LDS.
 #include <dlfcn.h>
 #include <hip/hiprtc.h>
+#include <sched.h>
+#include <spawn.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
+
+#include <cerrno>
 
 #include <algorithm>
 #include <cstring>
@@ -1777,6 +1782,11 @@ uint64_t jit_source_key(const std::string& src) {
 
 }  // namespace
 
+// Out-of-process compiles (sup_rtc helpers), defined with the code cache below.
+bool jit_code_cached(const Plan& P);
+size_t rtc_procs();
+void prefetch_compiles(const std::vector<const Plan*>& plans, size_t procs);
+
 int build_seg(Plan& P, int fixed_budget) {
   const int n = P.n, L = P.lay.L, m = P.lay.m;
   if (m < 3) {
@@ -1953,13 +1963,6 @@ int build_seg(Plan& P, int fixed_budget) {
     std::vector<CodeScan> scans(cand.size());
     std::vector<int> src(cand.size(), SUP_EHIP);
     std::vector<char> done(cand.size(), 0);
-    // One compile at a time: hiprtc compiles in one process do not overlap
-    // (measured on this image: 8 threads compiling 8 different kernels take
-    // 0.8 of the time of 8 sequential compiles, the comgr action behind
-    // hiprtcCompileProgram is serialised), so the ladder is bisected instead
-    // of walked in concurrent batches: 5 compiles instead of 8 on the n = 40
-    // bench matrix, the same choice wherever "clean" and "no scratch at all"
-    // are monotone in the budget (they are on every matrix measured).
     auto compile_one = [&](size_t i) {
       if (done[i]) return;
       const auto t0 = std::chrono::steady_clock::now();
@@ -1975,42 +1978,89 @@ int build_seg(Plan& P, int fixed_budget) {
     size_t pp = 0;
     for (size_t k = 0; k < idx.size(); ++k)
       if (budgets[idx[k]] <= kRegsMax) pp = k;
-    const size_t probe = idx[pp];
-    compile_one(probe);
-    if (src[probe] != SUP_OK) return SUP_EHIP;
-    // The largest clean budget: above the probe when the probe is clean, else
-    // below it (bisection over idx positions; lo clean, hi not).
-    size_t c_pos;
-    if (clean(probe)) {
-      size_t lo = pp, hi = idx.size();
-      while (hi - lo > 1) {
-        const size_t mid = lo + (hi - lo) / 2;
-        compile_one(idx[mid]);
-        (clean(idx[mid]) ? lo : hi) = mid;
+    // The search, as a replay over the outcomes known so far (0 = not compiled
+    // yet): the candidate it needs next, kLadderDone, or kLadderFail.  From the
+    // probe: the largest clean budget, bisected over idx positions (above the
+    // probe when the probe is clean, else below it; lo clean, hi not), then a
+    // kernel with no scratch at all within kScratchTolerance of its ops (the
+    // largest such budget below it).  One compile at a time in this process —
+    // hiprtc compiles in one process do not overlap (8 threads compiling 8
+    // kernels take 0.8 of the time of 8 sequential compiles; the comgr action
+    // is serialised), hence a bisection (5 compiles instead of 8 on the n = 40
+    // bench matrix; the same choice wherever "clean" and "no scratch at all"
+    // are monotone in the budget, as on every matrix measured).
+    enum { kUnknown = 0, kFail, kDirty, kCleanScratch, kClean0 };
+    constexpr long kLadderDone = -1, kLadderFail = -2;
+    auto next_needed = [&](const std::vector<int>& o) -> long {
+      const size_t probe = idx[pp];
+      if (o[probe] == kUnknown) return (long)probe;
+      if (o[probe] == kFail) return kLadderFail;
+      auto cl = [&](size_t i) { return o[i] >= kCleanScratch; };
+      size_t c_pos;
+      if (cl(probe)) {
+        size_t lo = pp, hi = idx.size();
+        while (hi - lo > 1) {
+          const size_t mid = lo + (hi - lo) / 2;
+          if (o[idx[mid]] == kUnknown) return (long)idx[mid];
+          (cl(idx[mid]) ? lo : hi) = mid;
+        }
+        c_pos = lo;
+      } else {
+        long lo = -1, hi = (long)pp;
+        while (hi - lo > 1) {
+          const long mid = lo + (hi - lo) / 2;
+          if (o[idx[mid]] == kUnknown) return (long)idx[mid];
+          (cl(idx[mid]) ? lo : hi) = mid;
+        }
+        if (lo < 0) return kLadderFail;
+        c_pos = (size_t)lo;
       }
-      c_pos = lo;
-    } else {
-      long lo = -1, hi = (long)pp;
-      while (hi - lo > 1) {
-        const long mid = lo + (hi - lo) / 2;
-        compile_one(idx[mid]);
-        if (clean(idx[mid])) lo = mid;
-        else hi = mid;
+      if (o[idx[c_pos]] != kClean0)
+        for (size_t k = c_pos; k-- > 0;) {
+          if (cand[idx[k]].seg_ops > cand[idx[c_pos]].seg_ops * (1.0 + kScratchTolerance)) break;
+          if (o[idx[k]] == kUnknown) return (long)idx[k];
+          if (o[idx[k]] == kClean0) break;
+        }
+      return kLadderDone;
+    };
+    std::vector<int> outcome(cand.size(), kUnknown);
+    const size_t procs = rtc_procs();
+    for (;;) {
+      const long k = next_needed(outcome);
+      if (k < 0) break;
+      if (procs > 1 && !jit_code_cached(cand[k])) {
+        // Ahead of the search: the candidates its next steps could need, over
+        // every outcome of the compiles still ahead (breadth first, up to one
+        // per host core), compiled at once by helper processes
+        // (prefetch_compiles).  The search then runs as above on the cached
+        // code objects: the same decisions, the same plan.
+        std::vector<const Plan*> batch;
+        std::vector<char> queued(cand.size(), 0);
+        std::queue<std::vector<int>> q;
+        q.push(outcome);
+        for (size_t visits = 0; !q.empty() && batch.size() < procs && visits < 4096; ++visits) {
+          std::vector<int> h = std::move(q.front());
+          q.pop();
+          const long s = next_needed(h);
+          if (s < 0) continue;
+          if (!queued[s] && !jit_code_cached(cand[s])) queued[s] = 1, batch.push_back(&cand[s]);
+          for (int r : {kDirty, kCleanScratch, kClean0}) {
+            std::vector<int> h2 = h;
+            h2[s] = r;
+            q.push(std::move(h2));
+          }
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        prefetch_compiles(batch, procs);
+        t_compile_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       }
-      if (lo < 0) {
-        set_error("segmented walk: every budget's kernel touches scratch inside its walk loop (or fails to compile)");
-        return SUP_EHIP;
-      }
-      c_pos = (size_t)lo;
+      compile_one((size_t)k);
+      outcome[k] = src[k] != SUP_OK         ? kFail
+                   : scans[k].loop_scratch  ? kDirty
+                   : scans[k].scratch_bytes ? kCleanScratch
+                                            : kClean0;
     }
-    // A kernel with no scratch at all is preferred within kScratchTolerance of
-    // the ops: the largest such budget below the chosen one.
-    if (scans[idx[c_pos]].scratch_bytes != 0)
-      for (size_t k = c_pos; k-- > 0;) {
-        if (cand[idx[k]].seg_ops > cand[idx[c_pos]].seg_ops * (1.0 + kScratchTolerance)) break;
-        compile_one(idx[k]);
-        if (clean(idx[k]) && scans[idx[k]].scratch_bytes == 0) break;
-      }
+    if (outcome[idx[pp]] == kFail) return SUP_EHIP;  // the probe's compile error is set
     auto pick = [&]() {
       int c = -1, bare = -1;
       for (size_t i : idx) {
@@ -2187,6 +2237,118 @@ int compile(const Plan& P, std::shared_ptr<std::vector<char>>& code) {
   if (!dir.empty()) write_file_atomic(dir, name, *co);
   return publish();
 }
+
+}  // namespace
+
+// ------------------------------------------------- out-of-process compiles --
+// hiprtc compiles in one process are serialised, so a batch of candidate
+// kernels (the budget ladder's next steps) is compiled by helper processes,
+// one per host core: superman_amd/bin/sup_rtc (sup_rtc.cpp) loads the same
+// hiprtc library as this process and writes the code object, which enters the
+// memory and disk caches exactly as an in-process compile's would.  Best
+// effort: a candidate whose helper fails is compiled in process when the
+// search reaches it (with the register retry and the error message).
+// SUP_RTC_PROCS caps the helpers (0 or 1: none); SUP_RTC_HELPER names the
+// helper binary.
+
+bool jit_code_cached(const Plan& P) {
+  {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    if (g_code.count(P.jit_key)) return true;
+  }
+  const std::string dir = cache_dir();
+  struct stat st;
+  return !dir.empty() && ::stat((dir + "/seg_" + key_hex(P.jit_key) + ".co").c_str(), &st) == 0 && st.st_size > 0;
+}
+
+namespace {
+
+std::string rtc_helper() {
+  if (const char* e = std::getenv("SUP_RTC_HELPER")) return e;
+  Dl_info info;
+  if (!dladdr((void*)&rtc_helper, &info) || !info.dli_fname) return "";
+  std::string lib = info.dli_fname;  // .../superman_amd/lib/libsuperman_hip.so
+  const size_t s = lib.rfind('/');
+  return (s == std::string::npos ? std::string(".") : lib.substr(0, s)) + "/../bin/sup_rtc";
+}
+
+std::string hiprtc_library() {
+  Dl_info info;
+  if (!dladdr((void*)&hiprtcCompileProgram, &info) || !info.dli_fname) return "";
+  return info.dli_fname;
+}
+
+}  // namespace
+
+size_t rtc_procs() {
+  if (const char* e = std::getenv("SUP_RTC_PROCS")) return (size_t)std::max(0, std::atoi(e));
+  if (g_jit_failed.load() || std::getenv("SUP_JIT_FAIL")) return 0;
+  cpu_set_t set;
+  size_t cpus = std::max(1u, std::thread::hardware_concurrency());
+  if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = (size_t)CPU_COUNT(&set);
+  return std::min<size_t>(16, cpus);
+}
+
+void prefetch_compiles(const std::vector<const Plan*>& plans, size_t procs) {
+  std::vector<const Plan*> todo;
+  for (const Plan* p : plans)
+    if (!jit_code_cached(*p)) todo.push_back(p);
+  if (todo.size() < 2 || procs < 2 || g_jit_failed.load()) return;  // one compile: in process, as fast
+  const std::string helper = rtc_helper(), lib = hiprtc_library();
+  if (helper.empty() || lib.empty() || ::access(helper.c_str(), X_OK) != 0) return;
+  const char* tmpdir = std::getenv("TMPDIR");
+  std::string dir = std::string(tmpdir && *tmpdir ? tmpdir : "/tmp") + "/sup_rtc_XXXXXX";
+  if (!::mkdtemp(&dir[0])) return;
+  auto put = [&](const std::string& name, const std::string& text) {
+    std::ofstream f(dir + "/" + name, std::ios::binary);
+    f << text;
+    return (bool)f;
+  };
+  std::vector<std::string> made;
+  if (put("walk_common.hpp", kWalkCommonSrc) && put("walk_params.hpp", kWalkParamsSrc)) {
+    made = {"walk_common.hpp", "walk_params.hpp"};
+    const std::vector<std::string> opts = jit_opts();
+    std::atomic<size_t> next{0};
+    std::mutex mu;
+    auto worker = [&]() {
+      for (size_t i; (i = next.fetch_add(1)) < todo.size();) {
+        const Plan& P = *todo[i];
+        const std::string name = "seg_" + key_hex(P.jit_key);
+        {
+          std::lock_guard<std::mutex> g(mu);
+          made.push_back(name + ".hip"), made.push_back(name + ".co"), made.push_back(name + ".log");
+        }
+        if (!put(name + ".hip", P.jit_src)) continue;
+        std::vector<std::string> args = {helper, lib, dir, name};
+        args.insert(args.end(), opts.begin(), opts.end());
+        std::vector<char*> argv;
+        for (std::string& a : args) argv.push_back(&a[0]);
+        argv.push_back(nullptr);
+        pid_t pid = 0;
+        if (posix_spawn(&pid, helper.c_str(), nullptr, nullptr, argv.data(), environ) != 0) continue;
+        int status = 0;
+        while (::waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+        }
+        if (!WIFEXITED(status) || WEXITSTATUS(status) != 0) continue;
+        auto co = std::make_shared<std::vector<char>>();
+        if (!read_file(dir + "/" + name + ".co", *co)) continue;
+        {
+          std::lock_guard<std::mutex> g(g_jit_mu);
+          g_code.emplace(P.jit_key, co);
+        }
+        const std::string cdir = cache_dir();
+        if (!cdir.empty()) write_file_atomic(cdir, name + ".co", *co);
+      }
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < std::min(procs, todo.size()); ++t) th.emplace_back(worker);
+    for (auto& t : th) t.join();
+  }
+  for (const std::string& f : made) ::unlink((dir + "/" + f).c_str());
+  ::rmdir(dir.c_str());
+}
+
+namespace {
 
 int resolve(int dev, const Plan& P, hipFunction_t* fn) {
   if (P.kind != kWalkSeg || P.jit_src.empty()) {

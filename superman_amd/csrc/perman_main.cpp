@@ -27,6 +27,7 @@
 #include <cstring>
 #include <iostream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/superman.h"
@@ -376,6 +377,18 @@ int main(int argc, char** argv) {
     }
   }
 
+  // HIP initialisation, the device contexts and the walk code objects on a
+  // thread beside the planning sup_perman does first on the host (a cold
+  // segmented plan is ~1 s of search and compiles): the walk then starts on a
+  // warm runtime.  Its errors surface again in the call itself.
+  std::thread warm;
+  if (on_gpu) warm = std::thread([&o, n] { (void)sup_device_warmup(o.device_id, o.gpu_num, n); });
+  struct Join {
+    std::thread& t;
+    ~Join() {
+      if (t.joinable()) t.join();
+    }
+  } join_warm{warm};
   for (int r = 0; r < c.reps; ++r) {
     double perm = 0.0;
     sup_stats st;

@@ -404,3 +404,35 @@ def test_seg_scheduling_knobs_keep_pinned_plan(sup, tmp_path, monkeypatch):
         keys.add(sup.plan_key(a, "seg"))
         monkeypatch.delenv(knob)
     assert len(keys) == 4
+
+
+def test_budget_ladder_helper_compiles_same_plan(tmp_path):
+    """The budget ladder's candidates compiled ahead of the bisection by
+    sup_rtc helper processes (one per host core; jit.cpp prefetch_compiles)
+    give the plan the serial in-process bisection gives: the same plan key
+    (walk, tables, kernel source), and every code object both runs compiled is
+    byte-identical — the helper loads this process's own hiprtc."""
+    import subprocess
+    import sys
+    code = ("import sys, numpy as np, superman_amd as S\n"
+            "a = np.load(sys.argv[1])\n"
+            "r = S.prepare(a, 'dense', jit=1)\n"
+            "print(r['kind'], hex(S.plan_key(a, 'dense', jit=1)))\n")
+    rng = np.random.default_rng(38)
+    a = np.where(rng.random((38, 38)) < 0.5, rng.random((38, 38)) * 5, 0.0)
+    a[np.arange(38), rng.permutation(38)] = 1.0
+    np.save(tmp_path / "a.npy", a)
+    out, objs = [], []
+    for procs in ("0", "8"):
+        cache = tmp_path / f"cache{procs}"
+        env = dict(os.environ, SUP_JIT_CACHE_DIR=str(cache), AMD_COMGR_CACHE_DIR=str(cache / "comgr"),
+                   SUP_RTC_PROCS=procs, PYTHONPATH=ROOT, OMP_NUM_THREADS="8")
+        r = subprocess.run([sys.executable, "-c", code, str(tmp_path / "a.npy")], capture_output=True, text=True,
+                           env=env, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        out.append(r.stdout.split())
+        objs.append({p.name: p.read_bytes() for p in cache.glob("seg_*.co")})
+    assert out[0][0] == "seg" and out[0] == out[1]
+    assert len(objs[1]) > len(objs[0]) >= 2  # the helpers compiled ahead; the serial run only what it visited
+    for name, data in objs[0].items():
+        assert objs[1][name] == data, name

@@ -21,6 +21,7 @@ for step in "$@"; do
   case $step in
     rccl) run pytest_rccl 900 $PYT tests/test_gpu_rccl_branch.py;;
     rccl_parity) run pytest_rccl_parity 600 $PYT tests/test_gpu_parity.py -k "rccl or schedulers";;
+    cold) run cold_start 400 python3 -c "import sys, json; sys.path.insert(0, '.'); import bench; print(json.dumps(bench.cold_start('tests/fixtures/double__40_0.50_0'), indent=1))";;
     trace) run probe_trace 400 python3 -u tools/probe_trace.py;;
     trace_cfg2) run probe_trace_cfg2 400 python3 -u tools/probe_trace.py double__32_0.50_0 --walk-log2 0 9 11;;
     pmc_cfg2) run pmc_cfg2 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU \
