@@ -21,6 +21,12 @@ for step in "$@"; do
   case $step in
     rccl) run pytest_rccl 900 $PYT tests/test_gpu_rccl_branch.py;;
     rccl_parity) run pytest_rccl_parity 600 $PYT tests/test_gpu_parity.py -k "rccl or schedulers";;
+    skip_tests) run pytest_skip 900 $PYT tests/test_gpu_parity.py tests/test_gpu_pinned.py tests/test_gpu_checkpoint.py \
+                  tests/test_gpu_multidev.py -k "skip or config5 or p8 or sparse_and_skipper";;
+    skip_time) run probe_skip 300 python3 -u tools/probe_skip.py 3;;
+    skip_pmc) run pmc_skip 180 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_ADD_F64 \
+                SQ_INSTS_VALU_MUL_F64 SQ_WAVES SQ_INSTS_SMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/pmc_skip -o run \
+                --output-format csv -- python3 tools/probe_skip.py 1;;
     cold) run cold_start 400 python3 -c "import sys, json; sys.path.insert(0, '.'); import bench; print(json.dumps(bench.cold_start('tests/fixtures/double__40_0.50_0'), indent=1))";;
     trace) run probe_trace 400 python3 -u tools/probe_trace.py;;
     trace_cfg2) run probe_trace_cfg2 400 python3 -u tools/probe_trace.py double__32_0.50_0 --walk-log2 0 9 11;;
