@@ -163,7 +163,7 @@ struct DevWorker {
     hipDeviceProp_t prop;
     AHIP(hipGetDeviceProperties(&prop, phys_device(dev)));
     cus = prop.multiProcessorCount;
-    // The cooperative form for large n (tools/probe_approx_coop.py,
+    // The cooperative form for large n (tools/probes/probe_approx_coop.py,
     // profiles/r2/probe_approx_coop.log): the scaling estimator from n > 96
     // (its per-lane factors live in an HBM scratch: 0.81x at n = 72, 2.5x at
     // 128, 110x at 288 and 648), Rasmussen from n > 128 (0.35x at 128, 4.6x at

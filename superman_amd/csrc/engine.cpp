@@ -160,7 +160,7 @@ std::vector<int> greedy_walk_order(const double* A, int n, int count) {
 // columns, so the column map decides how many chunks SkipPer walks at all.
 // SkipOrder's own map (identity) walks 25.7 % of config 5's states
 // (profiles/r5); a map chosen for these chunk ends walks 10.6 % at a lower
-// prefix cost (tools/skip_sim.c).
+// prefix cost (tools/probes/skip_sim.c).
 namespace {
 struct SkipOrderEval {
   const double* A;

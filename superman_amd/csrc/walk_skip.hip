@@ -177,7 +177,7 @@ __device__ __forceinline__ void skip_move(double (&x)[N], double (&U)[Blocks<N>:
 //     their walk columns toggles: the wave moves to the last of those toggles
 //     (a segment start).  Skipped terms are exactly zero, so the sum is the
 //     per-state walk's (the skips are fewer: the simulation on config 5
-//     visits 27.6 % of the states instead of 21.8 %, tools/skip_sim);
+//     visits 27.6 % of the states instead of 21.8 %, tools/probes/skip_sim);
 //   * the move adds the differing walk columns block-wise and re-forms the
 //     suffix products once (bit-identical to one step per bit, skip_move);
 //   * the arguments only the zero scan and the chunk end read are loaded

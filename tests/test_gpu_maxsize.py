@@ -74,7 +74,7 @@ def test_order_limit(sup):
 
 
 def _dense_mat(n, d):
-    """tools/sweep_large_n.py's matrices: Bernoulli(d), U(0,5), a permutation diagonal."""
+    """tools/probes/sweep_large_n.py's matrices: Bernoulli(d), U(0,5), a permutation diagonal."""
     rng = np.random.default_rng(1000 * n + int(round(100 * d)))
     a = np.where(rng.random((n, n)) < d, rng.random((n, n)) * 5, 0.0)
     a[np.arange(n), rng.permutation(n)] = 1.0 + rng.random(n)

@@ -23,21 +23,17 @@ for step in "$@"; do
     rccl_parity) run pytest_rccl_parity 600 $PYT tests/test_gpu_parity.py -k "rccl or schedulers";;
     skip_tests) run pytest_skip 900 $PYT tests/test_gpu_parity.py tests/test_gpu_pinned.py tests/test_gpu_checkpoint.py \
                   tests/test_gpu_multidev.py -k "skip or config5 or p8 or sparse_and_skipper";;
-    skip_time) run probe_skip 300 python3 -u tools/probe_skip.py 3;;
+    skip_time) run probe_skip 300 python3 -u tools/probes/probe_skip.py 3;;
     skip_pmc) run pmc_skip 180 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_ADD_F64 \
                 SQ_INSTS_VALU_MUL_F64 SQ_WAVES SQ_INSTS_SMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/pmc_skip -o run \
-                --output-format csv -- python3 tools/probe_skip.py 1;;
+                --output-format csv -- python3 tools/probes/probe_skip.py 1;;
     cold) run cold_start 400 python3 -c "import sys, json; sys.path.insert(0, '.'); import bench; print(json.dumps(bench.cold_start('tests/fixtures/double__40_0.50_0'), indent=1))";;
-    trace) run probe_trace 400 python3 -u tools/probe_trace.py;;
-    trace_cfg2) run probe_trace_cfg2 400 python3 -u tools/probe_trace.py double__32_0.50_0 --walk-log2 0 9 11;;
+    trace) run probe_trace 400 python3 -u tools/probes/probe_trace.py;;
+    trace_cfg2) run probe_trace_cfg2 400 python3 -u tools/probes/probe_trace.py double__32_0.50_0 --walk-log2 0 9 11;;
     pmc_cfg2) run pmc_cfg2 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU \
                 SQ_INSTS_SALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT -d $O/pmc_cfg2 -o run --output-format csv -- \
                 python3 bench.py --pmc-child --matrix tests/fixtures/double__32_0.50_0 --kernel dense --jit 1;;
-    seg_cli) run pytest_seg_cli 500 $PYT tests/test_gpu_seg.py -k "cli or schedule";;
     multidev) SUP_CHECK_DEVICE=1 run pytest_multidev 800 $PYT tests/test_gpu_multidev.py;;
-    skip_parity) run pytest_skip 600 $PYT tests/test_gpu_parity.py -k "config5 or skip or schedulers";;
-    skip_time) run probe_skip 300 python3 -u tools/probe_skip.py 3;;
-    skip_pmc) run pmc_skip 180 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_WAVES SQ_INSTS_SMEM GRBM_GUI_ACTIVE -d $O/pmc_skip -o run --output-format csv -- python3 tools/probe_skip.py 1;;
     bench_cold) run bench_cold 400 python3 bench.py --steps 1 --warmup 0 --cpu-seconds 0 --also= --configs 0 --pmc 0;;
     gpu_all) run pytest_gpu 1200 $PYT tests -m gpu;;
     smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()";;
