@@ -42,135 +42,16 @@ __device__ __forceinline__ void add_nest(double (&x)[N], cdbl* col, int nb) {
   }
 }
 
-// sparse_step with each 8-row block's column piece loaded right before the
-// block is added (one s_load_dwordx16 and its wait per block) instead of rows
-// 0-31 up front: at most one piece (16 SGPRs) of column data is live, so the
-// unrolled segment below does not spill SGPRs (the up-front form pins up to 96
-// SGPRs at n = 44).  The same operations in the same order as sparse_step.
-template <int N, int B>
-__device__ __forceinline__ void lean_block(double (&x)[N], double (&U)[Blocks<N>::NB + 1], cdbl* col) {
-  typedef const __attribute__((address_space(4))) dbl8 cdbl8;
-  const dbl8 t = ((cdbl8*)col)[B];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (8 * B + i < N) x[(8 * B + i < N) ? 8 * B + i : 0] += t[i];
-  blk_prod<N, B>(x, U);
-}
-
-template <int N, int B>
-__device__ __forceinline__ void lean_flat(double (&x)[N], double (&U)[Blocks<N>::NB + 1], cdbl* col, int nb) {
-  if constexpr (B >= 1) {
-    if (nb > B) lean_block<N, B>(x, U, col);
-    lean_flat<N, B - 1>(x, U, col, nb);
-  }
-}
-
-// Top-down over the blocks, each behind its own uniform branch (a flat
-// sequence, not nested: the nested form made LLVM's structurizer copy x at
-// every join, 210 VGPRs against 119).
-template <int N>
-__device__ __forceinline__ void lean_step(double (&x)[N], double (&U)[Blocks<N>::NB + 1], cdbl* col, int nb) {
-  lean_flat<N, Blocks<N>::NB - 1>(x, U, col, nb);
-  lean_block<N, 0>(x, U, col);
-}
-
-// One step of an aligned segment of 16 Gray steps (kSkipSegBits = 4): state
-// t0 + S, S = 1..15, flips walk bit k = ctz(S) with sign bit (t0 + S) >> (k + 1)
-// — a compile-time constant for k < 3, bit 4 of t0 (ng3) for k = 3 — and
-// adds its term with sign (-1)^S.  The column offset folds into the scalar
-// load's immediate and the block count is the launch's (nbk[k] in an SGPR):
-// no per-step index arithmetic.
-template <int N, int S>
-__device__ __forceinline__ void seg_fixed_step(double (&x)[N], double (&U)[Blocks<N>::NB + 1], const double* colw,
-                                               const int (&nbk)[4], uint32_t ng3, double& acc) {
-  constexpr uint32_t k = (uint32_t)__builtin_ctz(S);
-  constexpr int NP = pad8(N);
-  const uint32_t neg = k < 3 ? (((uint32_t)S >> (k + 1)) & 1u) : ng3;
-  int nb = nbk[k];
-  asm volatile("" : "+s"(nb));
-  nb = __builtin_amdgcn_readfirstlane(nb);  // uniform to LLVM too: scalar branches, no exec masking
-  lean_step<N>(x, U, opaque_c(colw, (2u * k + neg) * NP * 8u), nb);
-  if constexpr (S & 1) acc -= U[0];
-  else acc += U[0];
-}
-
-template <int N, int S = 1>
-__device__ __forceinline__ void seg_fixed_steps(double (&x)[N], double (&U)[Blocks<N>::NB + 1], const double* colw,
-                                                const int (&nbk)[4], uint32_t ng3, double& acc) {
-  if constexpr (S < 16) {
-    seg_fixed_step<N, S>(x, U, colw, nbk, ng3, acc);
-    __builtin_amdgcn_sched_barrier(0);  // keep the next step's column loads after this step
-    seg_fixed_steps<N, S + 1>(x, U, colw, nbk, ng3, acc);
-  }
-}
-
-// The segment start t: with every lane's term zero, the last next-toggle over
-// the lane-uniform rows that are exactly zero and that no walk bit below
-// kSkipSegBits touches (T: none before the chunk ends; t: no such row).
-template <int N>
-__device__ __forceinline__ uint32_t skip_target(const double (&x)[N], uint32_t t, uint32_t T) {
-  uint64_t zm = zero_rows<N>(x) & SUP_KARG(umask);
-  const __attribute__((address_space(4))) uint64_t* rmask =
-      (const __attribute__((address_space(4))) uint64_t*)SUP_KARG(rowmask);
-  uint32_t nx = t;
-  while (zm) {
-    const uint32_t r = (uint32_t)__builtin_ctzll(zm);
-    zm &= zm - 1;
-    uint64_t mm = rmask[r];
-    if (mm & kSkipSegMask) continue;
-    uint32_t tr = T;
-    while (mm) {
-      const uint32_t k = (uint32_t)__builtin_ctzll(mm);
-      mm &= mm - 1;
-      const uint32_t c = next_toggle(t, k);
-      tr = c < tr ? c : tr;
-    }
-    nx = tr > nx ? tr : nx;
-  }
-  return nx;
-}
-
-// Gray move t -> nx: add the differing walk columns in ascending bit order
-// (each to its nblk leading blocks), then re-form every suffix product once.
-// Bit-identical to one step per bit: block b's x is final after the last bit
-// with nblk > b, and that step formed U[b] from it and the final U[b + 1] —
-// the expression suffix_all evaluates on the final x (oracle: e_sparse_step per
-// bit).
-template <int N>
-__device__ __forceinline__ void skip_move(double (&x)[N], double (&U)[Blocks<N>::NB + 1], const WalkParams& p,
-                                          const double* colw, uint32_t t, uint32_t nx) {
-  constexpr int NP = pad8(N);
-  const uint32_t gn = nx ^ (nx >> 1);
-  uint32_t diff = (t ^ (t >> 1)) ^ gn;
-  do {
-    const uint32_t k = (uint32_t)__builtin_ctz(diff);
-    diff &= diff - 1;
-    const uint32_t neg = ((gn >> k) & 1u) ^ 1u;
-    add_nest<N, 0>(x, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_of(p, k));
-  } while (diff);
-  suffix_all<N>(x, U);
-}
-
-// Round 6: the walk goes a whole segment at a time.  The
-// 15 steps inside an aligned 16-step segment flip walk bits 0-3 in a fixed
-// pattern, so they are straight-line code (seg_fixed_steps: constant column
-// offsets, signs and term signs, the four block counts held for the launch);
-// only the step into the next segment has a run-time bit.  Round 5 walked
-// pairs in a loop whose per-pair bookkeeping (bit, sign, block count, offset,
-// exits) kept the CU's scalar unit as busy as the four SIMDs' VALU (21.2
-// scalar against 22.9 vector instructions per visited wave-state, 41 SGPRs
-// spilled and reloaded with v_readlane; profiles/r5/pmc_skip44_searched_map.csv).
-// Policy and arithmetic are round 5's (below), so the bits and visited counts
-// are unchanged: at a segment start with every lane's term zero the wave
-// moves to the last next-toggle of the qualifying zero rows.
-//
 // Round 5.  Round 4's kernel checked every visited
 // state for an all-zero product and jumped from there: 56 scalar against 37
 // vector instructions per visited wave-state (counters,
 // profiles/r4/pmc_skip44_*.csv) — the scalar unit the four SIMDs of a CU
-// share was the bound, and per-state bookkeeping was its load.  Round 5
-// changed the policy instead: it skips whole segments of 2^kSkipSegBits Gray
-// steps (aligned), and walks the others:
+// share was the bound, and per-state bookkeeping was its load (the check, the
+// sign, the loop's exits, the move).  A leaner per-state form of the same
+// policy still measured 59 scalar instructions (profiles/r5).  This kernel
+// changes the policy instead: it skips whole segments of 2^kSkipSegBits Gray
+// steps (aligned), and walks the others with walk_sparse's paired loop, whose
+// scalar work per step is a fraction of a checked step's:
 //   * at a segment start t (and only there) with every lane's term zero, the
 //     lane-uniform rows that are exactly zero and that no walk bit below
 //     kSkipSegBits touches are zero for the whole segment, and until one of
@@ -178,26 +59,24 @@ __device__ __forceinline__ void skip_move(double (&x)[N], double (&U)[Blocks<N>:
 //     (a segment start).  Skipped terms are exactly zero, so the sum is the
 //     per-state walk's (the skips are fewer: the simulation on config 5
 //     visits 27.6 % of the states instead of 21.8 %, tools/probes/skip_sim);
+//   * elsewhere the pair (walk bit 0 with its block count in an SGPR, then
+//     walk bit ctz) steps and accumulates as walk_sparse does;
 //   * the move adds the differing walk columns block-wise and re-forms the
-//     suffix products once (bit-identical to one step per bit, skip_move);
+//     suffix products once (bit-identical to one step per bit, see there);
 //   * the arguments only the zero scan and the chunk end read are loaded
 //     where they are used; U is kept out of LLVM's alloca-to-vector
 //     promotion (Makefile: promoted, the jump and step paths disagreed on its
 //     register layout, 8 v_mov_b64 per visited state).
 // The host twin (engine_cpu.cpp) and the oracle's mirror follow the same
-// segments, so results and visited counts agree bit for bit.  Walks shorter
-// than a segment (m < 4) take the pair loop below, a kernel of its own
-// (SEG = false: one kernel holding both loops needs 222 VGPRs, the segment
-// walk alone 150).
-template <int N, bool SEG>
+// segments, so results and visited counts agree bit for bit.
+template <int N>
 __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
   constexpr int NP = pad8(N);
-  static_assert(kSkipSegBits == 4, "seg_fixed_steps unrolls segments of 16 steps");
   const uint32_t lane = threadIdx.x & 63u;
   const bool lane_valid = lane < (1u << p.L);
   const uint32_t lane_par = __builtin_popcount(lane) & 1u;
   const uint32_t T = 1u << p.m;
-  const int nbk[4] = {nb_of(p, 0), nb_of(p, 1), nb_of(p, 2), nb_of(p, 3)};
+  const int nb0 = nb_of(p, 0);
 
   for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {
     double keep = 0.0;
@@ -213,63 +92,75 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
       const double* colw = p.cols + 2 * p.L * NP;  // walk bit k, sign s: colw + (2k + s) NP
       double acc = U[0];  // state 0
       uint32_t visited = 1;
-      if constexpr (SEG) {
-        for (uint32_t t = 0;;) {  // t: a segment start, its state's term accumulated
-          if (__builtin_amdgcn_ballot_w64(U[0] != 0.0) == 0) {
-            const uint32_t nx = skip_target<N>(x, t, T);
-            if (nx >= T) break;
-            if (nx > t) {
-              skip_move<N>(x, U, p, colw, t, nx);
-              t = nx;
-              ++visited;
-              acc += U[0];  // nx is a segment start: even
-              continue;     // check the new segment start
+      uint32_t u = 1;
+      // state 0 opens a segment: the zero check before its walk (T = 1: state 0 is the chunk)
+      bool check = true;
+      for (; T > 1;) {
+        if (check && __builtin_amdgcn_ballot_w64(U[0] != 0.0) == 0) {
+          // Every lane's term at the segment start t = u - 1 is zero.  A
+          // lane-uniform row that is exactly zero and that no walk bit below
+          // kSkipSegBits touches stays zero for the whole segment and until one of its
+          // walk columns toggles (for the rest of the chunk if it has none):
+          // the product is zero until the last of those toggles over all such
+          // rows, a segment start.  Skipped terms are exactly zero.
+          const uint32_t t = u - 1;
+          uint64_t zm = zero_rows<N>(x) & SUP_KARG(umask);
+          const __attribute__((address_space(4))) uint64_t* rmask =
+              (const __attribute__((address_space(4))) uint64_t*)SUP_KARG(rowmask);
+          uint32_t nx = t;
+          while (zm) {
+            const uint32_t r = (uint32_t)__builtin_ctzll(zm);
+            zm &= zm - 1;
+            uint64_t mm = rmask[r];
+            if (mm & kSkipSegMask) continue;
+            uint32_t tr = T;
+            while (mm) {
+              const uint32_t k = (uint32_t)__builtin_ctzll(mm);
+              mm &= mm - 1;
+              const uint32_t c = next_toggle(t, k);
+              tr = c < tr ? c : tr;
             }
+            nx = tr > nx ? tr : nx;
           }
-          seg_fixed_steps<N>(x, U, colw, nbk, (t >> 4) & 1u, acc);
-          visited += 15u;
-          if (t + 16u >= T) break;
-          const uint32_t v = t + 16u;
-          const uint32_t k = (uint32_t)__builtin_ctz(v);
-          const uint32_t neg = (v >> (k + 1)) & 1u;
-          lean_step<N>(x, U, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_of(p, k));
-          acc += U[0];
-          ++visited;
-          t = v;
+          if (nx >= T) break;
+          if (nx > t) {
+            // Gray move t -> nx: add the differing walk columns in ascending
+            // bit order (each to its nblk leading blocks), then re-form every
+            // suffix product once.  Bit-identical to one step per bit: block
+            // b's x is final after the last bit with nblk > b, and that step
+            // formed U[b] from it and the final U[b + 1] — the expression
+            // suffix_all evaluates on the final x (oracle: e_sparse_step per bit).
+            const uint32_t gn = nx ^ (nx >> 1);
+            uint32_t diff = (t ^ (t >> 1)) ^ gn;
+            do {
+              const uint32_t k = (uint32_t)__builtin_ctz(diff);
+              diff &= diff - 1;
+              const uint32_t neg = ((gn >> k) & 1u) ^ 1u;
+              add_nest<N, 0>(x, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_of(p, k));
+            } while (diff);
+            suffix_all<N>(x, U);
+            u = nx + 1;
+            ++visited;
+            acc += U[0];  // nx is a segment start: even
+            continue;  // check the new segment start
+          }
         }
-      } else {
-        uint32_t u = 1;
-        bool check = true;  // state 0 opens a segment
-        for (; T > 1;) {
-          if (check && __builtin_amdgcn_ballot_w64(U[0] != 0.0) == 0) {
-            const uint32_t t = u - 1;
-            const uint32_t nx = skip_target<N>(x, t, T);
-            if (nx >= T) break;
-            if (nx > t) {
-              skip_move<N>(x, U, p, colw, t, nx);
-              u = nx + 1;
-              ++visited;
-              acc += U[0];
-              continue;
-            }
-          }
-          // the pair u (walk bit 0), u + 1 (walk bit ctz(u + 1)), as walk_sparse
-          {
-            int nbo = nbk[0];
-            asm volatile("" : "+s"(nbo));
-            sparse_step<N>(x, U, opaque_c(colw, ((u >> 1) & 1u) * NP * 8u), nbo);
-          }
-          acc -= U[0];
-          visited += (u + 1 < T) ? 2u : 1u;  // this state, and the next if there is one
-          if (u + 1 >= T) break;
-          const uint32_t v = u + 1;
-          const uint32_t k = (uint32_t)__builtin_ctz(v);
-          const uint32_t neg = (v >> (k + 1)) & 1u;
-          sparse_step<N>(x, U, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_of(p, k));
-          acc += U[0];
-          u += 2;
-          check = (v & kSkipSegMask) == 0;  // v opens a segment
+        // the pair u (walk bit 0), u + 1 (walk bit ctz(u + 1)), as walk_sparse
+        {
+          int nbo = nb0;
+          asm volatile("" : "+s"(nbo));
+          sparse_step<N>(x, U, opaque_c(colw, ((u >> 1) & 1u) * NP * 8u), nbo);
         }
+        acc -= U[0];
+        visited += (u + 1 < T) ? 2u : 1u;  // this state, and the next if there is one
+        if (u + 1 >= T) break;
+        const uint32_t v = u + 1;
+        const uint32_t k = (uint32_t)__builtin_ctz(v);
+        const uint32_t neg = (v >> (k + 1)) & 1u;
+        sparse_step<N>(x, U, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_of(p, k));
+        acc += U[0];
+        u += 2;
+        check = (v & kSkipSegMask) == 0;  // v opens a segment
       }
       if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;
       const double part = wave_sum(lane_valid ? acc : 0.0);
@@ -288,8 +179,7 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
 template <int N, int HI>
 static hipError_t launch_rec(int n, const WalkParams& p, int grid, hipStream_t s) {
   if (n == N) {
-    if (p.m >= kSkipSegBits) hipLaunchKernelGGL((walk_skip<N, true>), dim3(grid), dim3(kBlock), 0, s, p);
-    else hipLaunchKernelGGL((walk_skip<N, false>), dim3(grid), dim3(kBlock), 0, s, p);
+    hipLaunchKernelGGL(walk_skip<N>, dim3(grid), dim3(kBlock), 0, s, p);
     return hipGetLastError();
   }
   if constexpr (N < HI) return launch_rec<N + 1, HI>(n, p, grid, s);
@@ -298,13 +188,7 @@ static hipError_t launch_rec(int n, const WalkParams& p, int grid, hipStream_t s
 
 template <int N, int HI>
 static hipError_t occ_rec(int n, int* blocks_per_cu) {
-  if (n == N) {  // the smaller residency of the two forms (the launch picks one by m)
-    int a = 0, b = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, walk_skip<N, true>, kBlock, 0);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, walk_skip<N, false>, kBlock, 0);
-    *blocks_per_cu = a < b ? a : b;
-    return e;
-  }
+  if (n == N) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_skip<N>, kBlock, 0);
   if constexpr (N < HI) return occ_rec<N + 1, HI>(n, blocks_per_cu);
   return hipErrorInvalidValue;
 }
