@@ -69,6 +69,20 @@ __device__ __forceinline__ void add_nest(double (&x)[N], cdbl* col, int nb) {
 //     register layout, 8 v_mov_b64 per visited state).
 // The host twin (engine_cpu.cpp) and the oracle's mirror follow the same
 // segments, so results and visited counts agree bit for bit.
+//
+// Round 6: the walk goes four steps at a time (walk bits
+// 0, 1, 0, then ctz >= 2), the first three with their block counts in SGPRs
+// held for the launch and their column offsets and signs fixed by the
+// position.  Round 5's pair loop spent 21.1 scalar instructions per visited
+// wave-state on each step's bit, sign, block count and offset, the SALU of
+// the CU as busy as its four SIMDs' VALU; the quad loop issues 14.5 (the
+// same 19.8 fp64 instructions): config 5 --jit -1 779 -> 685 ms
+// (profiles/r6/probe_skip_quad.log, pmc_skip44_quad.csv).  Measured and
+// dropped: eight steps at a time (SGPR spills 72 -> 140, 811 ms), the whole
+// 16-step segment straight-line (SALU 10.7 but 200 SGPR spills and phi copies
+// that doubled the VALU, 1138 ms), and block 0 kept as two half products so a
+// step re-forms only the half it touches (fewer fp64 operations, but 133
+// VGPRs: 3 waves per SIMD 1070 ms, 4 waves with scratch 970 ms).
 template <int N>
 __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
   constexpr int NP = pad8(N);
@@ -76,7 +90,7 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
   const bool lane_valid = lane < (1u << p.L);
   const uint32_t lane_par = __builtin_popcount(lane) & 1u;
   const uint32_t T = 1u << p.m;
-  const int nb0 = nb_of(p, 0);
+  const int nb0 = nb_of(p, 0), nb1 = nb_of(p, 1);
 
   for (uint32_t g = next_chunk(p.counter); (uint64_t)g * p.group < p.chunk_count; g = next_chunk(p.counter)) {
     double keep = 0.0;
@@ -145,21 +159,40 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
             continue;  // check the new segment start
           }
         }
-        // the pair u (walk bit 0), u + 1 (walk bit ctz(u + 1)), as walk_sparse
+        // the quad u (walk bit 0, +), u + 1 (walk bit 1), u + 2 (bit 0, -),
+        // u + 3 (walk bit ctz(u + 3) >= 2); u = 1 mod 4 here (segment starts
+        // are multiples of 16), so walk bit 0's sign is + then - and walk bit
+        // 1's is bit 2 of u + 1; the same steps in the same order as the pairs
         {
           int nbo = nb0;
           asm volatile("" : "+s"(nbo));
-          sparse_step<N>(x, U, opaque_c(colw, ((u >> 1) & 1u) * NP * 8u), nbo);
+          sparse_step<N>(x, U, opaque_c(colw, 0u), nbo);
         }
         acc -= U[0];
-        visited += (u + 1 < T) ? 2u : 1u;  // this state, and the next if there is one
-        if (u + 1 >= T) break;
-        const uint32_t v = u + 1;
+        if (u + 1 >= T) {  // T = 2: the chunk's last state
+          ++visited;
+          break;
+        }
+        {
+          int nbo = nb1;
+          asm volatile("" : "+s"(nbo));
+          sparse_step<N>(x, U, opaque_c(colw, (2u + (((u + 1) >> 2) & 1u)) * NP * 8u), nbo);
+        }
+        acc += U[0];
+        {
+          int nbo = nb0;
+          asm volatile("" : "+s"(nbo));
+          sparse_step<N>(x, U, opaque_c(colw, NP * 8u), nbo);
+        }
+        acc -= U[0];
+        visited += (u + 3 < T) ? 4u : 3u;
+        if (u + 3 >= T) break;
+        const uint32_t v = u + 3;
         const uint32_t k = (uint32_t)__builtin_ctz(v);
         const uint32_t neg = (v >> (k + 1)) & 1u;
         sparse_step<N>(x, U, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_of(p, k));
         acc += U[0];
-        u += 2;
+        u += 4;
         check = (v & kSkipSegMask) == 0;  // v opens a segment
       }
       if (((uint32_t)ga ^ lane_par) & 1u) acc = -acc;
