@@ -17,6 +17,8 @@
 //   * skipped terms are exactly zero (x_r stays exactly 0 until a column of
 //     row r flips), so the sum is unchanged.
 // Rows are prefix-blocked exactly as in walk_sparse.hip.
+#include <cstdlib>
+
 #include "walk_common.hpp"
 #include "walk_zero.hpp"
 #include "kernels.hpp"
@@ -39,6 +41,36 @@ __device__ __forceinline__ void add_nest(double (&x)[N], cdbl* col, int nb) {
       for (int j = 8 * B; j < 8 * B + 8 && j < N; ++j) x[j] += col[j];
       add_nest<N, B + 1>(x, col, nb);
     }
+  }
+}
+
+// nblk of walk bit k read from the kernel arguments where it is used (a
+// scalar load beside the column's): held in SGPRs across the walk, the two
+// packed words were spilled and reloaded with v_readlane on every segment.
+__device__ __forceinline__ int nb_at(uint32_t k) {
+  const uint64_t w = k < 16 ? SUP_KARG(nb_lo) : SUP_KARG(nb_hi);
+  return (int)((w >> ((k & 15u) * 4u)) & 15u);
+}
+
+// LOW = 3 (below): the 15 steps inside an aligned 16-step segment, state
+// t + S flipping walk bit k = ctz(S) with a compile-time block count (one
+// block for walk bits 0-2, two for bit 3: at least each bit's own count, and
+// re-forming a block a column does not touch gives the same values, so the
+// sum is bit-identical) and its sign bit (t + S) >> (k + 1): the position's
+// for k < 3, bit 4 of t (ng3) for k = 3.  Straight-line: no branch, no
+// per-step scalar arithmetic.
+template <int N, int S = 1>
+__device__ __forceinline__ void seg15(double (&x)[N], double (&U)[Blocks<N>::NB + 1], const double* colw,
+                                      uint32_t ng3, double& acc) {
+  if constexpr (S < 16) {
+    constexpr int NP = pad8(N);
+    constexpr uint32_t k = (uint32_t)__builtin_ctz(S);
+    constexpr int nbs = k < 3 ? 1 : 2;
+    const uint32_t neg = k < 3 ? (((uint32_t)S >> (k + 1)) & 1u) : ng3;
+    sparse_step_static<N, (nbs < Blocks<N>::NB ? nbs : Blocks<N>::NB)>(x, U, opaque_c(colw, (2u * k + neg) * NP * 8u));
+    if constexpr (S & 1) acc -= U[0];
+    else acc += U[0];
+    seg15<N, S + 1>(x, U, colw, ng3, acc);
   }
 }
 
@@ -70,21 +102,32 @@ __device__ __forceinline__ void add_nest(double (&x)[N], cdbl* col, int nb) {
 // The host twin (engine_cpu.cpp) and the oracle's mirror follow the same
 // segments, so results and visited counts agree bit for bit.
 //
-// Round 6: the walk goes four steps at a time (walk bits
-// 0, 1, 0, then ctz >= 2), the first three with their block counts in SGPRs
-// held for the launch and their column offsets and signs fixed by the
-// position.  Round 5's pair loop spent 21.1 scalar instructions per visited
-// wave-state on each step's bit, sign, block count and offset, the SALU of
-// the CU as busy as its four SIMDs' VALU; the quad loop issues 14.5 (the
-// same 19.8 fp64 instructions): config 5 --jit -1 779 -> 685 ms
-// (profiles/r6/probe_skip_quad.log, pmc_skip44_quad.csv).  Measured and
-// dropped: eight steps at a time (SGPR spills 72 -> 140, 811 ms), the whole
-// 16-step segment straight-line (SALU 10.7 but 200 SGPR spills and phi copies
-// that doubled the VALU, 1138 ms), and block 0 kept as two half products so a
-// step re-forms only the half it touches (fewer fp64 operations, but 133
-// VGPRs: 3 waves per SIMD 1070 ms, 4 waves with scratch 970 ms).
-template <int N>
-__global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
+// Round 6: round 5's pair loop spent 21.1 scalar
+// instructions per visited wave-state on each step's bit, sign, block count
+// and column offset — the CU's one scalar unit as busy as its four SIMDs'
+// VALU (issue 0.60).  The low walk bits flip in a fixed pattern, and their
+// block counts are the launch's, so the walk is now specialised by form (the
+// host picks the most specialised one the plan's block counts allow,
+// skip_form):
+//   LOW 3  the 15 steps inside an aligned 16-step segment are straight-line
+//          code with compile-time block counts, offsets and signs (seg15);
+//          only the step into the next segment has a run-time bit;
+//   LOW 2  eight steps per iteration, walk bits 0-2 on one block;
+//   LOW 1  four steps per iteration, walk bits 0-1 on one block;
+//   LOW 0  four steps per iteration, every block count at run time.
+// Config 5 (--jit -1, form 3): 779 -> 537 ms, scalar instructions per
+// visited wave-state 21.1 -> 4.9, the same 19.8 fp64 (profiles/r6/
+// probe_skip_forms.log, pmc_skip44_forms.csv; issue 0.87); every form gives
+// the same bits and visited counts (tests/test_gpu_skip_forms.py).  On the
+// way (profiles/r6/probe_skip_*.log): quad loop 685 ms, + one-block low bits
+// 636, + octet 575, + segment 531.  Measured and dropped: an octet loop with
+// run-time block counts (SGPR spills 72 -> 140, 811 ms), the whole segment
+// straight-line with run-time counts (200 SGPR spills and phi copies that
+// doubled the VALU, 1138 ms), block 0 kept as two half products (133 VGPRs:
+// 1070 ms at 3 waves, 970 ms at 4 with scratch).
+template <int N, int LOW>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void walk_skip(WalkParams p) {
+  constexpr bool ONE = LOW >= 1;
   constexpr int NP = pad8(N);
   const uint32_t lane = threadIdx.x & 63u;
   const bool lane_valid = lane < (1u << p.L);
@@ -150,7 +193,7 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
               const uint32_t k = (uint32_t)__builtin_ctz(diff);
               diff &= diff - 1;
               const uint32_t neg = ((gn >> k) & 1u) ^ 1u;
-              add_nest<N, 0>(x, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_of(p, k));
+              add_nest<N, 0>(x, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_at(k));
             } while (diff);
             suffix_all<N>(x, U);
             u = nx + 1;
@@ -163,34 +206,70 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
         // u + 3 (walk bit ctz(u + 3) >= 2); u = 1 mod 4 here (segment starts
         // are multiples of 16), so walk bit 0's sign is + then - and walk bit
         // 1's is bit 2 of u + 1; the same steps in the same order as the pairs
-        {
-          int nbo = nb0;
-          asm volatile("" : "+s"(nbo));
-          sparse_step<N>(x, U, opaque_c(colw, 0u), nbo);
+        if constexpr (LOW == 3) {  // u = t + 1, t a segment start
+          seg15<N>(x, U, colw, (u >> 4) & 1u, acc);
+          visited += 15u;
+          if (u + 15u >= T) break;
+          const uint32_t v = u + 15u;
+          const uint32_t k = (uint32_t)__builtin_ctz(v);
+          const uint32_t neg = (v >> (k + 1)) & 1u;
+          sparse_step<N>(x, U, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_at(k));
+          acc += U[0];
+          ++visited;
+          u += 16u;
+          check = true;  // v opens a segment
+          continue;
         }
+        // ONE (walk bits 0 and 1 touch row block 0 only, as on every sparse
+        // matrix measured): their steps are straight-line, one block
+#define SUP_SKIP_LOW(NBV, OFF)                                                        \
+  if constexpr (ONE) {                                                              \
+    sparse_step_static<N, 1>(x, U, opaque_c(colw, (OFF) * NP * 8u));                \
+  } else {                                                                          \
+    int nbo = (NBV);                                                                \
+    asm volatile("" : "+s"(nbo));                                                   \
+    sparse_step<N>(x, U, opaque_c(colw, (OFF) * NP * 8u), nbo);                     \
+  }
+        SUP_SKIP_LOW(nb0, 0u)
         acc -= U[0];
         if (u + 1 >= T) {  // T = 2: the chunk's last state
           ++visited;
           break;
         }
-        {
-          int nbo = nb1;
-          asm volatile("" : "+s"(nbo));
-          sparse_step<N>(x, U, opaque_c(colw, (2u + (((u + 1) >> 2) & 1u)) * NP * 8u), nbo);
-        }
+        SUP_SKIP_LOW(nb1, 2u + (((u + 1) >> 2) & 1u))
         acc += U[0];
-        {
-          int nbo = nb0;
-          asm volatile("" : "+s"(nbo));
-          sparse_step<N>(x, U, opaque_c(colw, NP * 8u), nbo);
-        }
+        SUP_SKIP_LOW(nb0, 1u)
         acc -= U[0];
+#undef SUP_SKIP_LOW
+        if constexpr (LOW == 2) {
+          // walk bit 2 on block 0 too: the octet u .. u + 7 (u = 1 mod 8 here)
+          if (u + 3 < T) {
+            sparse_step_static<N, 1>(x, U, opaque_c(colw, (4u + (((u + 3) >> 3) & 1u)) * NP * 8u));
+            acc += U[0];
+            sparse_step_static<N, 1>(x, U, opaque_c(colw, 0u));
+            acc -= U[0];
+            sparse_step_static<N, 1>(x, U, opaque_c(colw, 3u * NP * 8u));
+            acc += U[0];
+            sparse_step_static<N, 1>(x, U, opaque_c(colw, NP * 8u));
+            acc -= U[0];
+            visited += (u + 7 < T) ? 8u : 7u;
+            if (u + 7 >= T) break;
+            const uint32_t v = u + 7;
+            const uint32_t k = (uint32_t)__builtin_ctz(v);
+            const uint32_t neg = (v >> (k + 1)) & 1u;
+            sparse_step<N>(x, U, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_at(k));
+            acc += U[0];
+            u += 8;
+            check = (v & kSkipSegMask) == 0;  // v opens a segment
+            continue;
+          }
+        }
         visited += (u + 3 < T) ? 4u : 3u;
         if (u + 3 >= T) break;
         const uint32_t v = u + 3;
         const uint32_t k = (uint32_t)__builtin_ctz(v);
         const uint32_t neg = (v >> (k + 1)) & 1u;
-        sparse_step<N>(x, U, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_of(p, k));
+        sparse_step<N>(x, U, opaque_c(colw, (2u * k + neg) * NP * 8u), nb_at(k));
         acc += U[0];
         u += 4;
         check = (v & kSkipSegMask) == 0;  // v opens a segment
@@ -209,10 +288,32 @@ __global__ __launch_bounds__(kBlock) void walk_skip(WalkParams p) {
   }
 }
 
+// The form a launch takes: the most specialised one whose static block
+// counts cover the walk's own (LOW 3: bits 0-2 one block, bit 3 two; LOW 2:
+// bits 0-2 one; LOW 1: bits 0-1 one; LOW 0: every count at run time).
+// SUP_SKIP_FORM caps it (tests run every form on one matrix: same bits).
+static int skip_form(const WalkParams& p) {
+  static const int cap = [] {
+    const char* e = std::getenv("SUP_SKIP_FORM");
+    return e ? std::atoi(e) : 3;
+  }();
+  auto nbk = [&](int k) { return (int)((p.nb_lo >> (4 * k)) & 15ull); };
+  int form = 0;
+  if (p.m >= 4 && nbk(0) <= 1 && nbk(1) <= 1 && nbk(2) <= 1 && nbk(3) <= 2) form = 3;
+  else if (p.m >= 3 && nbk(0) <= 1 && nbk(1) <= 1 && nbk(2) <= 1) form = 2;
+  else if (p.m >= 2 && nbk(0) <= 1 && nbk(1) <= 1) form = 1;
+  return form < cap ? form : (cap < 0 ? 0 : cap);
+}
+
 template <int N, int HI>
 static hipError_t launch_rec(int n, const WalkParams& p, int grid, hipStream_t s) {
   if (n == N) {
-    hipLaunchKernelGGL(walk_skip<N>, dim3(grid), dim3(kBlock), 0, s, p);
+    switch (skip_form(p)) {
+      case 3: hipLaunchKernelGGL((walk_skip<N, 3>), dim3(grid), dim3(kBlock), 0, s, p); break;
+      case 2: hipLaunchKernelGGL((walk_skip<N, 2>), dim3(grid), dim3(kBlock), 0, s, p); break;
+      case 1: hipLaunchKernelGGL((walk_skip<N, 1>), dim3(grid), dim3(kBlock), 0, s, p); break;
+      default: hipLaunchKernelGGL((walk_skip<N, 0>), dim3(grid), dim3(kBlock), 0, s, p); break;
+    }
     return hipGetLastError();
   }
   if constexpr (N < HI) return launch_rec<N + 1, HI>(n, p, grid, s);
@@ -221,7 +322,16 @@ static hipError_t launch_rec(int n, const WalkParams& p, int grid, hipStream_t s
 
 template <int N, int HI>
 static hipError_t occ_rec(int n, int* blocks_per_cu) {
-  if (n == N) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, walk_skip<N>, kBlock, 0);
+  if (n == N) {  // the smaller residency of the two forms (the launch picks one by the block counts)
+    int occ[4] = {0, 0, 0, 0};
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0], walk_skip<N, 0>, kBlock, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1], walk_skip<N, 1>, kBlock, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[2], walk_skip<N, 2>, kBlock, 0);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[3], walk_skip<N, 3>, kBlock, 0);
+    *blocks_per_cu = occ[0];
+    for (int v : occ) *blocks_per_cu = v < *blocks_per_cu ? v : *blocks_per_cu;
+    return e;
+  }
   if constexpr (N < HI) return occ_rec<N + 1, HI>(n, blocks_per_cu);
   return hipErrorInvalidValue;
 }

@@ -23,6 +23,7 @@ for step in "$@"; do
     rccl_parity) run pytest_rccl_parity 600 $PYT tests/test_gpu_parity.py -k "rccl or schedulers";;
     skip_tests) run pytest_skip 900 $PYT tests/test_gpu_parity.py tests/test_gpu_pinned.py tests/test_gpu_checkpoint.py \
                   tests/test_gpu_multidev.py -k "skip or config5 or p8 or sparse_and_skipper";;
+    skip_forms) run pytest_skip_forms 600 $PYT tests/test_gpu_skip_forms.py tests/test_gpu_fuzz.py tests/test_gpu_maxsize.py;;
     skip_time) run probe_skip 300 python3 -u tools/probes/probe_skip.py 3;;
     skip_pmc) run pmc_skip 180 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_ADD_F64 \
                 SQ_INSTS_VALU_MUL_F64 SQ_WAVES SQ_INSTS_SMEM SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/pmc_skip -o run \
