@@ -785,11 +785,17 @@ int plan_for(const double* A, int n, sup_kernel kernel, const Layout& lay, Plan&
 // searched column map (skip_walk_order) on config 5 int: 19.3 modelled ops per
 // visited state, 10.6 % visited, 0.779 s — 2.31e13 ops/s against the plain
 // walks' 3.7e13 (profiles/r5/probe_skip_searched_map.log; SkipOrder's map:
-// 0.69, round 4's per-state kernel: 0.37).
+// 0.69, round 4's per-state kernel: 0.37).  Round 6's kernel forms
+// (walk_skip.hip: straight-line segments) walk the same states in 0.537 s,
+// 3.35e13 ops/s: 0.90 — the price SkipPer is weighed at; the column search's
+// threshold below keeps round 5's rate, so the plans (and bits) it picks are
+// unchanged.
 static constexpr double kSkipEfficiency = 0.62;
-// SkipPer walks predicted (every state, SkipOrder's map) to take at least
-// this long search their column map for chunk ends (~0.2-0.6 s of host time;
-// config 5: 9.5 s predicted, 0.74 s walked after the search).
+static constexpr double kSkipPriceEfficiency = 0.90;
+// SkipPer walks predicted (every state, SkipOrder's map, at kSkipEfficiency)
+// to take at least this long search their column map for chunk ends
+// (~0.2-0.6 s of host time; config 5: 9.5 s predicted, 0.54 s walked after
+// the search).
 static constexpr double kSkipSearchMinSec = 4.0;
 
 // Fraction of the states the SkipPer plan P evaluates, measured on a fixed
@@ -883,7 +889,7 @@ static int plan_for_uncached(const double* A, int n, sup_kernel kernel, const La
       }
       if (jit < 0 || n < 10 || lay.m < 3) return SUP_OK;
       const double steps = std::ldexp(1.0, n - 1) / std::max(ndev, 1);
-      double skip_cost = walk_cost(P) / (integral ? kSkipEfficiency : 1.0);  // f <= 1
+      double skip_cost = walk_cost(P) / (integral ? kSkipPriceEfficiency : 1.0);  // f <= 1
       const AutoRecord rec(A, n, lay, kernel, ndev, jit, steps * skip_cost / kLaneOpsPerSec);
       if (rec.recorded == 0) return SUP_OK;
       Plan s;
