@@ -572,9 +572,15 @@ static constexpr double kSegStartOps = 2048.0;
 // The segmented walk on the default layout, or on longer wave-chunks where its
 // steps are cheap: a chunk's walk (2^m steps) should be >= 32 chunk starts.
 // Both walks are planned and the one with fewer ops per nominal step, chunk
-// start and chunk skip included, wins.  At least 2^15 chunks remain (16 per
-// resident wave of one GPU).  The layout depends only on the matrix, so every
-// GPU count sums the same chunks (bit-identical results).
+// start and chunk skip included, wins.  At least 2^14 chunks remain (8 per
+// resident wave of one GPU, one per wave of each of 8 GPUs).  Round 6 lowered
+// this from 2^15: config 2 (n = 32) then walks m = 11 instead of 10, 0.555
+// against 0.580 ms (chunk starts 13.5 -> 10.2 % of the wave cycles, queue tail
+// 3.4 -> 7 %; profiles/r6/cfg2_knobs.log), config 3 m = 15 instead of 14
+// (1.905 against 1.92-1.94 ms, profiles/r6/cfg3_m.log).  The layout depends
+// only on the matrix, so every GPU count sums the same chunks (bit-identical
+// results).
+static constexpr int kSegMinChunkBits = 14;
 static uint64_t knob_hash_env();
 
 // Disk key of a segmented-walk plan: what its choices depend on, the layout
@@ -594,7 +600,7 @@ static uint64_t seg_disk_key(const double* A, int n, const Layout& lay) {
   const size_t nn = (size_t)n * n;
   bool integral = true;
   for (size_t i = 0; i < nn && integral; ++i) integral = A[i] == std::floor(A[i]);
-  const int32_t head[] = {5 /* format: bump when the planner changes */, n, lay.L, lay.m, (int32_t)lay.fixed, (int32_t)integral};
+  const int32_t head[] = {6 /* format: bump when the planner changes */, n, lay.L, lay.m, (int32_t)lay.fixed, (int32_t)integral};
   mix(head, sizeof head);
   if (integral) {
     mix(A, nn * sizeof(double));
@@ -639,7 +645,7 @@ static int make_seg_plan(const double* A, int n, const Layout& lay, Plan& P) {
   int rc = plan(lay, P);
   if (rc) return rc;
   if (!lay.fixed) {
-    const int mmax = std::min(lay.m + lay.h - 15, 31);
+    const int mmax = std::min(lay.m + lay.h - kSegMinChunkBits, 31);
     int m2 = lay.m;
     while (m2 < mmax && std::ldexp(walk_cost(P), m2) < 32.0 * kSegStartOps) ++m2;
     if (m2 != lay.m) {
