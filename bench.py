@@ -179,6 +179,12 @@ def pmc_child(args) -> None:
                       "walk_kind": st["walk_kind"]}), flush=True)
 
 
+def kernel_matches(walk: str, name: str) -> bool:
+    """rocprofv3's kernel name against a walk kernel's: `sup::walk_skip<44>`
+    also matches the launched form `sup::walk_skip<44, 3>` (walk_skip.hip)."""
+    return walk in name or (walk.endswith(">") and walk[:-1] + "," in name)
+
+
 def pmc_live(matrix: str, kernel: str, jit: int, prep: int, walk: str):
     """Measured fp64 work of one launch of `walk`: runs this script's
     --pmc-child under `rocprofv3 --pmc` (a child process, --kernel-trace only)
@@ -202,7 +208,7 @@ def pmc_live(matrix: str, kernel: str, jit: int, prep: int, walk: str):
         vals, ns = {}, []
         for f in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
-                if walk in row["Kernel_Name"]:
+                if kernel_matches(walk, row["Kernel_Name"]):
                     vals[row["Counter_Name"]] = vals.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
                     ns.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
         if r.returncode != 0 or not child or "SQ_INSTS_VALU_FMA_F64" not in vals:

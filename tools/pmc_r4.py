@@ -35,7 +35,7 @@ def counters(d, walk=WALK):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         seen = set()
         for r in csv.DictReader(open(f)):
-            if walk in r["Kernel_Name"]:
+            if walk in r["Kernel_Name"] or (walk.endswith(">") and walk[:-1] + "," in r["Kernel_Name"]):
                 vals[r["Counter_Name"]] = vals.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
                 k = (r.get("Dispatch_Id"), r["Start_Timestamp"])
                 if k not in seen:
