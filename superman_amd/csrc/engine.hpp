@@ -303,6 +303,18 @@ hipError_t select_device(int dev);
 // mismatch returns SUP_EHIP.  Off: one branch.
 int check_device(int dev, const char* what);
 uint64_t device_checks_passed();
+// A HIP call whose failure returns SUP_EHIP with the call's text and HIP's message.
+#ifndef SUP_HIP
+#define SUP_HIP(call)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      set_error(std::string(#call) + ": " + hipGetErrorString(e_));                    \
+      return SUP_EHIP;                                                                 \
+    }                                                                                  \
+  } while (0)
+#endif
+
 #define SUP_ON_DEVICE(dev, what)                 \
   do {                                           \
     const int rc_ = check_device((dev), (what)); \
