@@ -204,6 +204,10 @@ def main() -> None:
     if not quick:
         plan += [("double__30_0.50_0", "dense_q", 0, 0), ("int__30_0.50_0", "dense_q", 0, 0),
                  ("double__30_0.20_0", "dense_q", 0, 0), ("int__30_0.20_0", "dense_q", 0, 0),
+                 # round 6: BASELINE config 2's matrix through the reference's -q mode
+                 # (parallel_perman64<__float128,double>, ~15 min on 8 cores): the exact path's
+                 # value at n = 32 against the reference's own quad result
+                 ("double__32_0.50_0", "dense_q", 0, 0),
                  ("double__36_0.20_0", "sparse", 1, 0), ("int__36_0.20_0", "skip", 2, 0),
                  # the metric config (n = 40) and its d = 0.2 companion through the reference's own
                  # parallel_perman64<double,double> (cpu_algos.hpp:761-873): ~55 min each on 8 cores
