@@ -458,6 +458,10 @@ def main():
     # use_pg: the process group exists and every collective below runs (world
     # > 1, or --pg at world 1, which executes the RCCL branch on one GPU)
     use_pg = world > 1 or args.pg
+    # the ranks plan at once: each compiles its budget ladder ahead with helper
+    # processes (one per core up to 16); share the host's cores among them
+    if world > 1 and "SUP_RTC_PROCS" not in os.environ:
+        os.environ["SUP_RTC_PROCS"] = str(max(2, 16 // world))
     if use_pg:
         if env_world is None:  # --pg without a launcher: a one-rank group on this host
             os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
