@@ -391,7 +391,7 @@ int sup_perman_reduced_exact(const void* mat, sup_dtype t, int n, const sup_opts
  * every leaf by the double-double walk, the tree combined (sums, and the
  * scaling factors divided out) in double-double.  The leaf matrices are
  * formed in fp64 as in the reference; the fp64 walk's cancellation, which
- * costs the reduced sum its digits, is gone.  st->leaves = the
+ * costs the reduced sum its digits (HISTORY.md §7), is gone.  st->leaves = the
  * leaf count. */
 int sup_perman_reduced_quad(const void* mat, sup_dtype t, int n, const sup_opts* o, int on_cpu,
                             const sup_reduce_opts* r, double* out_hi, double* out_lo, sup_stats* st);

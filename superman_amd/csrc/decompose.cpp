@@ -11,7 +11,7 @@
 // the reference's order (left child + right child, scale factors divided out
 // column vector first, then row vector).
 //
-// Deliberate differences from the reference:
+// Deliberate differences from the reference (HISTORY.md §7):
 //   * the nonzero test is != 0 (the reference's getRowNnz uses > 0 and skips
 //     negative entries), as everywhere else in this engine;
 //   * all reductions run in fp64 (the reference runs them in the storage type:

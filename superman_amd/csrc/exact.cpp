@@ -335,7 +335,7 @@ int exact_perman(const double* A, int n, const sup_opts& o, bool on_cpu, std::st
 // every coefficient into its leaf matrices (integers stay integers), so
 // perm(A) = sum of the leaf permanents; each leaf is computed exactly and the
 // sum is a big integer (the fp64 combine of the same tree loses every digit on
-// chesapeake, DESIGN.md §7).
+// chesapeake, DESIGN.md §8).
 namespace {
 struct ReducedExact {
   const sup_opts* o;

@@ -1602,7 +1602,7 @@ struct Gen {
       o << "      acc = " << (U.empty() ? dname(0) : dname(0) + " * " + U) << ";\n";
     }
     // two-level lane sum: acc folds into tot after each shared dyn step, so
-    // no sequential sum runs longer than 2^b pairs (error growth)
+    // no sequential sum runs longer than 2^b pairs (error growth, HISTORY.md §3.3 "Lane sum")
     o << "      double tot = 0.0;\n";
     if (trace) o << "      asm volatile(\"\" : \"+v\"(acc));\n      tr_sc += __builtin_amdgcn_s_memtime() - tr_s;\n      ++tr_n;\n";
     o << "      for (uint32_t q = 0; q < " << Q << "u; ++q) {\n";

@@ -131,7 +131,7 @@ def test_gpu_exact_tiny(sup, orc):
 
 def test_gpu_chesapeake_exact_two_ways(sup):
     """chesapeake (n = 39, the matrix whose fp64 -o reduction has no correct digit
-    in the reference or here): the exact permanent from the -o tree
+    in the reference or here, HISTORY.md §7): the exact permanent from the -o tree
     (231 exact leaves, big-integer sum) equals the exact direct walk.  The matrix
     cancels badly: the fp64 direct walk is within the north star's 1e-6, closer
     than the best of the reference's five published runs

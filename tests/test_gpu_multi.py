@@ -3,7 +3,7 @@ ranks (gloo, all on device 0 — the rehearsal form of bench.py --rehearse)
 each plan on their own, agree on the plan fingerprint, walk their contiguous
 shard of wave-chunks with sup_perman_shard (the segmented walk, as the bench
 times it) and combine with the bench's one-slot-per-rank all-reduce.  The
-result equals the single-process walk bit for bit (DESIGN.md §3.5, §4)."""
+result equals the single-process walk bit for bit (DESIGN.md §4, §5)."""
 import os
 import socket
 

@@ -7,7 +7,7 @@ each with its own context (stream, buffers, chunk queue), so the per-device
 threads, their kernels (concurrently on one GPU), the item queue with several
 takers and the host combine all run as they would on four GPUs.  Results must
 equal the one-device walk bit for bit: pieces and queue items are aligned
-subtrees of the one fixed pairwise reduction (DESIGN §3.5, §4).  RCCL (-R)
+subtrees of the one fixed pairwise reduction (DESIGN §4, §5).  RCCL (-R)
 needs distinct physical devices and is refused under such a map."""
 import os
 from contextlib import contextmanager

@@ -83,7 +83,7 @@ def test_gpu_chesapeake_reduced_quad(sup):
     """chesapeake (n = 39 pattern matrix): its exact permanent is 13173481190272
     (two independent exact GPU computations, test_gpu_exact.py).  The fp64 -o
     reduction loses every digit to the fp64 walk's cancellation in its merged
-    leaves (the reference's own -o gives -2.6e24); with
+    leaves (the reference's own -o gives -2.6e24, HISTORY.md §7); with
     double-double leaves and combine, and the integer merges exact, -o -q gives
     the exact value."""
     a = sup.read_matrix(fixture_path("mtx/chesapeake.mtx"))[0]

@@ -12,7 +12,7 @@ Its JSON line must be bit-equal to the run without a process group.  The
 library's own RCCL combine (-p5 / -p6 / -p8 with use_rccl = 2, one
 communicator from ncclCommInitAll) then runs in a process that already holds
 torch's RCCL communicator.  The reference sums its device partials on the
-host (gpu_exact_dense.cu:847-901); DESIGN.md §4."""
+host (gpu_exact_dense.cu:847-901); DESIGN.md §5."""
 import json
 import os
 import socket

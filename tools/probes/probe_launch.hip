@@ -1,5 +1,5 @@
 // probe_launch.hip — what one small call's HIP API sequence costs on this box
-// (the per-call host cost of DESIGN §3.4): launch + sync round trips of tiny
+// (the per-call host cost of HISTORY.md §3.4): launch + sync round trips of tiny
 // kernels with and without timing events, the same sequence as a graph, and
 // waiting by polling mapped host memory instead of hipStreamSynchronize.
 //
