@@ -167,3 +167,28 @@ def test_exact_corpus_integers_consistent():
             n = int(f.readline().split()[0])
         scale = 1 if rec["scale"] == "1" else 10 ** (6 * n)
         assert float(Fraction(int(rec["integer"]), scale)) == ex[name]
+
+
+def test_exact_corpus_vs_reference_quad(golden):
+    """The exact permanents the benchmarked walks are pinned to
+    (tests/golden/exact_corpus.json, this engine's residue walk + CRT) against
+    the reference's own -q mode (parallel_perman64<__float128,double>,
+    rev/cpu_algos.hpp:761-873, compiled from its sources; tests/golden/
+    make_golden.py) wherever the reference ran it: n = 30 and, since round 6,
+    BASELINE config 2's n = 32 matrix (906 s on 8 cores).  The quad results
+    are printed with 17 digits, so they agree with the exact value to within
+    an ulp or two of fp64; the reference's own fp64 result is ~1e-10 away."""
+    import json
+    import os
+
+    from conftest import ROOT
+    ex = json.load(open(os.path.join(ROOT, "tests", "golden", "exact_corpus.json")))
+    checked = 0
+    for name in ("double__30_0.50_0", "double__32_0.50_0"):
+        q = golden[f"{name}|dense_q|r0|b0|t8"]
+        e = ex[name]
+        assert abs(q - e) <= 4.5e-16 * abs(e), (name, q, e)
+        f64 = golden[f"{name}|dense|r0|b0|t8"]
+        assert abs(f64 - e) > 1e-12 * abs(e)  # the reference's fp64 walk is the inaccurate side
+        checked += 1
+    assert checked == 2
