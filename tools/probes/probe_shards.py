@@ -15,6 +15,8 @@ import superman_amd as S  # noqa: E402
 # keeps the shards' skip patterns equal, engine.cpp make_plan)
 cases = [("dense n=40 d=0.5 (bench)", S.read_matrix(os.path.join(ROOT, "tests", "fixtures", "double__40_0.50_0"))[0],
           "dense"),
+         ("config 2 n=32 d=0.5", S.read_matrix(os.path.join(ROOT, "tests", "fixtures", "double__32_0.50_0"))[0], "dense"),
+         ("d=0.2 n=40", S.read_matrix(os.path.join(ROOT, "tests", "fixtures", "double__40_0.20_0"))[0], "dense"),
          ("config 5 n=44 d=0.15 int -p8 -s -r2",
           S.skip_order(S.read_matrix(os.path.join(ROOT, "tests", "fixtures", "synth44_0.15_int"))[0])[0], "skip")]
 for name, a, kern in cases:
@@ -23,6 +25,8 @@ for name, a, kern in cases:
     whole, st = S.perman_shard(a, 0, 1, kernel=kern, jit=1, return_stats=True)
     print(f"{name}: whole walk: kernel {st['kernel_ms']:.1f} ms", flush=True)
     for world in (2, 4, 8):
+        for r in range(world):  # warm each shard's call (its tables, flags)
+            S.perman_shard(a, r, world, kernel=kern, jit=1)
         parts, kms, walls, vis = [], [], [], []
         for r in range(world):
             t = time.perf_counter()
