@@ -290,7 +290,7 @@ void prefetch_compiles(const std::vector<const Plan*>& plans, size_t procs) {
         const std::string name = "seg_" + key_hex(P.jit_key);
         {
           std::lock_guard<std::mutex> g(mu);
-          made.push_back(name + ".hip"), made.push_back(name + ".co"), made.push_back(name + ".log");
+          for (const char* ext : {".hip", ".co", ".co.part", ".log", ".log.part"}) made.push_back(name + ext);
         }
         if (!put(name + ".hip", P.jit_src)) continue;
         std::vector<std::string> args = {helper, lib, dir, name};
