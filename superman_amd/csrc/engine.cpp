@@ -1028,8 +1028,13 @@ struct DeviceCtx {
   double* d_x0dd = nullptr;   // double-double walk: start vector (hi, lo)
   size_t x0dd_cap = 0;
   size_t visited_cap = 0;
+  // queue heads and the fused fold's visited accumulator: head 0 at [0], head 1
+  // at [16] (own 64-byte lines), the accumulator (u64) at byte 128
   unsigned* d_counter = nullptr;
-  bool counter_zero = false;  // d_counter known to be 0 (the last run_range's reduction zeroed it)
+  bool head_zero[2] = {false, false};  // head known to be 0 (zeroed by the last run_range's reduction)
+  int head = 0;                        // run_range's head for the next fused-fold walk
+  unsigned* d_foldcnt = nullptr;       // the fused fold's arrival counters (zero between launches)
+  size_t foldcnt_cap = 0;
   double* d_result = nullptr;
   double* h_result = nullptr;  // pinned host slot (mapped): the reduction writes the result here
   double* m_result = nullptr;  // its device address (nullptr: copy from d_result instead)
@@ -1180,7 +1185,11 @@ static int get_ctx(int dev, DeviceCtx** out) {
     SUP_HIP(hipMalloc(&c->d_x0, SUP_MAX_N * sizeof(double)));
     SUP_HIP(hipMalloc(&c->d_nblk, SUP_MAX_N * sizeof(int)));
     SUP_HIP(hipMalloc(&c->d_rowmask, SUP_MAX_N * sizeof(uint64_t)));
-    SUP_HIP(hipMalloc(&c->d_counter, 64));
+    SUP_HIP(hipMalloc(&c->d_counter, 256));
+    // zeroed on the context's own stream: a null-stream hipMemset is not ordered
+    // with this non-blocking stream and could land after the first walk began
+    SUP_HIP(hipMemsetAsync(c->d_counter, 0, 256, c->stream));
+    SUP_HIP(hipStreamSynchronize(c->stream));
     SUP_HIP(hipMalloc(&c->d_result, 64));
     // the result slot is host memory the device writes directly (mapped,
     // coherent): the reduction's last pass stores the partial there, so no
@@ -1226,6 +1235,16 @@ int warm_devices(int first, int count, int n) {
 static bool result_flag_wait() {
   static const bool on = [] {
     const char* e = std::getenv("SUP_FLAG_WAIT");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+// The fused fold (run_range; walk_common.hpp chunk_store) is the default;
+// SUP_FOLD=0 restores the reduction launches after the walk (A/B: the same
+// tree, the same bits).
+static bool fold_fused() {
+  static const bool on = [] {
+    const char* e = std::getenv("SUP_FOLD");
     return !e || std::atoi(e) != 0;
   }();
   return on;
@@ -1302,9 +1321,24 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
                            hipMemcpyHostToDevice, s));
     c->tables_uid = P.uid;
   }
-  // the queue head: zeroed by the previous run_range's reduction pass, else here
-  if (!c->counter_zero) SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
-  c->counter_zero = false;
+  // The fused fold (walk_common.hpp chunk_store): the walk folds its own
+  // partials, so no reduction launch follows it; its final fold zeroes the
+  // other queue head, which the next such walk takes (the heads alternate: a
+  // wave may still take its last, empty ticket after the fold completes).
+  const bool fused = fold_fused() && !P.lds &&
+                     (P.kind == kWalkSeg || P.kind == kWalkDense || P.kind == kWalkSparse || P.kind == kWalkSkip);
+  if (fused) {
+    // a grown buffer starts at zero (compare capacities: a reallocation may
+    // return the same address, with stale contents)
+    const size_t cap_before = c->foldcnt_cap;
+    if ((rc = ensure(c->d_foldcnt, c->foldcnt_cap, (size_t)pairwise_scratch_size(count)))) return rc;
+    if (c->foldcnt_cap != cap_before) SUP_HIP(hipMemsetAsync(c->d_foldcnt, 0, c->foldcnt_cap * sizeof(unsigned), s));
+  }
+  const int qh = fused ? c->head : 0;
+  unsigned* head = c->d_counter + 16 * qh;
+  // the queue head: zeroed by the previous run_range's reduction, else here
+  if (!c->head_zero[qh]) SUP_HIP(hipMemsetAsync(head, 0, sizeof(unsigned), s));
+  c->head_zero[qh] = false;
 
   int occ_seg = 0, occ_lds = 0;
   if (seg) SUP_ON_DEVICE(c->dev, "segmented-walk module load");
@@ -1361,8 +1395,8 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   p.n = P.n;
   p.umask = P.kind == kWalkSparse ? P.chunk_ends : P.umask;  // walk_sparse: its chunk-end rows
   p.chunk_out = c->d_chunk;
-  p.counter = c->d_counter;
-  p.visited = visited ? c->d_visited : nullptr;
+  p.counter = head;
+  p.visited = visited && !fused ? c->d_visited : nullptr;
   p.group = group;
   p.tail_group = tail_group;
   p.tail_begin = tail_begin;
@@ -1384,6 +1418,22 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     p.trace = d_trace;
   }
 
+  // where the result goes: mapped host memory (no D2H copy; with a sequence
+  // number the host can wait on) unless an -R slot copy takes it from d_result
+  const bool to_host = c->m_result && !slot;
+  const bool direct = to_host && (fused || count > 1);  // (old path: one chunk is a copy, not a pass)
+  const bool flagged = direct && (fused || !visited) && result_flag_wait();
+  const unsigned seq = ++c->flag_seq;
+  if (fused) {
+    p.fold_cnt = c->d_foldcnt;
+    p.fold_lv = c->d_scratch;
+    p.fold_out = to_host ? c->m_result : c->d_result;
+    p.fold_vis = visited ? reinterpret_cast<unsigned long long*>(c->d_counter + 32) : nullptr;
+    p.fold_reset = c->d_counter + 16 * (qh ^ 1);
+    p.fold_flag = flagged ? c->m_flag : nullptr;
+    p.fold_seq = seq;
+  }
+
   SUP_ON_DEVICE(c->dev, "walk launch");
   SUP_HIP(hipEventRecord(c->ev0, s));
   if (seg) {
@@ -1394,30 +1444,55 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     SUP_HIP(launch_walk(P.kind, P.n, p, (int)grid, s));
   }
   SUP_HIP(hipEventRecord(c->ev1, s));
-  // (the -R combine copies d_result into its slot on the device; one chunk is a copy, not a pass)
-  const bool direct = c->m_result && !slot && count > 1;
-  // a direct result also carries a sequence number the host can wait on
-  const bool flagged = direct && !visited && result_flag_wait();
-  const unsigned seq = ++c->flag_seq;
-  SUP_ON_DEVICE(c->dev, "reduction launch");
-  SUP_HIP(launch_pairwise_reduce(c->d_chunk, count, c->d_scratch, direct ? c->m_result : c->d_result, s,
-                                 c->d_counter, flagged ? c->m_flag : nullptr, seq));
-  if (slot) SUP_HIP(hipMemcpyAsync(slot, c->d_result, sizeof(double), hipMemcpyDeviceToDevice, s));
-  if (!direct) SUP_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
-  // visited states: summed on the device, 8 bytes back (beside the result in
-  // the mapped slot: h_result[2])
   unsigned long long* vsum = reinterpret_cast<unsigned long long*>(c->h_result + 2);
-  if (visited) {
-    SUP_HIP(launch_sum_visited(c->d_visited, count, reinterpret_cast<unsigned long long*>(c->d_result + 2), s));
-    SUP_HIP(hipMemcpyAsync(vsum, c->d_result + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+  if (fused) {
+    if (!to_host) {
+      SUP_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
+      if (visited) SUP_HIP(hipMemcpyAsync(vsum, c->d_result + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    }
+  } else {
+    // (the -R combine copies d_result into its slot on the device; one chunk is a copy, not a pass)
+    SUP_ON_DEVICE(c->dev, "reduction launch");
+    SUP_HIP(launch_pairwise_reduce(c->d_chunk, count, c->d_scratch, direct ? c->m_result : c->d_result, s, head,
+                                   flagged ? c->m_flag : nullptr, seq));
+    if (!direct) SUP_HIP(hipMemcpyAsync(c->h_result, c->d_result, sizeof(double), hipMemcpyDeviceToHost, s));
+    // visited states: summed on the device, 8 bytes back (beside the result in
+    // the mapped slot: h_result[2])
+    if (visited) {
+      SUP_HIP(launch_sum_visited(c->d_visited, count, reinterpret_cast<unsigned long long*>(c->d_result + 2), s));
+      SUP_HIP(hipMemcpyAsync(vsum, c->d_result + 2, sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    }
   }
+  if (slot) SUP_HIP(hipMemcpyAsync(slot, c->d_result, sizeof(double), hipMemcpyDeviceToDevice, s));
   // spin on the flag only where the walk is predicted to end within the spin
   // window (cost model on this device's CUs; a longer walk blocks in the
   // stream sync at once instead of holding a host core for 2 ms)
   const double predicted_ms = std::ldexp((double)count, P.lay.L + P.lay.m) * walk_cost_eff(P) / kLaneOpsPerSec *
                               1e3 * (256.0 / std::max(1, c->cus));
   if (!flagged || predicted_ms > kFlagSpinMs || !wait_flag(c->h_flag, seq)) SUP_HIP(hipStreamSynchronize(s));
-  c->counter_zero = count > 1;  // the reduction's first pass zeroed it (one chunk: a copy, no pass)
+  if (fused) {  // the final fold zeroed the other head
+    c->head_zero[qh ^ 1] = true;
+    c->head = qh ^ 1;
+    if (std::getenv("SUP_FOLD_CHECK")) {  // debugging: every arrival counter back at zero
+      SUP_HIP(hipStreamSynchronize(s));
+      std::vector<unsigned> cc(c->foldcnt_cap);
+      SUP_HIP(hipMemcpy(cc.data(), c->d_foldcnt, cc.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+      unsigned hd[64];
+      SUP_HIP(hipMemcpy(hd, c->d_counter, 256, hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < cc.size(); ++i)
+        if (cc[i]) {
+          std::fprintf(stderr, "SUP_FOLD_CHECK: counter %zu = %u after a fused walk (kind %d n %d count %llu group %u tail %u/%llu)\n",
+                       i, cc[i], (int)P.kind, P.n, (unsigned long long)count, group, tail_group, (unsigned long long)tail_begin);
+          break;
+        }
+      std::fprintf(stderr, "SUP_FOLD_CHECK: kind %d n %d count %llu grid %llu heads %u %u vis %llu result %.17g\n", (int)P.kind,
+                   P.n, (unsigned long long)count, (unsigned long long)grid, hd[0], hd[16],
+                   *reinterpret_cast<unsigned long long*>(hd + 32), *c->h_result);
+    }
+  } else {
+    c->head_zero[0] = count > 1;  // the reduction's first pass zeroed it (one chunk: a copy, no pass)
+  }
+
   float ms = 0.f;
   hipError_t ee = hipEventElapsedTime(&ms, c->ev0, c->ev1);
   if (ee == hipErrorNotReady) {  // (after a flag wait the walk is done; its event may not show it yet)
@@ -1516,7 +1591,7 @@ int run_range_batch(int dev, const std::vector<const Plan*>& plans, std::vector<
   SUP_HIP(hipMemcpyAsync(c->d_batch, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemcpyAsync(c->d_desc, desc.data(), K * sizeof(LeafDesc), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
-  c->counter_zero = false;  // this walk leaves the queue head nonzero
+  c->head_zero[0] = false;  // this walk leaves queue head 0 nonzero
   int& occ = c->occ_batch[P0.kind == kWalkSparse][P0.n];
   if (occ == 0) {
     int b = 0;
@@ -1596,7 +1671,7 @@ int run_range_exact(int dev, const Plan& P, int group, uint64_t c0, uint64_t c1,
   SUP_HIP(hipMemcpyAsync(c->d_cols, P.cols.data(), P.cols.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemcpyAsync(c->d_x0, P.x0.data(), P.x0.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
-  c->counter_zero = false;  // this walk leaves the queue head nonzero
+  c->head_zero[0] = false;  // this walk leaves queue head 0 nonzero
   WalkParams p{};
   p.cols = c->d_cols;
   p.x0 = c->d_x0;
@@ -1668,7 +1743,7 @@ int run_range_dd(int dev, const Plan& P, const std::vector<double>& x0dd, uint64
   SUP_HIP(hipMemcpyAsync(c->d_cols, P.cols.data(), P.cols.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemcpyAsync(c->d_x0dd, x0dd.data(), x0dd.size() * sizeof(double), hipMemcpyHostToDevice, s));
   SUP_HIP(hipMemsetAsync(c->d_counter, 0, sizeof(unsigned), s));
-  c->counter_zero = false;  // this walk leaves the queue head nonzero
+  c->head_zero[0] = false;  // this walk leaves queue head 0 nonzero
   WalkParams p{};
   p.cols = c->d_cols;
   p.x0 = c->d_x0dd;

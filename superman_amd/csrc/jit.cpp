@@ -1658,11 +1658,7 @@ struct Gen {
     o << "    __builtin_amdgcn_wave_barrier();\n";
     o << "    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n";
     o << "    const uint32_t lane = SUP_LANE();\n";
-    o << "    const uint64_t a = base + lane;\n";
-    o << "    if (lane < len && a < p.chunk_count) {\n";
-    o << "      p.chunk_out[a] = s_keep[wv][lane];\n";
-    o << "      if (p.visited) p.visited[a] = s_vkeep[wv][lane];\n";
-    o << "    }\n";
+    o << "    chunk_store(base, len, s_keep[wv][lane], s_vkeep[wv][lane]);\n";
     o << "    __builtin_amdgcn_wave_barrier();\n";
     o << "  }\n";
     if (trace)

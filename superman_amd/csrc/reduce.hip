@@ -11,28 +11,9 @@
 
 namespace sup {
 
-__global__ __launch_bounds__(kBlock) void pairwise64_pass(const double* __restrict__ in, uint64_t count,
-                                                          double* __restrict__ out, uint64_t groups,
-                                                          unsigned int* reset, unsigned int* flag, unsigned seq) {
-  const uint64_t g = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  const uint32_t lane = threadIdx.x & 63u;
-  if (reset && blockIdx.x == 0 && threadIdx.x == 0) *reset = 0u;  // the walk before this pass is done with it
-  if (g >= groups) return;  // whole wave exits together (g is wave-uniform)
-  const uint64_t i = g * 64u + lane;
-  const double v = (i < count) ? in[i] : 0.0;
-  const double s = wave_sum(v);
-  if (lane == 0) {
-    out[g] = s;
-    if (flag) {  // the last pass (one group): the call's result, then its sequence number
-      __threadfence_system();
-      __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-
 // One 64-way pass over each of nseg segments of `count` values: group g of
 // segment i reads that segment's values [64 g, 64 g + 64) (zero past its
-// end), the groups of one call to pairwise64_pass on the segment alone.
+// end), the groups of one 64-way pass over the segment alone.
 __global__ __launch_bounds__(kBlock) void pairwise64_pass_seg(const double* __restrict__ in, uint64_t count,
                                                               double* __restrict__ out, uint64_t groups,
                                                               uint64_t nseg) {
@@ -46,26 +27,40 @@ __global__ __launch_bounds__(kBlock) void pairwise64_pass_seg(const double* __re
   if (lane == 0) out[seg * groups + g] = s;
 }
 
+// The reduction kernels run 16 waves per block and issue every load of a wave
+// before its first butterfly: a pass is one memory latency, not one per group
+// (round 6: config 2's 2^14 partials took 9.8 us in 4-wave blocks that folded
+// 16 groups one after another, then a second launch).
+constexpr int kRedBlock = 1024;
+constexpr int kRedWaves = kRedBlock / 64;
+// pairwise_small: up to 16 level-1 groups per wave, so one block takes
+// count <= 16 * 16 * 64 = 2^14 values through every level.
+constexpr int kSmallGroups = 16;
+constexpr uint64_t kSmallMax = (uint64_t)kRedWaves * kSmallGroups * 64u;
+
 // Two 64-way levels in one launch: block b folds level-1 groups
 // [64 b, 64 b + 64) (each group = 64 inputs, zero past `count`, folded by one
-// wave as pairwise64_pass folds it) and then those 64 group sums (zero past
-// the last group) as the next pairwise64_pass would: out[b] is bit-identical
-// to two consecutive pairwise64_pass launches (round 4: half the launches).
-__global__ __launch_bounds__(kBlock) void pairwise4096_pass(const double* __restrict__ in, uint64_t count,
-                                                            double* __restrict__ out, uint64_t groups1,
-                                                            unsigned int* reset, unsigned int* flag, unsigned seq) {
+// wave's butterfly) and then those 64 group sums (zero past the last group):
+// out[b] is two consecutive 64-way levels of the tree.
+__global__ __launch_bounds__(kRedBlock) void pairwise4096_pass(const double* __restrict__ in, uint64_t count,
+                                                               double* __restrict__ out, uint64_t groups1,
+                                                               unsigned int* reset, unsigned int* flag, unsigned seq) {
+  constexpr int kPer = 64 / kRedWaves;  // level-1 groups per wave
   __shared__ double g1[64];
   const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   if (reset && blockIdx.x == 0 && threadIdx.x == 0) *reset = 0u;
   const uint64_t base = (uint64_t)blockIdx.x * 64u;
-  for (uint32_t k = w; k < 64u; k += kWavesPerBlock) {
-    const uint64_t g = base + k;  // level-1 group
-    double v = 0.0;
-    if (g < groups1) {
-      const uint64_t i = g * 64u + lane;
-      v = wave_sum((i < count) ? in[i] : 0.0);
-    }
-    if (lane == 0) g1[k] = v;
+  double v[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {  // every load first
+    const uint64_t g = base + w + (uint64_t)k * kRedWaves, i = g * 64u + lane;
+    v[k] = (g < groups1 && i < count) ? in[i] : 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const uint32_t j = w + (uint32_t)k * kRedWaves;
+    const double s = (base + j < groups1) ? wave_sum(v[k]) : 0.0;
+    if (lane == 0) g1[j] = s;
   }
   __syncthreads();
   if (w == 0) {
@@ -76,6 +71,53 @@ __global__ __launch_bounds__(kBlock) void pairwise4096_pass(const double* __rest
         __threadfence_system();
         __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
+    }
+  }
+}
+
+// Every remaining level of count <= kSmallMax values (count >= 2) in one block:
+// level 1 (64-way groups, zero past `count`), then each next level of
+// 64-way group sums (zero past the level's end) until one value is left —
+// bit-identical to the passes launch_pairwise_reduce ran before round 6.
+__global__ __launch_bounds__(kRedBlock) void pairwise_small(const double* __restrict__ in, uint64_t count,
+                                                            double* __restrict__ out, unsigned int* reset,
+                                                            unsigned int* flag, unsigned seq) {
+  __shared__ double lv[kRedWaves * kSmallGroups];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  if (reset && threadIdx.x == 0) *reset = 0u;
+  uint32_t cnt = (uint32_t)((count + 63u) / 64u);  // level-1 groups
+  double v[kSmallGroups];
+#pragma unroll
+  for (int k = 0; k < kSmallGroups; ++k) {  // every load first
+    const uint64_t i = (uint64_t)(w + (uint32_t)k * kRedWaves) * 64u + lane;
+    v[k] = i < count ? in[i] : 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < kSmallGroups; ++k) {
+    const uint32_t g = w + (uint32_t)k * kRedWaves;
+    if (g < cnt) {  // wave-uniform
+      const double s = wave_sum(v[k]);
+      if (lane == 0) lv[g] = s;
+    }
+  }
+  __syncthreads();
+  while (cnt > 1) {  // the next levels: at most 256 -> 4 -> 1 (block-uniform)
+    const uint32_t groups = (cnt + 63u) / 64u;
+    double s = 0.0;
+    if (w < groups) {
+      const uint32_t i = w * 64u + lane;
+      s = wave_sum(i < cnt ? lv[i] : 0.0);
+    }
+    __syncthreads();  // every read of this level before any write
+    if (w < groups && lane == 0) lv[w] = s;
+    __syncthreads();
+    cnt = groups;
+  }
+  if (threadIdx.x == 0) {
+    out[0] = lv[0];
+    if (flag) {
+      __threadfence_system();
+      __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -96,33 +138,19 @@ hipError_t launch_pairwise_reduce(const double* in, uint64_t count, double* scra
   const double* src = in;
   double* dst = scratch;
   unsigned int* reset = reset_counter;  // zeroed by the first pass
-  while (count > 1) {
-    const uint64_t groups = (count + 63) / 64;
-    if (groups > 1) {  // two levels at once
-      const uint64_t groups2 = (groups + 63) / 64;
-      double* target = (groups2 == 1) ? out : dst;
-      hipLaunchKernelGGL(pairwise4096_pass, dim3((unsigned)groups2), dim3(kBlock), 0, s, src, count, target, groups,
-                         reset, groups2 == 1 ? flag : nullptr, seq);
-      reset = nullptr;
-      hipError_t e = hipGetLastError();
-      if (e != hipSuccess) return e;
-      src = target;
-      dst = target + groups2;
-      count = groups2;
-      continue;
-    }
-    const uint64_t blocks = (groups + kWavesPerBlock - 1) / kWavesPerBlock;
-    double* target = (groups == 1) ? out : dst;
-    hipLaunchKernelGGL(pairwise64_pass, dim3((unsigned)blocks), dim3(kBlock), 0, s, src, count, target, groups, reset,
-                       groups == 1 ? flag : nullptr, seq);
+  while (count > kSmallMax) {  // two levels per launch; leaves > 2^14 / 4096 >= 5 values
+    const uint64_t groups = (count + 63) / 64, groups2 = (groups + 63) / 64;
+    hipLaunchKernelGGL(pairwise4096_pass, dim3((unsigned)groups2), dim3(kRedBlock), 0, s, src, count, dst, groups,
+                       reset, nullptr, seq);
     reset = nullptr;
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    src = target;
-    dst = target + groups;
-    count = groups;
+    src = dst;
+    dst += groups2;
+    count = groups2;
   }
-  return hipSuccess;
+  hipLaunchKernelGGL(pairwise_small, dim3(1), dim3(kRedBlock), 0, s, src, count, out, reset, flag, seq);
+  return hipGetLastError();
 }
 
 hipError_t launch_pairwise_reduce_seg(const double* in, uint64_t count, uint64_t nseg, double* scratch, double* out,

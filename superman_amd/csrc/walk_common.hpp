@@ -302,4 +302,109 @@ __device__ __forceinline__ void chunk_start(double (&x)[N], const WalkParams& p,
     add_col_masked<N>(x, opaque_c(p.cols, (2u * e) * NP * 8u), (lane >> e) & 1u);
 }
 
+// A kernel argument read where it is used: a scalar load from the kernarg
+// segment through an opaque base, so the value is not held in SGPRs across the
+// walk (the register allocator spilled such values to VGPR lanes and reloaded
+// them with v_readlane on every visited state).  Kernels whose first argument
+// is their WalkParams only.
+template <class T>
+__device__ __forceinline__ T karg_at(uint32_t offset) {
+  uint64_t a = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(a));
+  return *(const __attribute__((address_space(4))) T*)(a + offset);
+}
+#define SUP_KARG(field) karg_at<decltype(WalkParams::field)>((uint32_t)__builtin_offsetof(WalkParams, field))
+
+// ------------------------------------------------------------ the fused fold --
+// A value handed to another wave (any CU, any XCD: the XCDs' L2s are not
+// coherent) goes through 8-byte agent-scope atomics on both sides, which are
+// performed at the memory side (MI355X_MICROARCH.md, inter-workgroup
+// visibility: "8-B agent atomics both sides"), and the publishing wave waits
+// for them (vmcnt(0)) before its arrival is counted.
+__device__ __forceinline__ void fold_publish(double* a, double v) {
+  (void)__hip_atomic_exchange((unsigned long long*)a, __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double fold_fetch(double* a) {
+  return __builtin_bit_cast(double, __hip_atomic_fetch_or((unsigned long long*)a, 0ull, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void fold_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// The wave's chunk group [a0, a0 + len) leaves the wave: lane l < len holds
+// chunk a0 + l's partial (keep) and walked states (vkeep).  Called by the
+// whole wave.  Without fold_cnt the partials are stored for
+// launch_pairwise_reduce.  With it (round 6) the walk folds them itself into
+// exactly that tree — 64-way levels over the chunk index, zero padded, one
+// wave butterfly per group — each group formed by the wave whose arrival
+// completes it (one counter per group: the last arriver, told by the value
+// its atomic add returns, reads the group's values and publishes their sum
+// one level up); the wave completing the root writes the result, the visited
+// sum and the host's sequence flag, and zeroes the next launch's queue head.
+// No reduction launch follows the walk.  A group may be completed by any
+// wave; its sum is the same bits either way.
+__device__ __forceinline__ void chunk_store(uint64_t a0, uint32_t len, double keep, uint32_t vkeep) {
+  const uint32_t lane = __lane_id();
+  const uint64_t count = SUP_KARG(chunk_count);
+  if (a0 + len > count) len = (uint32_t)(count - a0);
+  unsigned int* cnt = SUP_KARG(fold_cnt);
+  if (!cnt) {
+    if (lane < len) {
+      SUP_KARG(chunk_out)[a0 + lane] = keep;
+      unsigned int* vis = SUP_KARG(visited);
+      if (vis) vis[a0 + lane] = vkeep;
+    }
+    return;
+  }
+  double* src = SUP_KARG(chunk_out);
+  if (lane < len) fold_publish(src + a0 + lane, keep);
+  unsigned long long* vacc = SUP_KARG(fold_vis);
+  if (vacc) {  // walked states: an exact integer sum, any order
+    unsigned long long v = lane < len ? (unsigned long long)vkeep : 0ull;
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) (void)__hip_atomic_fetch_add(vacc, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  fold_drain();  // every value above performed before this wave's arrival counts
+  double s = __shfl(keep, 0, 64);  // one chunk: the partial itself (no level)
+  if (count > 1) {
+    double* lv = SUP_KARG(fold_lv);
+    uint64_t cv = count, idx = a0;
+    uint32_t arrive = len;
+    for (;;) {  // wave-uniform throughout
+      const uint64_t g = idx >> 6, groups = (cv + 63u) >> 6;
+      const uint64_t rest = cv - 64u * g;
+      const uint32_t target = rest < 64u ? (uint32_t)rest : 64u;
+      uint32_t old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(cnt + g, arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = __builtin_amdgcn_readfirstlane(old);
+      if (old + arrive != target) return;  // another wave completes this group
+      if (lane == 0) __hip_atomic_store(cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+      s = wave_sum(lane < target ? fold_fetch(src + 64u * g + lane) : 0.0);
+      if (groups == 1) break;  // the root
+      if (lane == 0) fold_publish(lv + g, s);
+      fold_drain();
+      src = lv;
+      lv += groups;
+      cnt += groups;
+      cv = groups;
+      idx = g;
+      arrive = 1;
+    }
+  }
+  if (lane == 0) {
+    double* res = SUP_KARG(fold_out);
+    res[0] = s;
+    if (vacc)
+      ((unsigned long long*)res)[2] = __hip_atomic_exchange(vacc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned int* reset = SUP_KARG(fold_reset);
+    if (reset) __hip_atomic_store(reset, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned int* flag = SUP_KARG(fold_flag);
+    if (flag) {
+      __threadfence_system();
+      fold_drain();  // (the compiler may drop the fence's own wait: MI355X_MICROARCH.md, compiler hazard)
+      __hip_atomic_store(flag, SUP_KARG(fold_seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 }  // namespace sup

@@ -56,9 +56,8 @@ __global__ __launch_bounds__(kBlock) void walk_dense(WalkParams p) {
     const double part = wave_sum(lane_valid ? acc : 0.0);
     keep = (lane == j) ? part : keep;
    }
-   // one 64-byte store per group (8 lanes x 8 B)
-   const uint64_t a = (uint64_t)g * p.group + lane;
-   if (lane < (uint32_t)p.group && a < p.chunk_count) p.chunk_out[a] = keep;
+   // one 64-byte store per group (8 lanes x 8 B), or the fused fold
+   chunk_store((uint64_t)g * p.group, (uint32_t)p.group, keep, 0u);
   }
 }
 

@@ -55,6 +55,22 @@ struct WalkParams {
   // stamps at entry and exit, chunks walked, shader cycles spent in chunk
   // starts; nullptr (and never written) otherwise
   unsigned long long* trace;
+  // The fused fold (walk_common.hpp chunk_store; fold_cnt == nullptr: the
+  // partials go to chunk_out and launch_pairwise_reduce folds them after the
+  // walk).  fold_cnt: one arrival counter per 64-group of every level, zero
+  // between launches (the group's last arriver resets it); fold_lv: the
+  // level values; fold_out: [0] the result, [2] the visited sum (u64);
+  // fold_vis: the visited accumulator (zero between launches) or nullptr;
+  // fold_reset: the next launch's queue head, zeroed by the final fold;
+  // fold_flag: fold_seq is stored there (system scope) after the result.
+  unsigned int* fold_cnt;
+  double* fold_lv;
+  double* fold_out;
+  unsigned long long* fold_vis;
+  unsigned int* fold_reset;
+  unsigned int* fold_flag;
+  unsigned int fold_seq;
+  unsigned int pad4_;
 };
 
 // Exact path (walk_exact.hip): residues of the walk's terms modulo up to

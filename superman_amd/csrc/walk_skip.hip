@@ -279,12 +279,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
       keep = (lane == j) ? part : keep;
       vkeep = (lane == j) ? visited : vkeep;
     }
-    const uint64_t a = (uint64_t)g * p.group + lane;
-    if (lane < (uint32_t)p.group && a < p.chunk_count) {
-      SUP_KARG(chunk_out)[a] = keep;
-      unsigned int* vis = SUP_KARG(visited);
-      if (vis) vis[a] = vkeep;
-    }
+    chunk_store((uint64_t)g * SUP_KARG(group), SUP_KARG(group), keep, vkeep);
   }
 }
 

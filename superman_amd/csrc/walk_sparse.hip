@@ -80,8 +80,7 @@ __global__ __launch_bounds__(kBlock) void walk_sparse(WalkParams p) {
       const double part = wave_sum(lane_valid ? acc : 0.0);
       keep = (lane == j) ? part : keep;
     }
-    const uint64_t a = (uint64_t)g * p.group + lane;
-    if (lane < (uint32_t)p.group && a < p.chunk_count) p.chunk_out[a] = keep;
+    chunk_store((uint64_t)g * p.group, (uint32_t)p.group, keep, 0u);
   }
 }
 

@@ -6,18 +6,6 @@
 
 namespace sup {
 
-// A kernel argument read where it is used: a scalar load from the kernarg
-// segment through an opaque base, so the value is not held in SGPRs across the
-// walk (the register allocator spilled such values to VGPR lanes and reloaded
-// them with v_readlane on every visited state).
-template <class T>
-__device__ __forceinline__ T karg_at(uint32_t offset) {
-  uint64_t a = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(a));
-  return *(const __attribute__((address_space(4))) T*)(a + offset);
-}
-#define SUP_KARG(field) karg_at<decltype(WalkParams::field)>((uint32_t)__builtin_offsetof(WalkParams, field))
-
 // Zero test of every row, one bit per row: a lane-uniform row holds the same
 // value on every lane, so its ballot is 0 or all ones and bit r of it stands
 // for lane 0 (rows outside the caller's lane-uniform mask are dropped by the
