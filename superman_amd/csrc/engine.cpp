@@ -1375,8 +1375,13 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     tail_group = std::max(1u, group / 4);
     if (const char* e = std::getenv("SUP_WALK_TAIL"))  // experiments: tail group (0 = no tail phase)
       tail_group = std::min(group, (unsigned)std::max(0, std::atoi(e)));
-    const uint64_t tail = 2 * res_waves * group;
-    tail_begin = count > tail ? (count - tail) / group * group : 0;
+    if (tail_group) {
+      tail_group = 1u << (31 - __builtin_clz(tail_group));  // a power of two
+      const uint64_t tail = 2 * res_waves * group;
+      // on a multiple of 64 (so of the group): no 64-group of the fused fold
+      // mixes group sizes (walk_common.hpp chunk_store)
+      tail_begin = count > tail ? (count - tail) / 64 * 64 : 0;
+    }
   }
   const uint64_t waves_needed = (count + group - 1) / group;  // one chunk group per wave at a time
   uint64_t grid = (waves_needed + wpb - 1) / wpb;

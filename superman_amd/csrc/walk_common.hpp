@@ -346,6 +346,7 @@ __device__ __forceinline__ void fold_drain() { asm volatile("s_waitcnt vmcnt(0)"
 __device__ __forceinline__ void chunk_store(uint64_t a0, uint32_t len, double keep, uint32_t vkeep) {
   const uint32_t lane = __lane_id();
   const uint64_t count = SUP_KARG(chunk_count);
+  const uint32_t nominal = len;  // the group's size (a power of two, a0 a multiple of it)
   if (a0 + len > count) len = (uint32_t)(count - a0);
   unsigned int* cnt = SUP_KARG(fold_cnt);
   if (!cnt) {
@@ -357,7 +358,17 @@ __device__ __forceinline__ void chunk_store(uint64_t a0, uint32_t len, double ke
     return;
   }
   double* src = SUP_KARG(chunk_out);
-  if (lane < len) fold_publish(src + a0 + lane, keep);
+  // The group's lowest tree levels inside the wave: it publishes one value,
+  // the subtree sum of its `nominal` chunks (zero past the end) — the same
+  // butterfly steps a 64-lane fold takes over them: the same bits — at
+  // src[a0 / nominal].  A 64-group holds groups of one size (the host starts
+  // the tail phase on a multiple of 64), so its level-1 fold reads 64 / size
+  // values: the groups', or the tail groups' from tail_begin on.
+  {
+    double v = lane < len ? keep : 0.0;
+    for (uint32_t o = 1; o < nominal; o <<= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) fold_publish(src + a0 / nominal, v);
+  }
   unsigned long long* vacc = SUP_KARG(fold_vis);
   if (vacc) {  // walked states: an exact integer sum, any order
     unsigned long long v = lane < len ? (unsigned long long)vkeep : 0ull;
@@ -370,6 +381,7 @@ __device__ __forceinline__ void chunk_store(uint64_t a0, uint32_t len, double ke
     double* lv = SUP_KARG(fold_lv);
     uint64_t cv = count, idx = a0;
     uint32_t arrive = len;
+    uint32_t sub = (idx & ~63ull) >= SUP_KARG(tail_begin) ? SUP_KARG(tail_group) : SUP_KARG(group);
     for (;;) {  // wave-uniform throughout
       const uint64_t g = idx >> 6, groups = (cv + 63u) >> 6;
       const uint64_t rest = cv - 64u * g;
@@ -379,7 +391,11 @@ __device__ __forceinline__ void chunk_store(uint64_t a0, uint32_t len, double ke
       old = __builtin_amdgcn_readfirstlane(old);
       if (old + arrive != target) return;  // another wave completes this group
       if (lane == 0) __hip_atomic_store(cnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-      s = wave_sum(lane < target ? fold_fetch(src + 64u * g + lane) : 0.0);
+      // the rest of the group's tree: 64 / sub values (zero past the level's end)
+      const uint32_t nsub = 64u / sub, real = (target + sub - 1u) / sub;
+      double x = lane < real ? fold_fetch(src + (64u * g) / sub + lane) : 0.0;
+      for (uint32_t o = 1; o < nsub; o <<= 1) x += __shfl_xor(x, o, 64);
+      s = __shfl(x, 0, 64);
       if (groups == 1) break;  // the root
       if (lane == 0) fold_publish(lv + g, s);
       fold_drain();
@@ -389,6 +405,7 @@ __device__ __forceinline__ void chunk_store(uint64_t a0, uint32_t len, double ke
       cv = groups;
       idx = g;
       arrive = 1;
+      sub = 1;
     }
   }
   if (lane == 0) {
