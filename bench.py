@@ -505,8 +505,11 @@ def main():
         keys = check_plans_agree(S.plan_key(a, kernel, jit=jit, gpu_num=world, device_id=dev), rank, world, tdev)
         plan_keys.append([hex(k) for k in keys])
 
-        # the same C-ABI call every step (sup_perman_shard), its arguments built once
-        call = S.ShardCall(a, rank, world, kernel=kernel, device_id=dev, jit=jit)
+        # the same C-ABI call every step (sup_perman_shard), its arguments built
+        # once; its walk's HIP events are read after the timed steps
+        # (sup_opts.timing = 0: a call returns when its result is there instead
+        # of waiting for the end event too)
+        call = S.ShardCall(a, rank, world, kernel=kernel, device_id=dev, jit=jit, timing=False)
 
         def step():
             part, k_ms = call()
@@ -530,20 +533,22 @@ def main():
                 t = torch.tensor([steps], dtype=torch.float64, device=tdev)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
                 steps = int(t.item())
+        S.kernel_time(dev)  # (the warm-up walks' times: dropped)
         barrier()
         t0 = time.perf_counter()
-        kms, perm = [], None
+        perm = None
         for _ in range(steps):
-            perm, k_ms = step()
-            kms.append(k_ms)
+            perm, _ = step()
         barrier()
         elapsed = time.perf_counter() - t0
+        k_total, k_n = S.kernel_time(dev)  # the timed walks' HIP-event times (walk stream)
+        assert k_n == steps, (k_n, steps)
         st = call.stats()
         if use_pg:
             t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        return elapsed, perm, sum(kms) / len(kms), st, prep["compile_ms"], steps
+        return elapsed, perm, k_total / k_n, st, prep["compile_ms"], steps
 
     walk_names = {0: "dense", 1: "prefix-blocked", 2: "skipper", 3: "segmented (pattern-specialised)",
                   4: "dense, X in LDS"}

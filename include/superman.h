@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SUP_ABI_VERSION 9  /* 9: sup_device_warmup, sup_opts.use_rccl = -1 (round 6); 8: sup_device_checks (round 5); 7: sup_rccl_devices, sup_stats.seg_cached_bits / seg_pair_bits */
+#define SUP_ABI_VERSION 10  /* 10: sup_opts.timing, sup_kernel_time (round 6); 9: sup_device_warmup, sup_opts.use_rccl = -1 (round 6); 8: sup_device_checks (round 5); 7: sup_rccl_devices, sup_stats.seg_cached_bits / seg_pair_bits */
 
 /* ---- error codes ------------------------------------------------------ */
 #define SUP_OK            0
@@ -117,6 +117,11 @@ typedef struct {
                       /*  walking them, so an interrupted run resumes; the result is bit-    */
                       /*  identical to an uninterrupted one.  A mismatching header is         */
                       /*  SUP_EINVAL.  (ABI version 6)                                        */
+  int timing;         /* sup_perman_shard: 1 (default) sup_stats.kernel_ms of the call (it waits */
+                      /*  for the walk's end event); 0: the walk's HIP events are recorded but */
+                      /*  read later by sup_kernel_time (kernel_ms 0) — the call returns as   */
+                      /*  soon as its result is there (~8 us sooner on a 0.5 ms walk).        */
+                      /*  (ABI version 10)                                                    */
 } sup_opts;
 
 typedef struct {
@@ -165,6 +170,12 @@ uint64_t    sup_device_checks(void);
  * caller can run it on a thread beside its planning (the perman CLI does).
  * Thread-safe; a later call on the same devices returns at once. */
 int         sup_device_warmup(int device_id, int gpu_num, int n);
+/* The walk-kernel times (HIP events on the walk's stream) of this thread's
+ * sup_perman_shard calls on logical device `device_id` made with
+ * sup_opts.timing = 0 since the last sup_kernel_time: waits for them, returns
+ * their sum (*total_ms) and count (*launches), and starts a new tally.  Any
+ * pointer may be NULL (the tally is still reset). */
+int         sup_kernel_time(int device_id, double* total_ms, uint64_t* launches);
 
 /* ------------------------------------------------------------------------ *
  * Generic entry point.  `mat` is n x n row-major of type `t` (already

@@ -231,10 +231,13 @@ class ShardCall:
     kernel ms); stats() -> the last call's sup_stats."""
 
     def __init__(self, mat, shard: int, nshards: int, kernel: str = "dense", device_id: int = 0, jit: int = 0,
-                 walk_log2: int = 0):
+                 walk_log2: int = 0, timing: bool = True):
         self._a, dt, n = _mat(mat)
         self._lib = _lib.load()
         self._o = _opts(device_id=device_id, jit=jit, walk_log2=walk_log2)
+        # timing=False: the walk's HIP events are read later by kernel_time()
+        # (the call returns as soon as its result is there; kernel ms 0)
+        self._o.timing = int(bool(timing))
         self._out, self._st = C.c_double(0.0), SupStats()
         self._fn = self._lib.sup_perman_shard
         self._args = (self._a.ctypes.data, dt, n, _KERNELS[kernel], int(shard), int(nshards), C.byref(self._o),
@@ -248,6 +251,16 @@ class ShardCall:
 
     def stats(self) -> dict:
         return self._st.as_dict()
+
+
+def kernel_time(device_id: int = 0):
+    """(total ms, launches) of this thread's walk kernels on `device_id` since
+    the last call, from ShardCall(..., timing=False) calls (sup_kernel_time:
+    their HIP events, read now)."""
+    lib = _lib.load()
+    ms, cnt = C.c_double(0.0), C.c_uint64(0)
+    _lib.check(lib.sup_kernel_time(int(device_id), C.byref(ms), C.byref(cnt)), "kernel_time")
+    return ms.value, cnt.value
 
 
 def plan_info(mat, kernel: str = "dense", jit: int = 0, gpu_num: int = 1, device_id: int = 0,

@@ -32,7 +32,7 @@ SCHED_SINGLE, SCHED_STATIC, SCHED_CHUNKS, SCHED_MANUAL = 0, 1, 2, 3
 
 # Every symbol include/superman.h declares (checked by tests/test_capi.py).
 EXPORTS = [
-    "sup_opts_init", "sup_abi_version", "sup_last_error", "sup_device_count", "sup_rccl_devices", "sup_device_checks", "sup_device_warmup",
+    "sup_opts_init", "sup_abi_version", "sup_last_error", "sup_device_count", "sup_rccl_devices", "sup_device_checks", "sup_device_warmup", "sup_kernel_time",
     "sup_perman", "sup_partial", "sup_perman_cpu", "sup_nw_start", "sup_perman_shard", "sup_plan_info",
     "sup_prepare", "sup_plan_key", "sup_perman_exact", "sup_perman_reduced_exact", "sup_perman_quad",
     "sup_perman_reduced_quad",
@@ -57,7 +57,7 @@ class SupOpts(C.Structure):
         ("gpu_num", C.c_int), ("device_id", C.c_int), ("threads", C.c_int),
         ("cpu_worker", C.c_int), ("grid_dim", C.c_int), ("block_dim", C.c_int),
         ("walk_log2", C.c_int), ("chunk_log2", C.c_int), ("use_rccl", C.c_int),
-        ("verbose", C.c_int), ("jit", C.c_int), ("checkpoint", C.c_char_p),
+        ("verbose", C.c_int), ("jit", C.c_int), ("checkpoint", C.c_char_p), ("timing", C.c_int),
     ]
 
 
@@ -130,7 +130,7 @@ def load() -> C.CDLL:
             build()
         lib = C.CDLL(LIB_PATH)
         _declare(lib)
-        if lib.sup_abi_version() != 9:
+        if lib.sup_abi_version() != 10:
             raise RuntimeError("libsuperman_hip.so ABI version mismatch")
         _lib = lib
         return lib
@@ -146,6 +146,8 @@ def _declare(lib: C.CDLL) -> None:
     lib.sup_rccl_devices.argtypes = [I, C.POINTER(I)]
     lib.sup_device_checks.restype = C.c_uint64
     lib.sup_device_warmup.argtypes = [I, I, I]
+    lib.sup_kernel_time.restype = I
+    lib.sup_kernel_time.argtypes = [I, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     lib.sup_perman.argtypes = [P, I, I, I, I, C.POINTER(SupOpts), C.POINTER(D), C.POINTER(SupStats)]
     lib.sup_partial.argtypes = [P, I, I, I, C.c_uint64, C.c_uint64, C.POINTER(SupOpts), C.POINTER(D),
                                 C.POINTER(SupStats)]

@@ -83,6 +83,7 @@ void sup_opts_init(sup_opts* o) {
   o->device_id = 0;
   o->threads = 16;  // main.cu:333
   o->block_dim = 256;
+  o->timing = 1;
 }
 
 int sup_abi_version(void) { return SUP_ABI_VERSION; }
@@ -95,6 +96,10 @@ uint64_t sup_device_checks(void) { return device_checks_passed(); }
 int sup_device_warmup(int device_id, int gpu_num, int n) {
   if (device_id < 0 || gpu_num < 1) return SUP_EINVAL;
   return warm_devices(device_id, gpu_num, n);
+}
+int sup_kernel_time(int device_id, double* total_ms, uint64_t* launches) {
+  if (device_id < 0) return SUP_EINVAL;
+  return kernel_time(device_id, total_ms, launches);
 }
 int sup_rccl_devices(int ndev, int* phys) {
   if (ndev < 1 || ndev > 1024 || !phys) return SUP_EINVAL;
@@ -239,6 +244,10 @@ int sup_perman_shard(const void* mat, sup_dtype t, int n, sup_kernel kernel, int
   const uint64_t C = P.lay.chunks();
   const uint64_t c0 = C * (uint64_t)shard / (uint64_t)nshards, c1 = C * (uint64_t)(shard + 1) / (uint64_t)nshards;
   SchedResult r;
+  struct DeferTiming {  // sup_opts.timing = 0: this call's walk time is read by sup_kernel_time
+    explicit DeferTiming(bool on) { set_defer_timing(on); }
+    ~DeferTiming() { set_defer_timing(false); }
+  } defer(o.timing == 0);
   if ((rc = schedule(P, SUP_SCHED_SINGLE, o, c0, c1, r))) return rc;
   *out = r.total;
   const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -1011,6 +1011,11 @@ struct DeviceCtx {
   int cus = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // deferred walk timing (set_defer_timing): event pairs recorded around walks
+  // whose times are read later (kernel_time), and the pairs free for reuse
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending, ev_free;
+  double deferred_ms = 0.0;
+  uint64_t deferred_n = 0;
   double* d_cols = nullptr;
   size_t cols_cap = 0;
   double* d_jtab = nullptr;
@@ -1065,6 +1070,13 @@ static std::vector<std::unique_ptr<DeviceCtx>> g_ctx;  // [logical device * kCtx
 static thread_local int t_ctx_lane = 0;
 void set_ctx_lane(int lane) { t_ctx_lane = std::max(0, std::min(kCtxLanes - 1, lane)); }
 int ctx_lane() { return t_ctx_lane; }
+
+// Deferred walk timing (sup_opts.timing = 0, sup_perman_shard): run_range
+// records its walk's HIP events as usual but does not wait for the end event
+// — the call returns once its result is there, while the kernel's last waves
+// may still be exiting — and kernel_time reads the deferred pairs later.
+static thread_local bool t_defer_timing = false;
+void set_defer_timing(bool on) { t_defer_timing = on; }
 
 // Logical devices.  Every device id of the API (sup_opts::device_id, the
 // devices of a multi-device schedule) is a logical id; SUP_DEVICE_MAP (a
@@ -1221,6 +1233,30 @@ int warm_devices(int first, int count, int n) {
         SUP_HIP(walk_occupancy(k, n, &b));
       }
   }
+  return SUP_OK;
+}
+
+// The deferred walk times of the calling thread's context on logical device
+// `dev` since the last read: waits for their end events, returns their sum
+// and count, and starts a new tally.
+int kernel_time(int dev, double* total_ms, uint64_t* launches) {
+  DeviceCtx* c = nullptr;
+  if (int rc = get_ctx(dev, &c)) return rc;
+  std::lock_guard<std::mutex> g(c->mu);
+  SUP_HIP(select_device(c->dev));
+  for (auto& ev : c->ev_pending) {
+    SUP_HIP(hipEventSynchronize(ev.second));
+    float m = 0.f;
+    SUP_HIP(hipEventElapsedTime(&m, ev.first, ev.second));
+    c->deferred_ms += m;
+    ++c->deferred_n;
+    c->ev_free.push_back(ev);
+  }
+  c->ev_pending.clear();
+  if (total_ms) *total_ms = c->deferred_ms;
+  if (launches) *launches = c->deferred_n;
+  c->deferred_ms = 0.0;
+  c->deferred_n = 0;
   return SUP_OK;
 }
 
@@ -1439,8 +1475,21 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
     p.fold_seq = seq;
   }
 
+  hipEvent_t e0 = c->ev0, e1 = c->ev1;
+  const bool defer = t_defer_timing;
+  if (defer) {
+    if (c->ev_free.empty()) {
+      std::pair<hipEvent_t, hipEvent_t> ev;
+      SUP_HIP(hipEventCreate(&ev.first));
+      SUP_HIP(hipEventCreate(&ev.second));
+      c->ev_free.push_back(ev);
+    }
+    std::tie(e0, e1) = c->ev_free.back();
+    c->ev_free.pop_back();
+    c->ev_pending.emplace_back(e0, e1);
+  }
   SUP_ON_DEVICE(c->dev, "walk launch");
-  SUP_HIP(hipEventRecord(c->ev0, s));
+  SUP_HIP(hipEventRecord(e0, s));
   if (seg) {
     if ((rc = jit_launch(c->phys, P, p, (int)grid, s))) return rc;
   } else if (P.lds) {
@@ -1448,7 +1497,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   } else {
     SUP_HIP(launch_walk(P.kind, P.n, p, (int)grid, s));
   }
-  SUP_HIP(hipEventRecord(c->ev1, s));
+  SUP_HIP(hipEventRecord(e1, s));
   unsigned long long* vsum = reinterpret_cast<unsigned long long*>(c->h_result + 2);
   if (fused) {
     if (!to_host) {
@@ -1499,10 +1548,24 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   }
 
   float ms = 0.f;
-  hipError_t ee = hipEventElapsedTime(&ms, c->ev0, c->ev1);
-  if (ee == hipErrorNotReady) {  // (after a flag wait the walk is done; its event may not show it yet)
-    SUP_HIP(hipEventSynchronize(c->ev1));
-    ee = hipEventElapsedTime(&ms, c->ev0, c->ev1);
+  // (after a flag wait the walk's result is there, but its end event may not
+  // be: waiting for it costs ~8 us per call on config 2 — deferred timing
+  // leaves it for kernel_time)
+  hipError_t ee = defer ? hipSuccess : hipEventElapsedTime(&ms, e0, e1);
+  if (ee == hipErrorNotReady) {
+    SUP_HIP(hipEventSynchronize(e1));
+    ee = hipEventElapsedTime(&ms, e0, e1);
+  }
+  if (defer && c->ev_pending.size() >= 256) {  // bound the pending pairs: read the finished ones
+    size_t k = 0;
+    for (; k < c->ev_pending.size() && hipEventQuery(c->ev_pending[k].second) == hipSuccess; ++k) {
+      float m = 0.f;
+      SUP_HIP(hipEventElapsedTime(&m, c->ev_pending[k].first, c->ev_pending[k].second));
+      c->deferred_ms += m;
+      ++c->deferred_n;
+      c->ev_free.push_back(c->ev_pending[k]);
+    }
+    c->ev_pending.erase(c->ev_pending.begin(), c->ev_pending.begin() + (long)k);
   }
   if (ee != hipSuccess) {
     set_error(std::string("hipEventElapsedTime: ") + hipGetErrorString(ee));

@@ -290,6 +290,10 @@ int device_count(int* n);
 constexpr int kCtxLanes = 8;
 void set_ctx_lane(int lane);
 int ctx_lane();
+// Deferred walk timing for the calling thread (sup_opts.timing = 0): run_range
+// records the walk's events without waiting for them; kernel_time reads them.
+void set_defer_timing(bool on);
+int kernel_time(int dev, double* total_ms, uint64_t* launches);
 int phys_device(int dev);  // logical -> physical (SUP_DEVICE_MAP; identity when unset)
 // Select logical device `dev` (physical phys_device(dev)) on this thread:
 // hipSetDevice plus a thread-local note of the logical id, which

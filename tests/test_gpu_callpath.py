@@ -63,3 +63,31 @@ def test_call_path_legs_bit_identical():
     assert ref[0][0] != ref[1][0]
     # calls on one matrix with one walk agree among themselves
     assert ref[0][0] == ref[4][0] and ref[1][0] == ref[5][0]
+
+
+def test_deferred_kernel_time():
+    """sup_opts.timing = 0 (the bench's timed steps): the call returns once its
+    result is there and leaves its walk's HIP events to sup_kernel_time — the
+    same bits, one deferred time per call, each close to the per-call time."""
+    import superman_amd as S
+
+    a = S.read_matrix(os.path.join(ROOT, "tests", "fixtures", "double__32_0.50_0"))[0]
+    S.prepare(a, "dense", jit=1)
+    eager = S.ShardCall(a, 0, 1, kernel="dense", jit=1)
+    lazy = S.ShardCall(a, 0, 1, kernel="dense", jit=1, timing=False)
+    S.kernel_time(0)
+    ref, k_ref = [], []
+    for _ in range(5):
+        v, k = eager()
+        ref.append(v)
+        k_ref.append(k)
+    assert S.kernel_time(0) == (0.0, 0)  # eager calls leave nothing deferred
+    got = []
+    for _ in range(300):  # past the 256 pending pairs the call reads the finished ones itself
+        v, k = lazy()
+        assert k == 0.0
+        got.append(v)
+    total, n = S.kernel_time(0)
+    assert n == 300 and set(got) == set(ref) and len(set(ref)) == 1
+    assert 0.5 * min(k_ref) < total / n < 2.0 * max(k_ref)
+    assert S.kernel_time(0) == (0.0, 0)
