@@ -399,6 +399,38 @@ __device__ __forceinline__ void chunk_store(uint64_t a0, uint32_t len, double ke
       if (groups == 1) break;  // the root
       if (lane == 0) fold_publish(lv + g, s);
       fold_drain();
+      if (cv == count && groups <= 1024u) {
+        // Up to 1024 level-1 groups: one counter for all of them, and the wave
+        // completing the last one forms every upper level itself (level 2:
+        // 64-groups of the level-1 values, zero past their end; level 3: the
+        // <= 16 level-2 values) — the same tree in three memory round trips
+        // instead of six at the walk's very end.
+        unsigned int* top = cnt + groups;  // (where the level-2 counters would be)
+        uint32_t o2 = 0;
+        if (lane == 0) o2 = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        o2 = __builtin_amdgcn_readfirstlane(o2);
+        if (o2 + 1u != (uint32_t)groups) return;
+        if (lane == 0) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t g2 = (uint32_t)((groups + 63u) >> 6);  // <= 16
+        double v[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16u; ++k) {  // every fetch first
+          const uint64_t i = 64u * k + lane;
+          v[k] = (k < g2 && i < groups) ? fold_fetch(lv + i) : 0.0;
+        }
+        double y = 0.0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16u; ++k)
+          if (k < g2) {
+            double x2 = v[k];
+            for (uint32_t o = 1; o < 64u; o <<= 1) x2 += __shfl_xor(x2, o, 64);
+            y = lane == k ? x2 : y;
+          }
+        if (g2 > 1u)
+          for (uint32_t o = 1; o < 64u; o <<= 1) y += __shfl_xor(y, o, 64);
+        s = __shfl(y, 0, 64);
+        break;
+      }
       src = lv;
       lv += groups;
       cnt += groups;
