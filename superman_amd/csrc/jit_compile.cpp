@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 #include <sched.h>
+#include <signal.h>
 #include <spawn.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
@@ -254,6 +255,10 @@ std::string hiprtc_library() {
 
 }  // namespace
 
+// A helper compile that runs longer than this is abandoned (a candidate's
+// compile takes 0.2-2.5 s on the bench matrices).
+constexpr int kHelperLimitS = 300;
+
 size_t rtc_procs() {
   if (const char* e = std::getenv("SUP_RTC_PROCS")) return (size_t)std::max(0, std::atoi(e));
   if (g_jit_failed.load() || std::getenv("SUP_JIT_FAIL")) return 0;
@@ -300,10 +305,27 @@ void prefetch_compiles(const std::vector<const Plan*>& plans, size_t procs) {
         argv.push_back(nullptr);
         pid_t pid = 0;
         if (posix_spawn(&pid, helper.c_str(), nullptr, nullptr, argv.data(), environ) != 0) continue;
+        // a helper that has not finished in kHelperLimitS is killed: its
+        // candidate is then compiled in process if the search reaches it
         int status = 0;
-        while (::waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+        const auto t_spawn = std::chrono::steady_clock::now();
+        bool done = false;
+        for (;;) {
+          const pid_t w = ::waitpid(pid, &status, WNOHANG);
+          if (w == pid) {
+            done = true;
+            break;
+          }
+          if (w < 0 && errno != EINTR) break;
+          if (std::chrono::steady_clock::now() - t_spawn > std::chrono::seconds(kHelperLimitS)) {
+            ::kill(pid, SIGKILL);
+            while (::waitpid(pid, &status, 0) < 0 && errno == EINTR) {
+            }
+            break;
+          }
+          ::usleep(1000);
         }
-        if (!WIFEXITED(status) || WEXITSTATUS(status) != 0) continue;
+        if (!done || !WIFEXITED(status) || WEXITSTATUS(status) != 0) continue;
         auto co = std::make_shared<std::vector<char>>();
         if (!read_file(dir + "/" + name + ".co", *co)) continue;
         {
