@@ -1020,6 +1020,8 @@ struct DeviceCtx {
   size_t cols_cap = 0;
   double* d_jtab = nullptr;
   size_t jtab_cap = 0;
+  double* d_start = nullptr;  // the segmented walk's start table (Plan::start_tab)
+  size_t start_cap = 0;
   double* d_x0 = nullptr;
   int* d_nblk = nullptr;
   uint64_t* d_rowmask = nullptr;
@@ -1342,14 +1344,21 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
 
   const bool seg = P.kind == kWalkSeg;
   if (seg && (rc = ensure(c->d_jtab, c->jtab_cap, P.jtab.size()))) return rc;
+  const bool stab = seg && !P.start_tab.empty();
+  const double* start_before = c->d_start;
+  if (stab && (rc = ensure(c->d_start, c->start_cap, P.start_tab.size()))) return rc;
 
   hipStream_t s = c->stream;
   // the plan's tables: uploaded unless this device already holds them (same
   // cached plan, buffers not reallocated) — repeated calls on one matrix
   // (bench steps, -p6 items, reduction leaves) skip five H2D copies
-  if (P.uid == 0 || P.uid != c->tables_uid || c->d_cols != cols_before || c->d_jtab != jtab_before) {
+  if (P.uid == 0 || P.uid != c->tables_uid || c->d_cols != cols_before || c->d_jtab != jtab_before ||
+      c->d_start != start_before) {
     if (seg)
       SUP_HIP(hipMemcpyAsync(c->d_jtab, P.jtab.data(), P.jtab.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    if (stab)
+      SUP_HIP(hipMemcpyAsync(c->d_start, P.start_tab.data(), P.start_tab.size() * sizeof(double),
+                             hipMemcpyHostToDevice, s));
     SUP_HIP(hipMemcpyAsync(c->d_cols, P.cols.data(), P.cols.size() * sizeof(double), hipMemcpyHostToDevice, s));
     SUP_HIP(hipMemcpyAsync(c->d_x0, P.x0.data(), P.x0.size() * sizeof(double), hipMemcpyHostToDevice, s));
     SUP_HIP(hipMemcpyAsync(c->d_nblk, P.nblk.data(), P.nblk.size() * sizeof(int), hipMemcpyHostToDevice, s));
@@ -1443,6 +1452,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   p.tail_begin = tail_begin;
   p.tail_ticket = tail_group ? (unsigned)(tail_begin / group) : 0xffffffffu;
   p.jtab = seg ? c->d_jtab : nullptr;
+  p.start_tab = stab ? c->d_start : nullptr;
   p.nb_lo = p.nb_hi = 0;
   for (int k = 0; k < P.lay.m && k < 32; ++k) {
     const uint64_t v = (uint64_t)(P.nblk[P.lay.L + k] & 15);

@@ -107,6 +107,12 @@ struct Plan {
   std::vector<double> jtab;        // packed touched values: + block, - block (each padded to 8); then,
                                    // from seg_cbase, the row-copy constants (jit.cpp Gen::tail)
   size_t seg_cbase = 0;
+  // Segmented walk: every wave-chunk's start state without the lane columns
+  // (x0 + the chunk bits' columns, added on the host in chunk_start's order:
+  // the same values), read by the kernel instead of formed (walk_common.hpp
+  // chunk_start_tab) when the table is at most kStartTabMaxBytes.
+  bool start_tab_on = false;
+  std::vector<double> start_tab;   // chunks x NP
   int seg_kp = 4;                  // SGPR pieces (8 doubles) pinned per step region of the generated code
   std::string jit_src;             // generated HIP source of the specialised kernel
   uint64_t jit_key = 0;            // hash of jit_src + compile options

@@ -1553,7 +1553,7 @@ struct Gen {
     o << "      const uint64_t ga = p.chunk_begin + a;\n";
     o << "      double x[N], y[" << len0 << "];\n";
     if (trace) o << "      const uint64_t tr_s = __builtin_amdgcn_s_memtime();\n";
-    o << "      chunk_start<N>(x, p, ga, SUP_LANE());\n";
+    o << "      chunk_start" << (P.start_tab_on ? "_tab" : "") << "<N>(x, p, ga, SUP_LANE());\n";
     o << "      {\n";  // y = x + a_0 on segment 0 (the + block of walk bit 0) = y^0
     o << "        cjdbl8* cv = (cjdbl8*)opaque_c(p.jtab, " << off_const(0, 0) << ");\n";
     for (int r = 0; r < len0; ++r) o << "        y[" << r << "] = x[" << r << "] + cv[" << r / 8 << "][" << r % 8 << "];\n";
@@ -1752,6 +1752,35 @@ uint64_t jit_source_key(const std::string& src) {
 
 }  // namespace
 
+// Start tables up to this size (bytes): config 2's 2^14 chunks x 32 rows are
+// 4 MB, the n = 40 bench matrix's 2^20 chunks would be 335 MB (formed on the
+// device instead).  Measured on config 2: the chunk starts without their
+// chunk-bit column adds take 2.2 % off the walk (an upper bound: the table
+// row's scalar loads remain).
+constexpr size_t kStartTabMaxBytes = 16u << 20;
+
+// Plan::start_tab: chunk ga's start state without the lane columns — x0, then
+// the columns of the set bits of gray(ga) in ascending order, each added to
+// rows [0, n): chunk_start's own additions in its order (IEEE adds, so the
+// same values the device would form).
+static void seg_start_table(Plan& P) {
+  const int n = P.n, NP = P.NP;
+  const uint64_t C = P.lay.chunks();
+  const unsigned hb = (unsigned)(P.lay.L + P.lay.m);
+  P.start_tab.assign((size_t)C * NP, 0.0);
+  const size_t blocks = (size_t)std::min<uint64_t>(C, 64);
+  parallel_tasks(blocks, [&](size_t b) {
+    for (uint64_t ga = C * b / blocks; ga < C * (b + 1) / blocks; ++ga) {
+      double* x = P.start_tab.data() + (size_t)ga * NP;
+      for (int j = 0; j < NP; ++j) x[j] = P.x0[j];
+      for (uint64_t h = ga ^ (ga >> 1); h; h &= h - 1) {
+        const double* col = P.cols.data() + (size_t)(2u * (hb + (unsigned)__builtin_ctzll(h))) * NP;
+        for (int j = 0; j < n; ++j) x[j] += col[j];
+      }
+    }
+  });
+}
+
 int build_seg(Plan& P, int fixed_budget) {
   const int n = P.n, L = P.lay.L, m = P.lay.m;
   if (m < 3) {
@@ -1759,6 +1788,11 @@ int build_seg(Plan& P, int fixed_budget) {
     return SUP_EINVAL;
   }
   if (P.cols.empty()) return SUP_EINVAL;
+  // the start table (chunk_start_tab): decided before any source is generated,
+  // built once the plan is chosen (the ladder's candidates are copies of P)
+  P.start_tab.clear();
+  P.start_tab_on = !std::getenv("SUP_JIT_NO_START_TAB") &&
+                   (double)P.lay.chunks() * P.NP * sizeof(double) <= (double)kStartTabMaxBytes;
   // rows are in first-touch order already: rebuild the shape in engine rows
   P.touched.assign(m, {});
   P.seg_start.assign(1, 0);
@@ -2050,6 +2084,7 @@ int build_seg(Plan& P, int fixed_budget) {
     P = std::move(cand[best]);
   }
   P.seg_skip = seg_skip_fraction_plan(P, 2048);
+  if (P.start_tab_on) seg_start_table(P);
   if (std::getenv("SUP_JIT_VERBOSE"))
     std::fprintf(stderr, "seg plan n=%d m=%d b=%d ops/step=%.4f regs=%d cc=%d table=%zu B (columns %zu B) key=%016llx "
                  "(storage plans evaluated: %ld)\n", n, m, P.seg_b, P.seg_ops, P.seg_regs, P.seg_cc,

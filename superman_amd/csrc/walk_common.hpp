@@ -315,6 +315,20 @@ __device__ __forceinline__ T karg_at(uint32_t offset) {
 }
 #define SUP_KARG(field) karg_at<decltype(WalkParams::field)>((uint32_t)__builtin_offsetof(WalkParams, field))
 
+// chunk_start with the chunk bits' part read from the plan's start table
+// (Plan::start_tab: x0 + those columns, added on the host in chunk_start's
+// order, so the same values): one scalar-loaded row instead of popcount(gray
+// ga) column adds; the lane columns are added here as chunk_start adds them.
+template <int N>
+__device__ __forceinline__ void chunk_start_tab(double (&x)[N], const WalkParams& p, uint64_t ga, uint32_t lane) {
+  constexpr int NP = pad8(N);
+  cdbl* t = opaque_c(SUP_KARG(start_tab), (uint32_t)ga * (uint32_t)(NP * 8));
+#pragma unroll
+  for (int j = 0; j < N; ++j) x[j] = t[j];
+  for (int e = 0; e < p.L; ++e)
+    add_col_masked<N>(x, opaque_c(p.cols, (2u * e) * NP * 8u), (lane >> e) & 1u);
+}
+
 // ------------------------------------------------------------ the fused fold --
 // A value handed to another wave (any CU, any XCD: the XCDs' L2s are not
 // coherent) goes through 8-byte agent-scope atomics on both sides, which are

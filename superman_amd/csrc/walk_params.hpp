@@ -71,6 +71,9 @@ struct WalkParams {
   unsigned int* fold_flag;
   unsigned int fold_seq;
   unsigned int pad4_;
+  // segmented walk with a start table (Plan::start_tab): chunk ga's start
+  // state without the lane columns at start_tab[ga * NP], or nullptr
+  const double* start_tab;
 };
 
 // Exact path (walk_exact.hip): residues of the walk's terms modulo up to
