@@ -1758,6 +1758,10 @@ uint64_t jit_source_key(const std::string& src) {
 // chunk-bit column adds take 2.2 % off the walk (an upper bound: the table
 // row's scalar loads remain).
 constexpr size_t kStartTabMaxBytes = 16u << 20;
+// ... and for short chunks only: the chunk-bit adds are ~1.6 % of a 2^11-step
+// chunk's ops (config 2: the walk 2 % faster), 0.5 % at 2^15 (config 3: no
+// measurable gain for 5 MB more reads per launch).
+constexpr int kStartTabMaxWalkBits = 12;
 
 // Plan::start_tab: chunk ga's start state without the lane columns — x0, then
 // the columns of the set bits of gray(ga) in ascending order, each added to
@@ -1791,7 +1795,7 @@ int build_seg(Plan& P, int fixed_budget) {
   // the start table (chunk_start_tab): decided before any source is generated,
   // built once the plan is chosen (the ladder's candidates are copies of P)
   P.start_tab.clear();
-  P.start_tab_on = !std::getenv("SUP_JIT_NO_START_TAB") &&
+  P.start_tab_on = !std::getenv("SUP_JIT_NO_START_TAB") && P.lay.m <= kStartTabMaxWalkBits &&
                    (double)P.lay.chunks() * P.NP * sizeof(double) <= (double)kStartTabMaxBytes;
   // rows are in first-touch order already: rebuild the shape in engine rows
   P.touched.assign(m, {});
