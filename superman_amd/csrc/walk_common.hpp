@@ -456,11 +456,22 @@ __device__ __forceinline__ void chunk_store(uint64_t a0, uint32_t len, double ke
   }
   if (lane == 0) {
     double* res = SUP_KARG(fold_out);
-    res[0] = s;
-    if (vacc)
-      ((unsigned long long*)res)[2] = __hip_atomic_exchange(vacc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long* res64 = (unsigned long long*)res;
+    const unsigned long long vis_total =
+        vacc ? __hip_atomic_exchange(vacc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     unsigned int* reset = SUP_KARG(fold_reset);
     if (reset) __hip_atomic_store(reset, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (SUP_KARG(fold_sys)) {  // the result is the signal: visited sum first, drained, then the value
+      if (vacc) {
+        __hip_atomic_store(res64 + 2, vis_total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        fold_drain();
+      }
+      __hip_atomic_store(res64, __builtin_bit_cast(unsigned long long, s), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    res[0] = s;
+    if (vacc) res64[2] = vis_total;
     unsigned int* flag = SUP_KARG(fold_flag);
     if (flag) {
       __threadfence_system();

@@ -70,7 +70,10 @@ struct WalkParams {
   unsigned int* fold_reset;
   unsigned int* fold_flag;
   unsigned int fold_seq;
-  unsigned int pad4_;
+  // 1: the final fold publishes the result (and the visited sum before it)
+  // with system-scope stores and no flag: the host waits for the result slot
+  // to leave the sentinel it wrote (run_range); 0: result, fence, flag
+  unsigned int fold_sys;
   // segmented walk with a start table (Plan::start_tab): chunk ga's start
   // state without the lane columns at start_tab[ga * NP], or nullptr
   const double* start_tab;
