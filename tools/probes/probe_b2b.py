@@ -5,6 +5,8 @@ import os
 import sys
 import time
 
+if os.environ.get("PROBE_IMPORT_TORCH"):  # as bench.py: torch (and its HIP runtime) loaded first
+    import torch  # noqa: F401
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import superman_amd as S  # noqa: E402
@@ -29,5 +31,6 @@ for rnd in range(3):
     wall = (time.perf_counter() - t0) / calls * 1e3
     tot, n = S.kernel_time(0)
     res.append(f"{wall:.4f}/{tot / n:.4f}")
-knobs = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith("SUP_JIT_"))
+knobs = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items())
+                 if k.startswith("SUP_JIT_") or k in ("SUP_RESULT_SYS", "SUP_FOLD", "PROBE_IMPORT_TORCH"))
 print(f"{name} [{knobs or 'default'}] ms per call / kernel: {' '.join(res)}  value {v!r}", flush=True)
