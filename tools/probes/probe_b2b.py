@@ -20,7 +20,7 @@ elif prep == 2:
     a = S.skip_order(a)[0]
 S.prepare(a, kern, jit=1)
 c = S.ShardCall(a, 0, 1, kernel=kern, jit=1, timing=False)
-for _ in range(50):
+for _ in range(min(50, calls)):
     v = c()[0]
 S.kernel_time(0)
 res = []
@@ -32,5 +32,5 @@ for rnd in range(3):
     tot, n = S.kernel_time(0)
     res.append(f"{wall:.4f}/{tot / n:.4f}")
 knobs = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items())
-                 if k.startswith("SUP_JIT_") or k in ("SUP_RESULT_SYS", "SUP_FOLD", "PROBE_IMPORT_TORCH"))
+                 if k.startswith("SUP_JIT_") or k in ("SUP_RESULT_SYS", "SUP_FOLD", "SUP_WALK_TAIL", "PROBE_IMPORT_TORCH"))
 print(f"{name} [{knobs or 'default'}] ms per call / kernel: {' '.join(res)}  value {v!r}", flush=True)
