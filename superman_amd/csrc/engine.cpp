@@ -1431,16 +1431,18 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   while (group > 1 && count / ((uint64_t)group * res_waves) < 32) group >>= 1;
   if (const char* e = std::getenv("SUP_WALK_GROUP"))  // experiments: force the chunk group (power of two <= 64)
     group = std::max(1u, std::min(64u, 1u << (31 - __builtin_clz((unsigned)std::max(1, std::atoi(e))))));
-  // Segmented walk: the last chunks go out in groups of group / 16 (at least
-  // one chunk), so the waves finish within a chunk or so of each other (a
-  // group of 16 n = 40 chunks is ~5 ms of one wave's time; the headline on one
-  // box: tail groups of 4 174.7-174.9 ms, of 2 174.4-174.5, of 1 174.3-174.5,
-  // profiles/r6/probe_tail_group.log).  The tail phase holds ~2 groups per
-  // resident wave, rounded to whole groups.
+  // Segmented walk: the last chunks go out in quarter groups, so the waves
+  // finish within a quarter group of each other (a group of 16 n = 40 chunks
+  // is ~5 ms of one wave's time).  Smaller tail groups measured 0.25 % faster
+  // on the headline (tail groups of 4 174.7-174.9 ms, of 2 174.4-174.5, of 1
+  // 174.3-174.5, profiles/r6/probe_tail_group.log) but each tail chunk then
+  // costs its own ticket, publish and fold reads: 11.7 -> 16.8 MB of HBM
+  // traffic per launch (pmc_hbm_final4_d050.json), so quarter groups stay.
+  // The tail phase holds ~2 groups per resident wave, rounded to whole groups.
   unsigned tail_group = 0;
   uint64_t tail_begin = count;
   if (seg && group >= 2) {
-    tail_group = std::max(1u, group / 16);
+    tail_group = std::max(1u, group / 4);
     if (const char* e = std::getenv("SUP_WALK_TAIL"))  // experiments: tail group (0 = no tail phase)
       tail_group = std::min(group, (unsigned)std::max(0, std::atoi(e)));
     if (tail_group) {
