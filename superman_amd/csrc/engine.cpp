@@ -1437,7 +1437,7 @@ int run_range(int dev, const Plan& P, uint64_t c0, uint64_t c1, bool want_visite
   // on the headline (tail groups of 4 174.7-174.9 ms, of 2 174.4-174.5, of 1
   // 174.3-174.5, profiles/r6/probe_tail_group.log) but each tail chunk then
   // costs its own ticket, publish and fold reads: 11.7 -> 16.8 MB of HBM
-  // traffic per launch (pmc_hbm_final4_d050.json), so quarter groups stay.
+  // traffic per launch (profiles/r6/tail1_hbm_d050.json), so quarter groups stay.
   // The tail phase holds ~2 groups per resident wave, rounded to whole groups.
   unsigned tail_group = 0;
   uint64_t tail_begin = count;
